@@ -1,0 +1,33 @@
+"""Build libadfl_slq.so in-tree with hipcc for gfx950 (no JIT cache: the .so travels with the repo)."""
+
+import os
+import subprocess
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+SRC_ROOT = os.path.dirname(PKG_DIR)                      # ad-federatedlearning_amd/
+REPO_ROOT = os.path.dirname(SRC_ROOT)
+CSRC = os.path.join(SRC_ROOT, "csrc", "slq_codec.hip")
+INCLUDE = os.path.join(REPO_ROOT, "include")
+LIB_DIR = os.path.join(PKG_DIR, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libadfl_slq.so")
+
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# No fast-math, no FMA contraction, default fp32 denormal handling (IEEE): the codec is bit-exact.
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-Wall"]
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(LIB_DIR, exist_ok=True)
+    header = os.path.join(INCLUDE, "adfl_slq.h")
+    if (not force and os.path.exists(LIB_PATH)
+            and os.path.getmtime(LIB_PATH) >= max(os.path.getmtime(CSRC), os.path.getmtime(header))):
+        return LIB_PATH
+    cmd = [HIPCC, *FLAGS, f"-I{INCLUDE}", "-o", LIB_PATH, CSRC]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    print(build(force=True, verbose=True))

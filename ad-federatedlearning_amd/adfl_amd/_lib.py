@@ -1,0 +1,78 @@
+"""ctypes binding of libadfl_slq.so (the C ABI declared in include/adfl_slq.h).
+
+The product path has no CPU fallback: if the HIP library is missing this module raises at import
+time, and every op checks the status code the library returns.
+"""
+
+import ctypes
+import os
+
+from ._build import LIB_PATH
+
+P = ctypes.c_void_p
+I32 = ctypes.c_int32
+I64 = ctypes.c_int64
+INT = ctypes.c_int
+
+ALIGN_ELEMS = 64     # ADFL_SLQ_ALIGN_ELEMS
+CHUNK_ELEMS = 8192   # ADFL_SLQ_CHUNK_ELEMS
+ABI_VERSION = 1      # ADFL_SLQ_ABI_VERSION
+
+
+class AdflError(RuntimeError):
+    """A non-zero status from libadfl_slq (argument error or HIP launch error)."""
+
+
+class Chunk(ctypes.Structure):
+    """adfl_slq_chunk."""
+    _fields_ = [("start", I64), ("len", I32), ("tensor", I32), ("first_chunk", I32), ("nchunks", I32)]
+
+
+# name -> (restype, argtypes); the complete exported surface of include/adfl_slq.h
+SIGNATURES = {
+    "adfl_slq_abi_version": (INT, []),
+    "adfl_slq_strerror": (ctypes.c_char_p, [INT]),
+    "adfl_slq_workspace_bytes": (I64, []),
+    "adfl_slq_absmax": (INT, [P, I64, P, I64, P]),
+    "adfl_slq_quantize": (INT, [P, I64, INT, P, P, P, P]),
+    "adfl_slq_encode": (INT, [P, I64, INT, P, P, P, I64, P]),
+    "adfl_slq_dequantize": (INT, [P, I64, P, P, P]),
+    "adfl_slq_build_chunks": (I64, [P, P, I32, P, I64]),
+    "adfl_slq_encode_batched": (INT, [P, P, I64, INT, P, P, P, P]),
+    "adfl_slq_dequantize_batched": (INT, [P, P, I64, P, P, P]),
+    "adfl_slq_quantize_int4": (INT, [P, I64, INT, P, P, P, P]),
+    "adfl_slq_encode_int4": (INT, [P, I64, INT, P, P, P, I64, P]),
+    "adfl_slq_dequantize_int4": (INT, [P, I64, P, P, P]),
+    "adfl_pack_int4": (INT, [P, I64, P, P]),
+    "adfl_unpack_int4": (INT, [P, I64, P, P]),
+    "adfl_slq_dequantize_mean": (INT, [P, I64, I32, I64, P, I64, P, P]),
+}
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load the in-tree HIP library once; raise loudly if it was not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"adfl_amd: HIP codec library not found at {LIB_PATH}; "
+                          "build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype, fn.argtypes = res, args
+    if lib.adfl_slq_abi_version() != ABI_VERSION:
+        raise ImportError(f"adfl_amd: ABI mismatch: library {lib.adfl_slq_abi_version()} != {ABI_VERSION}")
+    _lib = lib
+    return lib
+
+
+def check(status: int) -> None:
+    if status != 0:
+        raise AdflError(load().adfl_slq_strerror(status).decode())
+
+
+def workspace_bytes() -> int:
+    return int(load().adfl_slq_workspace_bytes())

@@ -1,0 +1,253 @@
+"""Device-resident SLQ codec ops over the HIP C ABI (include/adfl_slq.h).
+
+Every function here takes and returns CUDA (HIP) tensors, launches on the current stream and never
+synchronises. Semantics are the reference's, bit for bit:
+
+* ``encode``  — ``SLQChannel._quantize_tensor`` (Src/ADFL/Channel/quant.py:97-104)
+* ``decode``  — ``SLQChannel._dequantize_tensor`` (quant.py:107-112)
+* ``encode_batched`` / ``decode_batched`` — the per-tensor loop of ``_quantize_params`` / ``_receive``
+  (quant.py:67-94) as one launch per pass over a whole bucketed state dict
+* ``encode_int4`` / ``decode_int4`` / ``pack_int4`` / ``unpack_int4`` — Src/ADFL/compression.py:35-66
+* ``dequantize_mean`` — the peer mean after the exchange (Examples/ray_ad.py:188)
+
+The same ops are registered as PyTorch custom ops ``torch.ops.adfl.*`` at the bottom of this file.
+"""
+
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import ALIGN_ELEMS, Chunk, check
+
+_TORCH_TYPE_NAMES = {
+    torch.float64: "Double", torch.float16: "Half", torch.bfloat16: "BFloat16", torch.int64: "Long",
+    torch.int32: "Int", torch.int16: "Short", torch.int8: "Char", torch.uint8: "Byte", torch.bool: "Bool",
+    torch.complex64: "ComplexFloat", torch.complex128: "ComplexDouble",
+}
+EMPTY_MAX_MSG = ("max(): Expected reduction dim to be specified for input.numel() == 0. "
+                 "Specify the reduction dim with the 'dim' argument.")
+
+
+def require_quantizable(t: torch.Tensor) -> None:
+    """Raise exactly what the reference raises for a tensor it cannot quantize (quant.py:100-103)."""
+    if t.numel() == 0:
+        raise RuntimeError(EMPTY_MAX_MSG)
+    if t.dtype != torch.float32:
+        name = _TORCH_TYPE_NAMES.get(t.dtype, str(t.dtype).replace("torch.", ""))
+        raise RuntimeError(f"Quantize only works on Float Tensor, got {name}")
+
+
+def _stream(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _dev(t: torch.Tensor, what: str) -> torch.Tensor:
+    """A contiguous, 16-byte aligned device view of t (copying only when it is not already one)."""
+    if not t.is_cuda:
+        raise ValueError(f"adfl_amd.ops: {what} must be a CUDA/HIP device tensor, got {t.device}")
+    if not t.is_contiguous():
+        t = t.contiguous()
+    if t.data_ptr() % 16:
+        t = t.clone()
+    return t
+
+
+def new_workspace(device) -> torch.Tensor:
+    return torch.empty(_lib.workspace_bytes(), dtype=torch.uint8, device=device)
+
+
+# ------------------------------------------------------------------------------------------------
+# flat codec
+# ------------------------------------------------------------------------------------------------
+def encode(x: torch.Tensor, bits: int, *, q: Optional[torch.Tensor] = None, scale: Optional[torch.Tensor] = None,
+           workspace: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """quant.py:97-104 on the device: returns (int8 payload shaped like x, fp32 scale of shape [1])."""
+    require_quantizable(x)
+    x = _dev(x, "x")
+    q = torch.empty(x.shape, dtype=torch.int8, device=x.device) if q is None else q
+    scale = torch.empty(1, dtype=torch.float32, device=x.device) if scale is None else scale
+    ws = new_workspace(x.device) if workspace is None else workspace
+    check(_lib.load().adfl_slq_encode(x.data_ptr(), x.numel(), bits, q.data_ptr(), scale.data_ptr(), ws.data_ptr(),
+                                      ws.numel(), _stream(x.device)))
+    return q, scale
+
+
+def decode(q: torch.Tensor, scale: torch.Tensor, *, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """quant.py:110 ``q.dequantize()`` on the device: fp32(scale * q)."""
+    q = _dev(q, "q")
+    if q.dtype != torch.int8:
+        raise TypeError(f"adfl_amd.ops.decode: payload must be int8, got {q.dtype}")
+    out = torch.empty(q.shape, dtype=torch.float32, device=q.device) if out is None else out
+    check(_lib.load().adfl_slq_dequantize(q.data_ptr(), q.numel(), scale.data_ptr(), out.data_ptr(),
+                                          _stream(q.device)))
+    return out
+
+
+def encode_int4(x: torch.Tensor, bits: int = 4, *, packed: Optional[torch.Tensor] = None,
+                scale: Optional[torch.Tensor] = None,
+                workspace: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """SLQ encode fused with pack_4bit (compression.py:35-48): returns (uint8 [ceil(n/2)], fp32 [1])."""
+    require_quantizable(x)
+    x = _dev(x, "x")
+    n = x.numel()
+    packed = torch.empty((n + 1) // 2, dtype=torch.uint8, device=x.device) if packed is None else packed
+    scale = torch.empty(1, dtype=torch.float32, device=x.device) if scale is None else scale
+    ws = new_workspace(x.device) if workspace is None else workspace
+    check(_lib.load().adfl_slq_encode_int4(x.data_ptr(), n, bits, packed.data_ptr(), scale.data_ptr(),
+                                           ws.data_ptr(), ws.numel(), _stream(x.device)))
+    return packed, scale
+
+
+def decode_int4(packed: torch.Tensor, n: int, scale: torch.Tensor, *,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """unpack_4bit (compression.py:51-66) fused with dequantize: fp32 [n]."""
+    packed = _dev(packed, "packed")
+    out = torch.empty(n, dtype=torch.float32, device=packed.device) if out is None else out
+    check(_lib.load().adfl_slq_dequantize_int4(packed.data_ptr(), n, scale.data_ptr(), out.data_ptr(),
+                                               _stream(packed.device)))
+    return out
+
+
+def pack_int4(q: torch.Tensor) -> torch.Tensor:
+    """compression.py:35-48 ``pack_4bit`` on a device int8 tensor: uint8 [ceil(n/2)]."""
+    q = _dev(q, "q")
+    n = q.numel()
+    packed = torch.empty((n + 1) // 2, dtype=torch.uint8, device=q.device)
+    check(_lib.load().adfl_pack_int4(q.data_ptr(), n, packed.data_ptr(), _stream(q.device)))
+    return packed
+
+
+def unpack_int4(packed: torch.Tensor, shape: Sequence[int]) -> torch.Tensor:
+    """compression.py:51-66 ``unpack_4bit`` on the device: int8 of `shape`."""
+    packed = _dev(packed, "packed")
+    n = int(np.prod(shape)) if len(shape) else 1
+    q = torch.empty(tuple(shape), dtype=torch.int8, device=packed.device)
+    check(_lib.load().adfl_unpack_int4(packed.data_ptr(), n, q.data_ptr(), _stream(packed.device)))
+    return q
+
+
+def dequantize_mean(q_rows: torch.Tensor, scales: torch.Tensor, n: int, *,
+                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Mean over K int8 payload rows (Examples/ray_ad.py:188): q_rows is [K, row_bytes] int8 (row_bytes >= n,
+    16-byte multiple), scales is [K] or [K, stride] fp32 (column 0 used)."""
+    if q_rows.dim() != 2 or q_rows.dtype != torch.int8 or not q_rows.is_contiguous():
+        raise ValueError("dequantize_mean: q_rows must be a contiguous [K, row_bytes] int8 tensor")
+    k, row = q_rows.shape
+    sc = scales.reshape(k, -1)
+    out = torch.empty(n, dtype=torch.float32, device=q_rows.device) if out is None else out
+    check(_lib.load().adfl_slq_dequantize_mean(q_rows.data_ptr(), row, k, n, sc.data_ptr(), sc.stride(0),
+                                               out.data_ptr(), _stream(q_rows.device)))
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
+# bucketed codec (one launch per pass for a whole state dict)
+# ------------------------------------------------------------------------------------------------
+class BucketLayout:
+    """Placement of T tensors in one flat buffer: tensor t at a 64-element-aligned offset, plus the
+    chunk table the bucketed kernels walk (one 256-thread block per <= 8192-element chunk)."""
+
+    def __init__(self, sizes: Sequence[int]):
+        sizes = [int(s) for s in sizes]
+        if not sizes or min(sizes) < 1:
+            raise ValueError("BucketLayout: every tensor needs at least one element")
+        self.sizes = np.asarray(sizes, dtype=np.int64)
+        padded = (self.sizes + ALIGN_ELEMS - 1) // ALIGN_ELEMS * ALIGN_ELEMS
+        self.offsets = np.concatenate([[0], np.cumsum(padded)[:-1]]).astype(np.int64)
+        self.total = int(padded.sum())
+        self.ntensors = len(sizes)
+        lib = _lib.load()
+        off_p, siz_p = self.offsets.ctypes.data, self.sizes.ctypes.data
+        count = lib.adfl_slq_build_chunks(off_p, siz_p, self.ntensors, None, 0)
+        if count < 0:
+            check(int(count))
+        self.chunks = (Chunk * count)()
+        got = lib.adfl_slq_build_chunks(off_p, siz_p, self.ntensors, self.chunks, count)
+        if got != count:
+            check(int(got) if got < 0 else -1)
+        self.nchunks = int(count)
+        self._device_chunks = {}
+
+    def device_chunks(self, device: torch.device) -> torch.Tensor:
+        key = (device.type, device.index)
+        t = self._device_chunks.get(key)
+        if t is None:
+            host = torch.frombuffer(bytearray(bytes(self.chunks)), dtype=torch.uint8)
+            t = host.to(device)
+            self._device_chunks[key] = t
+        return t
+
+
+def encode_batched(flat: torch.Tensor, layout: BucketLayout, bits: int, *, q: Optional[torch.Tensor] = None,
+                   scales: Optional[torch.Tensor] = None,
+                   partials: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Encode every tensor of a bucketed flat fp32 buffer with its own scale (quant.py:74-94)."""
+    if flat.dtype != torch.float32:
+        raise RuntimeError(f"Quantize only works on Float Tensor, got {_TORCH_TYPE_NAMES.get(flat.dtype, flat.dtype)}")
+    flat = _dev(flat, "flat")
+    if flat.numel() < layout.total:
+        raise ValueError("encode_batched: flat buffer smaller than the layout")
+    dev = flat.device
+    q = torch.empty(layout.total, dtype=torch.int8, device=dev) if q is None else q
+    scales = torch.empty(layout.ntensors, dtype=torch.float32, device=dev) if scales is None else scales
+    partials = torch.empty(layout.nchunks, dtype=torch.int32, device=dev) if partials is None else partials
+    check(_lib.load().adfl_slq_encode_batched(flat.data_ptr(), layout.device_chunks(dev).data_ptr(), layout.nchunks,
+                                              bits, q.data_ptr(), scales.data_ptr(), partials.data_ptr(),
+                                              _stream(dev)))
+    return q, scales
+
+
+def decode_batched(q: torch.Tensor, scales: torch.Tensor, layout: BucketLayout, *,
+                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Decode a bucketed int8 payload with per-tensor scales (quant.py:67-71)."""
+    q = _dev(q, "q")
+    dev = q.device
+    out = torch.empty(layout.total, dtype=torch.float32, device=dev) if out is None else out
+    check(_lib.load().adfl_slq_dequantize_batched(q.data_ptr(), layout.device_chunks(dev).data_ptr(),
+                                                  layout.nchunks, scales.data_ptr(), out.data_ptr(), _stream(dev)))
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
+# torch.ops.adfl.* custom ops (device tensors; fake impls for tracing / meta shapes)
+# ------------------------------------------------------------------------------------------------
+@torch.library.custom_op("adfl::slq_encode", mutates_args=())
+def slq_encode_op(x: torch.Tensor, bits: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    return encode(x, bits)
+
+
+@slq_encode_op.register_fake
+def _(x, bits):
+    return x.new_empty(x.shape, dtype=torch.int8), x.new_empty((1,), dtype=torch.float32)
+
+
+@torch.library.custom_op("adfl::slq_decode", mutates_args=())
+def slq_decode_op(q: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
+    return decode(q, scale)
+
+
+@slq_decode_op.register_fake
+def _(q, scale):
+    return q.new_empty(q.shape, dtype=torch.float32)
+
+
+@torch.library.custom_op("adfl::slq_encode_int4", mutates_args=())
+def slq_encode_int4_op(x: torch.Tensor, bits: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    return encode_int4(x, bits)
+
+
+@slq_encode_int4_op.register_fake
+def _(x, bits):
+    return x.new_empty(((x.numel() + 1) // 2,), dtype=torch.uint8), x.new_empty((1,), dtype=torch.float32)
+
+
+@torch.library.custom_op("adfl::slq_decode_int4", mutates_args=())
+def slq_decode_int4_op(packed: torch.Tensor, n: int, scale: torch.Tensor) -> torch.Tensor:
+    return decode_int4(packed, n, scale)
+
+
+@slq_decode_int4_op.register_fake
+def _(packed, n, scale):
+    return packed.new_empty((n,), dtype=torch.float32)

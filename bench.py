@@ -1,0 +1,205 @@
+"""Headline benchmark: device-resident SLQ quantize+dequantize of a 1 GiB fp32 gradient per GPU.
+
+Metric (BASELINE.json): "GiB/s device-resident quantize+dequantize, 1 GiB fp32 grads, 1/2/4/8 GPU".
+One step = one round trip of the hot path over one 1 GiB fp32 buffer already resident in HBM
+(BASELINE.json configs[1], shape [262144, 1024], randn * 1e-3): encode (absmax pass + quantize pass,
+quant.py:97-104) then decode (quant.py:107-112), 3 HIP launches. With N GPUs (torchrun, one process per
+GPU) every rank round-trips its own 1 GiB client update concurrently (weak scaling, no collective in the
+data path); value = N GiB / max-over-ranks time per step.
+
+Also reported on the same line:
+* roofline — the dominant kernel's algorithmic bytes / its average launch time, measured with HIP
+  events on the launch stream inside the timed region, against the 8.0 TB/s HBM3E peak; `traffic` is
+  the PMC-measured HBM bytes per launch from profiles/ when a summary for that kernel exists;
+* cpu_baseline — the reference's ATen op sequence (quant.py:100-103,110) timed on this host's cores
+  (rank 0, N=1), over a bounded sample of the same workload.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "ad-federatedlearning_amd"))
+
+GIB = 1 << 30
+N_ELEMS = 1 << 28                 # 1 GiB of fp32
+SHAPE = (262144, 1024)
+HBM_PEAK_GBS = 8000.0             # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# algorithmic bytes per fp32 element, per kernel
+KERNEL_BYTES = {"absmax": 4, "quantize": 5, "dequantize": 5}
+KERNEL_SYMBOLS = {"absmax": "k_absmax_flat", "quantize": "k_quantize_flat", "dequantize": "k_dequantize_flat"}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--bits", type=int, default=8)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget for the CPU baseline sample")
+    return p.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(v: float, world: int) -> float:
+    if world == 1:
+        return v
+    import torch.distributed as dist
+    t = torch.tensor([v], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch from the committed PMC summary (profiles/pmc_traffic.json), if present."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d["kernels"][KERNEL_SYMBOLS[kernel]]["hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def cpu_baseline(x_dev: torch.Tensor, bits: int, budget_s: float, q_dev: torch.Tensor, s_dev: torch.Tensor):
+    """The reference's own op sequence on host cores, timed on a bounded sample of the workload."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import slq_oracle as oracle  # test infrastructure: the checker / baseline leg only
+
+    threads = torch.get_num_threads()
+    x = x_dev.cpu()
+    # sample: the full 1 GiB buffer, as many round trips as fit the budget (at least one)
+    times, parity = [], None
+    t_start = time.perf_counter()
+    while True:
+        t0 = time.perf_counter()
+        q, scale = oracle.aten_encode(x, bits)
+        d = oracle.aten_decode(q)
+        times.append(time.perf_counter() - t0)
+        if parity is None:  # the GPU result on this very workload must equal the reference's
+            parity = bool(torch.equal(q.int_repr(), q_dev.cpu())) and float(s_dev.item()) == scale
+        del q, d
+        if time.perf_counter() - t_start + min(times) > budget_s or len(times) >= 5:
+            break
+    best = min(times)
+    cpu = {"value": round((x.numel() * 4 / GIB) / best, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+           "sample": f"{len(times)} x full 1 GiB round trip (torch.abs/max/quantize_per_tensor/dequantize, "
+                     f"quant.py:100-110) on {threads} host threads, best-of; {os.cpu_count()} CPUs visible",
+           "ms_per_round_trip": round(best * 1e3, 1)}
+    return cpu, parity
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_setup(args)
+    from adfl_amd import ops
+    from adfl_amd import _lib
+
+    lib = _lib.load()
+    dev = torch.device("cuda", local)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+    g = torch.Generator(device=dev).manual_seed(rank)
+    x = (torch.randn(SHAPE, device=dev, generator=g) * 1e-3).contiguous()
+    n = x.numel()
+    q = torch.empty(SHAPE, dtype=torch.int8, device=dev)
+    scale = torch.empty(1, dtype=torch.float32, device=dev)
+    ws = ops.new_workspace(dev)
+    out = torch.empty(SHAPE, dtype=torch.float32, device=dev)
+    xp, qp, sp, wp, op = x.data_ptr(), q.data_ptr(), scale.data_ptr(), ws.data_ptr(), out.data_ptr()
+    wsb = ws.numel()
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        _lib.check(lib.adfl_slq_absmax(xp, n, wp, wsb, sh))
+        if ev is not None:
+            ev[1].record(stream)
+        _lib.check(lib.adfl_slq_quantize(xp, n, args.bits, wp, qp, sp, sh))
+        if ev is not None:
+            ev[2].record(stream)
+        _lib.check(lib.adfl_slq_dequantize(qp, n, sp, op, sh))
+        if ev is not None:
+            ev[3].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(events[k])
+    torch.cuda.synchronize()
+    barrier(world)
+    elapsed = time.perf_counter() - t0
+    elapsed = max_over_ranks(elapsed, world)
+
+    per_kernel = {name: sum(e[i].elapsed_time(e[i + 1]) for e in events) / args.steps
+                  for i, name in enumerate(("absmax", "quantize", "dequantize"))}
+    ms_per_step = elapsed / args.steps * 1e3
+    gib_per_rank = n * 4 / GIB
+    value = world * gib_per_rank / (elapsed / args.steps)
+
+    if rank != 0:
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
+    dominant = max(per_kernel, key=per_kernel.get)
+    alg_bytes = KERNEL_BYTES[dominant] * n
+    achieved = alg_bytes / (per_kernel[dominant] * 1e-3) / 1e9
+    kernels_ms = sum(per_kernel.values())
+    line = {
+        "metric": "GiB/s device-resident quantize+dequantize, 1 GiB fp32 grads, 1/2/4/8 GPU",
+        "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f32", "data": "synthetic (torch.randn * 1e-3 on device, seed = rank)",
+        "config": {"workload": "C2: 1 GiB fp32 flat gradient [262144,1024] per GPU, SLQ bits=8 encode+decode",
+                   "bits": args.bits, "elements_per_gpu": n, "parallelism": f"independent clients x{world}"},
+        "roofline": {"bound": "hbm", "kernel": KERNEL_SYMBOLS[dominant], "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": pmc_traffic(dominant),
+                     "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": round(per_kernel[dominant], 4)},
+        "kernels_ms": {k: round(v, 4) for k, v in per_kernel.items()},
+        "round_trip_roofline": {"alg_bytes": 14 * n, "kernel_ms": round(kernels_ms, 4),
+                                "achieved_GBs": round(14 * n / (kernels_ms * 1e-3) / 1e9, 1),
+                                "frac": round(14 * n / (kernels_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                "wall_frac": round(14 * n / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+        "cpu_baseline": None,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        cpu, parity = cpu_baseline(x, args.bits, args.cpu_seconds, q, scale)
+        line["cpu_baseline"] = cpu
+        line["parity_vs_reference_ops"] = parity
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,124 @@
+/*
+ * adfl_slq.h — C ABI of the MI355X (gfx950) SLQ gradient codec: libadfl_slq.so.
+ *
+ * Drop-in boundary for ADFL's symmetric-linear-quantization channel. The reference codec is pure
+ * Python over ATen CPU kernels; the entry points below are what its Channel plugin layer
+ * (Src/ADFL/Channel/channel.py:10-45) binds through ctypes — see INTEGRATION.md. Each function names
+ * the reference interface it replaces (file:line under the reference tree).
+ *
+ * Conventions
+ *  - Every pointer named d_* is DEVICE memory (hipMalloc / torch CUDA allocator) on the current device.
+ *    Pointers to fp32 / int8 element data must be 16-byte aligned (torch allocations are); element
+ *    counts are int64 (a 4 GiB gradient overflows 32 bits).
+ *  - `stream` is a hipStream_t passed as void* (NULL = legacy default stream). Every call is
+ *    asynchronous on that stream, never synchronises, allocates nothing and is graph-capturable.
+ *  - Return value: 0 on success; a positive hipError_t from a failed launch; a negative ADFL_E_* code
+ *    for an argument error (nothing is launched then). adfl_slq_strerror() names either kind.
+ *  - Bit-exact semantics (pinned by tests/golden): scale = fp32(absmax / (2^(bits-1)-1)), with absmax =
+ *    max|x| (NaN propagates); inv = fp32(1/scale); q = NaN(x*inv) ? 127 : clamp(rne(fp32(x*inv)),
+ *    -128, 127); dequantized value = fp32(scale * q).
+ */
+#ifndef ADFL_SLQ_H
+#define ADFL_SLQ_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ADFL_SLQ_ABI_VERSION 1
+
+enum {
+  ADFL_OK = 0,
+  ADFL_E_ARG = -1,       /* null pointer, negative count, bad tensor count */
+  ADFL_E_BITS = -2,      /* bits outside [1, 16] */
+  ADFL_E_ALIGN = -3,     /* a data pointer is not 16-byte aligned */
+  ADFL_E_WORKSPACE = -4  /* workspace smaller than adfl_slq_workspace_bytes() */
+};
+
+/* Library / ABI identification. */
+int adfl_slq_abi_version(void);
+const char* adfl_slq_strerror(int status);
+
+/* Bytes of device workspace the flat encode needs (per-block absmax partials). Constant. */
+int64_t adfl_slq_workspace_bytes(void);
+
+/* ---------------------------------------------------------------------------------------------
+ * Flat (single tensor) codec — SLQChannel._quantize_tensor / _dequantize_tensor
+ * (Src/ADFL/Channel/quant.py:97-104 and :107-112). n may be any value >= 1.
+ * ------------------------------------------------------------------------------------------- */
+
+/* Pass 1 of encode: max|x| partials into d_workspace (torch.max(torch.abs(t)), quant.py:100). */
+int adfl_slq_absmax(const float* d_x, int64_t n, void* d_workspace, int64_t workspace_bytes, void* stream);
+
+/* Pass 2 of encode: reduce the partials, scale = absmax/q_max (quant.py:99-100), write d_scale[0],
+ * quantize x into d_q (torch.quantize_per_tensor(t, scale, 0, qint8), quant.py:102-103). */
+int adfl_slq_quantize(const float* d_x, int64_t n, int bits, const void* d_workspace, int8_t* d_q,
+                      float* d_scale, void* stream);
+
+/* absmax + quantize (two launches): the whole of quant.py:97-104. */
+int adfl_slq_encode(const float* d_x, int64_t n, int bits, int8_t* d_q, float* d_scale, void* d_workspace,
+                    int64_t workspace_bytes, void* stream);
+
+/* q.dequantize() (quant.py:110): d_out[i] = d_scale[0] * d_q[i]. */
+int adfl_slq_dequantize(const int8_t* d_q, int64_t n, const float* d_scale, float* d_out, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Bucketed (multi-tensor) codec — SLQChannel._quantize_params / _receive over a whole state dict
+ * (quant.py:74-94, :67-71): one launch per pass for all tensors, per-tensor scales.
+ *
+ * Layout: tensor t owns elements [offset_t, offset_t + size_t) of the flat x / q / out buffers, with
+ * every offset_t a multiple of ADFL_SLQ_ALIGN_ELEMS. The work is described by a chunk table built
+ * on the host by adfl_slq_build_chunks() and copied to the device once per layout.
+ * ------------------------------------------------------------------------------------------- */
+#define ADFL_SLQ_ALIGN_ELEMS 64
+#define ADFL_SLQ_CHUNK_ELEMS 8192
+
+typedef struct adfl_slq_chunk {
+  int64_t start;        /* first element of the chunk in the flat buffer */
+  int32_t len;          /* elements in the chunk, 1..ADFL_SLQ_CHUNK_ELEMS */
+  int32_t tensor;       /* owning tensor index */
+  int32_t first_chunk;  /* index of the owning tensor's first chunk */
+  int32_t nchunks;      /* number of chunks of the owning tensor */
+} adfl_slq_chunk;
+
+/* Host-side: number of chunks for the given sizes (call with chunks == NULL), or fill `chunks`.
+ * Returns the chunk count, or a negative ADFL_E_* code. */
+int64_t adfl_slq_build_chunks(const int64_t* offsets, const int64_t* sizes, int32_t ntensors,
+                              adfl_slq_chunk* chunks, int64_t capacity);
+
+/* d_partials: int64 nchunks * 4 bytes of device scratch. d_scales: ntensors floats. */
+int adfl_slq_encode_batched(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, int bits,
+                            int8_t* d_q, float* d_scales, uint32_t* d_partials, void* stream);
+int adfl_slq_dequantize_batched(const int8_t* d_q, const adfl_slq_chunk* d_chunks, int64_t nchunks,
+                                const float* d_scales, float* d_out, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * int4 packed variant — compression.py pack_4bit / unpack_4bit (Src/ADFL/compression.py:35-66)
+ * fused with SLQ quantize / dequantize. Packed bytes = ceil(n/2); byte j = ((q[2j]+8)<<4) | (q[2j+1]+8)
+ * in int8 wraparound arithmetic (high nibble = even element), a zero element padding odd n.
+ * ------------------------------------------------------------------------------------------- */
+int adfl_slq_quantize_int4(const float* d_x, int64_t n, int bits, const void* d_workspace, uint8_t* d_packed,
+                           float* d_scale, void* stream);
+int adfl_slq_encode_int4(const float* d_x, int64_t n, int bits, uint8_t* d_packed, float* d_scale,
+                         void* d_workspace, int64_t workspace_bytes, void* stream);
+int adfl_slq_dequantize_int4(const uint8_t* d_packed, int64_t n, const float* d_scale, float* d_out,
+                             void* stream);
+int adfl_pack_int4(const int8_t* d_q, int64_t n, uint8_t* d_packed, void* stream);
+int adfl_unpack_int4(const uint8_t* d_packed, int64_t n, int8_t* d_q, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Peer exchange epilogue — the mean over K gathered payloads that follows the all-gather
+ * (Examples/ray_ad.py:188 `torch.stack(updates).mean(0)`, Src/ADFL/model.py:221-234 simple_aggregate):
+ * d_out[i] = (sum_r d_scales[r] * q_r[i]) / K, summed in r order, fp32. The K payloads are rows of one
+ * buffer: q_r = d_q + r * row_stride_bytes.
+ * ------------------------------------------------------------------------------------------- */
+int adfl_slq_dequantize_mean(const int8_t* d_q, int64_t row_stride_bytes, int32_t k, int64_t n,
+                             const float* d_scales, int64_t scale_stride, float* d_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ADFL_SLQ_H */

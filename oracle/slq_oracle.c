@@ -1,0 +1,119 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY. CPU restatement of ADFL's SLQ gradient codec.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library, and only
+ * as the checker. The product path (ad-federatedlearning_amd/) never links or calls it.
+ *
+ * Parity pin: checked against tests/golden/ (vectors produced by executing the reference's
+ * Src/ADFL/Channel/quant.py in place on torch 2.10.0+rocm7.0, quantized engine x86; generator
+ * tests/golden/make_golden.py). The arithmetic itself lives in third-party ATen/fbgemm kernels
+ * (torch 2.10.0, requirements.txt:1 pins no version): torch.max/abs, quantize_per_tensor and
+ * Tensor.dequantize, called at Src/ADFL/Channel/quant.py:100-103,110. This file restates what those
+ * calls compute, as established empirically against that torch build.
+ *
+ * Build: oracle/Makefile (gcc -O2 -ffp-contract=off, no fast-math: SSE scalar fp32 is IEEE).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+/* torch.max(torch.abs(t)) — Src/ADFL/Channel/quant.py:100. NaN propagates (torch.max semantics). */
+float oracle_slq_absmax(const float* x, int64_t n) {
+    float m = 0.0f;
+    for (int64_t i = 0; i < n; ++i) {
+        float a = fabsf(x[i]);
+        if (isnan(a)) return a;
+        if (a > m) m = a;
+    }
+    return m;
+}
+
+/* q_max = 2**(bits-1)-1; scale = fp32(absmax / q_max) — quant.py:99-100 (fp32 tensor / int). */
+float oracle_slq_scale(float absmax, int bits) {
+    int qmax = (1 << (bits - 1)) - 1;
+    return absmax / (float)qmax;
+}
+
+/* torch.quantize_per_tensor(t, scale, 0, qint8) — quant.py:102-103.
+ * Elementwise: inv = fp32(1/scale); y = fp32(x*inv); NaN -> 127; clamp to [-128,127];
+ * round half to even. (Multiply-by-reciprocal, not divide: SURVEY.md §7 "Hard parts".) */
+void oracle_slq_quantize(const float* x, int64_t n, float scale, int8_t* q) {
+    float inv = 1.0f / scale;
+    for (int64_t i = 0; i < n; ++i) {
+        float y = x[i] * inv;
+        if (isnan(y)) { q[i] = 127; continue; }
+        if (y > 127.0f) y = 127.0f;
+        if (y < -128.0f) y = -128.0f;
+        q[i] = (int8_t)nearbyintf(y); /* default FE_TONEAREST = ties to even */
+    }
+}
+
+/* SLQChannel._quantize_tensor (quant.py:97-104): returns the fp32 scale, writes the int8 payload. */
+float oracle_slq_encode(const float* x, int64_t n, int bits, int8_t* q) {
+    float scale = oracle_slq_scale(oracle_slq_absmax(x, n), bits);
+    oracle_slq_quantize(x, n, scale, q);
+    return scale;
+}
+
+/* q.dequantize() — quant.py:110: fp32(scale * float(q)), zero point 0. */
+void oracle_slq_dequantize(const int8_t* q, int64_t n, float scale, float* out) {
+    for (int64_t i = 0; i < n; ++i) out[i] = scale * (float)q[i];
+}
+
+/* Multi-tensor form of SLQChannel._quantize_params (quant.py:74-94) over a flat buffer: tensor t owns
+ * elements [offsets[t], offsets[t] + sizes[t]) of x and of q. */
+void oracle_slq_encode_batched(const float* x, const int64_t* offsets, const int64_t* sizes, int32_t ntensors,
+                               int bits, int8_t* q, float* scales) {
+    for (int32_t t = 0; t < ntensors; ++t)
+        scales[t] = oracle_slq_encode(x + offsets[t], sizes[t], bits, q + offsets[t]);
+}
+
+void oracle_slq_dequantize_batched(const int8_t* q, const int64_t* offsets, const int64_t* sizes, int32_t ntensors,
+                                   const float* scales, float* out) {
+    for (int32_t t = 0; t < ntensors; ++t)
+        oracle_slq_dequantize(q + offsets[t], sizes[t], scales[t], out + offsets[t]);
+}
+
+/* pack_4bit — Src/ADFL/compression.py:35-48. Flatten; pad one 0 if odd; q+8 in int8 arithmetic
+ * (wraps); byte = (hi << 4) | lo with hi = even element, lo = odd element, int8 wraparound, the low
+ * operand NOT masked to a nibble (out-of-range values alias, e.g. 127 packs as nibbles (7,-1)). */
+int64_t oracle_pack_int4(const int8_t* q, int64_t n, uint8_t* packed) {
+    int64_t np = (n + 1) / 2;
+    for (int64_t j = 0; j < np; ++j) {
+        int64_t i0 = 2 * j, i1 = 2 * j + 1;
+        uint8_t hi = (uint8_t)(q[i0] + 8);
+        uint8_t lo = (uint8_t)((i1 < n ? q[i1] : 0) + 8);
+        packed[j] = (uint8_t)((uint8_t)(hi << 4) | lo);
+    }
+    return np;
+}
+
+/* unpack_4bit — Src/ADFL/compression.py:51-66: high = ((b>>4)&0xF)-8, low = (b&0xF)-8, truncated to n. */
+void oracle_unpack_int4(const uint8_t* packed, int64_t n, int8_t* q) {
+    for (int64_t i = 0; i < n; ++i) {
+        uint8_t b = packed[i / 2];
+        q[i] = (int8_t)((i & 1) ? ((b & 0xF) - 8) : (((b >> 4) & 0xF) - 8));
+    }
+}
+
+/* int4 end-to-end as the composition the reference's functions define: dequantize(unpack(pack(q))). */
+void oracle_slq_dequantize_int4(const uint8_t* packed, int64_t n, float scale, float* out) {
+    for (int64_t i = 0; i < n; ++i) {
+        uint8_t b = packed[i / 2];
+        int v = (i & 1) ? ((b & 0xF) - 8) : (((b >> 4) & 0xF) - 8);
+        out[i] = scale * (float)v;
+    }
+}
+
+/* Peer mean of K decoded payloads (Examples/ray_ad.py:188 torch.stack(...).mean(0)): fp32 sum in
+ * payload order, then divide by K. */
+void oracle_slq_dequantize_mean(const int8_t* const* qs, const float* scales, int32_t k, int64_t n, float* out) {
+    for (int64_t i = 0; i < n; ++i) {
+        float s = scales[0] * (float)qs[0][i];
+        for (int32_t r = 1; r < k; ++r) s += scales[r] * (float)qs[r][i];
+        out[i] = s / (float)k;
+    }
+}
+
+/* Thread-free helper the tests use for SHA inputs of recipe cases. */
+uint32_t oracle_f32_bits(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }

@@ -1,0 +1,139 @@
+"""GPU: the drop-in Channel surface (SLQChannel / USLQChannel) against the reference's golden output.
+
+Mirrors the reference's own codec test flow (Src/ADFL/Channel/Tests/test_quant.py:126-161: server->client
+and client->server round trips) but asserts values instead of printing them."""
+
+import pickle
+
+import numpy as np
+import pytest
+import torch
+
+import recipes
+from golden_util import manifest, same_f32, same_scale, small
+
+pytestmark = pytest.mark.gpu
+
+adfl_amd = pytest.importorskip("adfl_amd")
+from adfl_amd.Channel import SLQChannel, USLQChannel  # noqa: E402
+from adfl_amd.model import ByteParameters, QuantParameters  # noqa: E402
+
+
+def _golden_dict(names):
+    A = small()
+    return {n: torch.from_numpy(A[n + "__x"].copy()) for n in names}
+
+
+def test_c1_two_client_round_trip_matches_golden():
+    """C1 shape (Examples/ray_async.py:63-70): [10,3072] weight + [10] bias, both directions."""
+    m = {c["name"]: c for c in manifest()["raw"]}
+    A = small()
+    w = torch.from_numpy(A["c1_fc_weight_b8__x"].copy())
+    b = torch.from_numpy(recipes.randn((10,), 31, 1.0))
+    ch = SLQChannel(bits=8)
+    for send, recv in ((ch.on_server_send, ch.on_client_receive), (ch.on_client_send, ch.on_server_receive)):
+        qp, t_enc = send({"fc.weight": w, "fc.bias": b})
+        assert isinstance(qp, QuantParameters) and t_enc > 0
+        p = qp.params["fc.weight"]
+        assert p.data.dtype == torch.qint8 and p.data.device.type == "cpu"
+        assert np.array_equal(p.data.int_repr().numpy(), A["c1_fc_weight_b8__q"])
+        assert isinstance(p.scale, float) and same_scale(p.scale, m["c1_fc_weight_b8"]["scale_bits"])
+        assert p.data.q_scale() == p.scale and p.data.q_zero_point() == 0
+        assert qp.params["fc.bias"].data is b and qp.params["fc.bias"].scale == 1
+        assert qp.size == m["c1_fc_weight_b8"]["size"] + b.nbytes
+        dec, t_dec = recv(qp)
+        assert same_f32(dec["fc.weight"].numpy(), A["c1_fc_weight_b8__deq"])
+        assert dec["fc.weight"].dtype == torch.float32 and dec["fc.weight"].shape == w.shape
+        dec["fc.weight"].add_(1.0)  # owned and writable, as strategies require
+        assert dec["fc.bias"] is b
+
+
+@pytest.mark.parametrize("bits", [8, 4, 2])
+def test_whole_dict_of_golden_cases(bits):
+    """Every small golden case of this bit width in ONE dict -> one bucketed launch per pass."""
+    cases = [c for g in ("raw", "edge") for c in manifest()[g] if c["bits"] == bits]
+    A = small()
+    params = {c["name"]: torch.from_numpy(A[c["name"] + "__x"].copy()) for c in cases}
+    params["bias"] = torch.randn(7)
+    params["num_batches_tracked"] = torch.tensor(3, dtype=torch.int64)
+    ch = SLQChannel(bits=bits)
+    qp, _ = ch.on_client_send(params)
+    dec, _ = ch.on_server_receive(qp)
+    assert list(qp.params) == list(params) and list(dec) == list(params)
+    for c in cases:
+        p = qp.params[c["name"]]
+        assert np.array_equal(p.data.int_repr().numpy(), A[c["name"] + "__q"]), c["name"]
+        assert same_scale(p.scale, c["scale_bits"]), c["name"]
+        assert same_f32(dec[c["name"]].numpy(), A[c["name"] + "__deq"]), c["name"]
+    assert qp.params["num_batches_tracked"].data is params["num_batches_tracked"]
+
+
+def test_passthrough_metadata_matches_reference():
+    g = manifest()["passthrough"]
+    bias = torch.from_numpy(recipes.randn((10,), 31, 1.0))
+    nbt = torch.tensor(7, dtype=torch.int64)
+    ivec = torch.arange(5, dtype=torch.int64)
+    qp, _ = SLQChannel(8).on_client_send({"bias": bias, "num_batches_tracked": nbt, "ivec": ivec})
+    for (name, p), src in zip(qp.params.items(), (bias, nbt, ivec)):
+        ref = g[name]
+        assert (p.data is src) == ref["same_object"]
+        assert p.scale == ref["scale"] and type(p.scale).__name__ == ref["scale_type"]
+        assert str(p.dtype) == ref["dtype"] and str(p.q_dtype) == ref["q_dtype"]
+        assert list(p.shape) == ref["shape"] and p.bits == ref["bits"]
+        assert p.signs.tolist() == ref["signs"] and str(p.signs.dtype) == ref["signs_dtype"]
+    assert qp.size == g["__size__"]
+    meta = manifest()["quant_meta"]
+    w = SLQChannel(8).on_client_send({"w": torch.ones(2, 3)})[0].params["w"]
+    assert str(w.q_dtype) == meta["q_dtype"] and str(w.data.dtype) == meta["data_dtype"]
+    assert w.scale_2 == meta["scale_2"] and type(w.scale).__name__ == meta["scale_type"]
+
+
+def test_uslq_directions():
+    params = {"w": torch.randn(33, 31), "b": torch.randn(31)}
+    ch = USLQChannel(bits=8)
+    bp, t = ch.on_server_send(params)
+    assert isinstance(bp, ByteParameters) and t == 0.0
+    back, _ = ch.on_client_receive(bp)
+    assert torch.equal(back["w"], params["w"])
+    qp, _ = ch.on_client_send(params)
+    assert isinstance(qp, QuantParameters)
+    dec, _ = ch.on_server_receive(qp)
+    assert dec["w"].shape == (33, 31)
+    assert ch.to_json() == manifest()["to_json"]["USLQChannel_4"] | {"bits": 8}
+
+
+def test_device_resident_dict_stays_on_device():
+    dev = torch.device("cuda", 0)
+    x = torch.randn(257, 129, device=dev)
+    qp, _ = SLQChannel(8).on_client_send({"w": x, "cpu_w": x.cpu()})
+    assert qp.params["w"].data.is_cuda and not qp.params["cpu_w"].data.is_cuda
+    assert torch.equal(qp.params["w"].data.int_repr().cpu(), qp.params["cpu_w"].data.int_repr())
+    assert qp.params["w"].scale == qp.params["cpu_w"].scale
+    dec, _ = SLQChannel(8).on_server_receive(qp)
+    assert dec["w"].is_cuda and torch.equal(dec["w"].cpu(), dec["cpu_w"])
+
+
+def test_channel_pickles_without_device_state():
+    ch = SLQChannel(8)
+    SLQChannel(8).on_client_send({"w": torch.randn(4, 4)})  # warm the per-process cache
+    ch2 = pickle.loads(pickle.dumps(ch))
+    assert ch2.bits == 8 and vars(ch2) == {"bits": 8}
+
+
+def test_payload_pickles_compactly():
+    """Ray pickles the payload; each tensor owns its storage (no shared staging buffer rides along)."""
+    qp, _ = SLQChannel(8).on_client_send({"a": torch.randn(64, 64), "b": torch.randn(4096, 16)})
+    blob = pickle.dumps(qp.params["a"])
+    assert len(blob) < 64 * 64 + 2048
+
+
+def test_reference_errors():
+    ch = SLQChannel(8)
+    with pytest.raises(RuntimeError, match="Quantize only works on Float Tensor, got Double"):
+        ch.on_client_send({"w": torch.randn(2, 2, dtype=torch.float64)})
+    with pytest.raises(RuntimeError, match="Quantize only works on Float Tensor, got Long"):
+        ch.on_client_send({"w": torch.ones(2, 2, dtype=torch.int64)})
+    with pytest.raises(RuntimeError, match="numel\\(\\) == 0"):
+        ch.on_client_send({"w": torch.empty(0, 3)})
+    with pytest.raises(AssertionError):
+        ch.on_server_receive(ByteParameters({}, 0))
