@@ -7,6 +7,11 @@ time, and every op checks the status code the library returns.
 import ctypes
 import os
 
+# torch must be loaded first: it brings its own libamdhip64 (SONAME libamdhip64.so.7). Loading our
+# library first would pull in /opt/rocm's copy too, and two HIP runtimes in one process do not share
+# devices, streams or allocations. With torch loaded, our DT_NEEDED resolves to torch's runtime.
+import torch  # noqa: F401
+
 from ._build import LIB_PATH
 
 P = ctypes.c_void_p
@@ -46,6 +51,7 @@ SIGNATURES = {
     "adfl_pack_int4": (INT, [P, I64, P, P]),
     "adfl_unpack_int4": (INT, [P, I64, P, P]),
     "adfl_slq_dequantize_mean": (INT, [P, I64, I32, I64, P, I64, P, P]),
+    "adfl_slq_dequantize_mean_int4": (INT, [P, I64, I32, I64, P, I64, P, P]),
 }
 
 _lib = None

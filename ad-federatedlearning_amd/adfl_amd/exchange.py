@@ -1,0 +1,123 @@
+"""One simulated client per GPU: quantized peer exchange over RCCL (BASELINE configs C4 and C5).
+
+Reference shape: every decentralized peer sends its parameters to every other peer and then averages
+what it holds, ``torch.stack([update.parameters[name] for update in updates]).mean(dim=0)``
+(``Examples/ray_ad.py:164-190``; ``Src/ADFL/Client/async_peer.py:137-176``). In the reference that is
+fp32 tensors pickled through Ray's object store. Here each rank is one client on its own MI355X:
+
+    encode (SLQ, this rank's update)  ->  RCCL all-gather of the int8 / int4 payload over xGMI
+                                      ->  fused decode + mean of the K payloads (one HIP launch)
+
+Message layout (one row per chunk per rank, 16-byte aligned): ``payload | pad to 16 | fp32 scale | pad``.
+The scale rides in the row, so one all-gather moves payloads and scales together. The mean sums the K
+decoded payloads in rank order, fp32, then divides by K (the oracle's ``dequantize_mean``).
+
+With ``chunks > 1`` (the C5 4 GiB/client int4 variant) the absmax pass runs over the whole update first
+(the scale needs the global max), then chunk c is quantized while chunk c-1's all-gather is in flight:
+each all-gather is issued ``async_op=True`` right after its chunk's quantize, so RCCL's stream runs it
+concurrently with the next quantize on the compute stream.
+
+The codec backend is injectable so the exchange protocol can be exercised by gloo on CPU in tests; the
+product backend is the HIP codec (``HipCodec``) and there is no other.
+"""
+
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from . import _lib
+from ._lib import check
+
+
+def _pad16(n: int) -> int:
+    return (n + 15) // 16 * 16
+
+
+class HipCodec:
+    """The exchange's codec on the device: absmax over the full update, chunk quantize into a message
+    row (payload + scale trailer), fused decode + mean over gathered rows."""
+
+    def __init__(self, device: torch.device):
+        self.device = device
+        self.lib = _lib.load()
+        self.ws = torch.empty(_lib.workspace_bytes(), dtype=torch.uint8, device=device)
+
+    def _stream(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def absmax(self, x: torch.Tensor) -> None:
+        check(self.lib.adfl_slq_absmax(x.data_ptr(), x.numel(), self.ws.data_ptr(), self.ws.numel(), self._stream()))
+
+    def quantize(self, x: torch.Tensor, bits: int, packed: bool, row: torch.Tensor, payload_bytes: int) -> None:
+        scale_ptr = row.data_ptr() + _pad16(payload_bytes)
+        fn = self.lib.adfl_slq_quantize_int4 if packed else self.lib.adfl_slq_quantize
+        check(fn(x.data_ptr(), x.numel(), bits, self.ws.data_ptr(), row.data_ptr(), scale_ptr, self._stream()))
+
+    def mean(self, rows: torch.Tensor, n: int, packed: bool, payload_bytes: int, out: torch.Tensor) -> None:
+        k, row_bytes = rows.shape
+        scales = rows.data_ptr() + _pad16(payload_bytes)
+        fn = self.lib.adfl_slq_dequantize_mean_int4 if packed else self.lib.adfl_slq_dequantize_mean
+        check(fn(rows.data_ptr(), row_bytes, k, n, scales, row_bytes // 4, out.data_ptr(), self._stream()))
+
+
+class PeerExchange:
+    """Quantized all-gather + mean of one flat fp32 update per rank.
+
+    numel   elements of each rank's update (same on every rank)
+    bits    SLQ bit width (8: int8 payload; with packed=True the int4 nibble layout, compression.py:35-66)
+    chunks  >1 splits quantize + all-gather into a pipeline (C5)
+    """
+
+    def __init__(self, numel: int, bits: int = 8, packed: bool = False, chunks: int = 1,
+                 group: Optional[dist.ProcessGroup] = None, device: Optional[torch.device] = None, codec=None):
+        if numel < 1 or chunks < 1:
+            raise ValueError("PeerExchange: numel and chunks must be >= 1")
+        self.numel, self.bits, self.packed, self.group = numel, bits, packed, group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = device
+        self.codec = HipCodec(device) if codec is None else codec
+        # chunk boundaries: multiples of 32 elements keep every payload offset 16-byte aligned
+        step = -(-numel // chunks)
+        step = (step + 31) // 32 * 32
+        self.bounds = [(c0, min(numel, c0 + step)) for c0 in range(0, numel, step)]
+        self.payload = [self._payload_bytes(c1 - c0) for c0, c1 in self.bounds]
+        self.row_bytes = [_pad16(p) + 16 for p in self.payload]
+        self.local = [torch.empty(rb, dtype=torch.uint8, device=device) for rb in self.row_bytes]
+        self.gathered = [torch.empty(self.world, rb, dtype=torch.uint8, device=device) for rb in self.row_bytes]
+
+    def _payload_bytes(self, n: int) -> int:
+        return (n + 1) // 2 if self.packed else n
+
+    @property
+    def bytes_per_rank(self) -> int:
+        """Bytes each rank contributes to the all-gather (payloads + scale trailers)."""
+        return sum(self.row_bytes)
+
+    def encode_and_gather(self, x: torch.Tensor) -> List:
+        """Encode this rank's update chunk by chunk; each chunk's all-gather is issued as soon as it is
+        quantized. Returns the pending collective works."""
+        if x.numel() != self.numel or x.dtype != torch.float32:
+            raise ValueError(f"PeerExchange: expected {self.numel} fp32 elements, got {x.numel()} {x.dtype}")
+        x = x.reshape(-1)
+        self.codec.absmax(x)
+        works = []
+        for (c0, c1), row, out, pb in zip(self.bounds, self.local, self.gathered, self.payload):
+            self.codec.quantize(x[c0:c1], self.bits, self.packed, row, pb)
+            works.append(dist.all_gather_into_tensor(out.view(-1), row, group=self.group, async_op=True))
+        return works
+
+    def mean(self, works: List, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Wait for each chunk's all-gather and decode the K payloads into their fp32 mean."""
+        out = torch.empty(self.numel, dtype=torch.float32, device=self.device) if out is None else out
+        for (c0, c1), rows, pb, w in zip(self.bounds, self.gathered, self.payload, works):
+            w.wait()
+            self.codec.mean(rows, c1 - c0, self.packed, pb, out[c0:c1])
+        return out
+
+    def exchange_mean(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """stack(all ranks' decoded updates).mean(0) (Examples/ray_ad.py:188), via quantized all-gather."""
+        return self.mean(self.encode_and_gather(x), out)

@@ -336,6 +336,46 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_mean(const int8_t* __rest
     }
 }
 
+// int4 variant of the exchange epilogue: K packed rows (ceil(n/2) bytes each), one lane = 32 elements.
+__global__ __launch_bounds__(kBlock) void k_dequantize_mean_int4(const uint8_t* __restrict__ p, int64_t row_stride,
+                                                                 int k, int64_t n, const float* __restrict__ scales,
+                                                                 int64_t scale_stride, float* __restrict__ out) {
+  const int64_t ng = n >> 5;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  const double dk = (double)k;
+  for (int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x; g < ng; g += stride) {
+    float acc[32];
+    for (int r = 0; r < k; ++r) {
+      const uint4 w = *reinterpret_cast<const uint4*>(p + r * row_stride + 16 * g);
+      const float s = scales[r * scale_stride];
+      const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float4 a, b;
+        dequant8_int4(ws[j], s, a, b);
+        const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[8 * j + e] = (r == 0) ? v[e] : acc[8 * j + e] + v[e];
+      }
+    }
+    float4* o4 = reinterpret_cast<float4*>(out + 32 * g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      o4[j] = make_float4((float)((double)acc[4 * j] / dk), (float)((double)acc[4 * j + 1] / dk),
+                          (float)((double)acc[4 * j + 2] / dk), (float)((double)acc[4 * j + 3] / dk));
+  }
+  if (blockIdx.x == gridDim.x - 1)
+    for (int64_t i = (ng << 5) + threadIdx.x; i < n; i += kBlock) {
+      float acc = 0.0f;
+      for (int r = 0; r < k; ++r) {
+        float e0, e1;
+        dequant_byte_int4(p[r * row_stride + (i >> 1)], scales[r * scale_stride], e0, e1);
+        acc = (r == 0) ? ((i & 1) ? e1 : e0) : acc + ((i & 1) ? e1 : e0);
+      }
+      out[i] = (float)((double)acc / dk);
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // bucketed kernels (many tensors, one block per chunk of <= 8192 elements)
 // ------------------------------------------------------------------------------------------------
@@ -568,6 +608,16 @@ int adfl_slq_dequantize_mean(const int8_t* d_q, int64_t row_stride_bytes, int32_
   if (!d_q || !d_scales || !d_out || n < 1 || k < 1 || row_stride_bytes < n || scale_stride < 1) return ADFL_E_ARG;
   if (!aligned16(d_q) || !aligned16(d_out) || (row_stride_bytes & 15) != 0) return ADFL_E_ALIGN;
   hipLaunchKernelGGL(k_dequantize_mean, dim3(grid_for(n >> 4)), dim3(kBlock), 0, (hipStream_t)stream, d_q,
+                     row_stride_bytes, (int)k, n, d_scales, scale_stride, d_out);
+  return launch_status();
+}
+
+int adfl_slq_dequantize_mean_int4(const uint8_t* d_packed, int64_t row_stride_bytes, int32_t k, int64_t n,
+                                  const float* d_scales, int64_t scale_stride, float* d_out, void* stream) {
+  if (!d_packed || !d_scales || !d_out || n < 1 || k < 1 || row_stride_bytes < (n + 1) / 2 || scale_stride < 1)
+    return ADFL_E_ARG;
+  if (!aligned16(d_packed) || !aligned16(d_out) || (row_stride_bytes & 15) != 0) return ADFL_E_ALIGN;
+  hipLaunchKernelGGL(k_dequantize_mean_int4, dim3(grid_for(n >> 5)), dim3(kBlock), 0, (hipStream_t)stream, d_packed,
                      row_stride_bytes, (int)k, n, d_scales, scale_stride, d_out);
   return launch_status();
 }

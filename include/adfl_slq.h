@@ -116,6 +116,9 @@ int adfl_unpack_int4(const uint8_t* d_packed, int64_t n, int8_t* d_q, void* stre
  * ------------------------------------------------------------------------------------------- */
 int adfl_slq_dequantize_mean(const int8_t* d_q, int64_t row_stride_bytes, int32_t k, int64_t n,
                              const float* d_scales, int64_t scale_stride, float* d_out, void* stream);
+/* Same over K int4-packed rows (ceil(n/2) bytes of payload each, layout of adfl_slq_quantize_int4). */
+int adfl_slq_dequantize_mean_int4(const uint8_t* d_packed, int64_t row_stride_bytes, int32_t k, int64_t n,
+                                  const float* d_scales, int64_t scale_stride, float* d_out, void* stream);
 
 #ifdef __cplusplus
 }

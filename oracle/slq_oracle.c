@@ -115,5 +115,19 @@ void oracle_slq_dequantize_mean(const int8_t* const* qs, const float* scales, in
     }
 }
 
+/* Same mean over K int4-packed payloads (unpack_4bit then dequantize, compression.py:51-66). */
+void oracle_slq_dequantize_mean_int4(const uint8_t* const* ps, const float* scales, int32_t k, int64_t n, float* out) {
+    for (int64_t i = 0; i < n; ++i) {
+        float s = 0.0f;
+        for (int32_t r = 0; r < k; ++r) {
+            uint8_t b = ps[r][i / 2];
+            int v = (i & 1) ? ((b & 0xF) - 8) : (((b >> 4) & 0xF) - 8);
+            float d = scales[r] * (float)v;
+            s = (r == 0) ? d : s + d;
+        }
+        out[i] = s / (float)k;
+    }
+}
+
 /* Thread-free helper the tests use for SHA inputs of recipe cases. */
 uint32_t oracle_f32_bits(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }

@@ -55,6 +55,8 @@ def lib():
         L.oracle_slq_dequantize_int4.argtypes, L.oracle_slq_dequantize_int4.restype = [P, I64, F, P], None
         L.oracle_slq_dequantize_mean.argtypes = [P, P, I32, I64, P]
         L.oracle_slq_dequantize_mean.restype = None
+        L.oracle_slq_dequantize_mean_int4.argtypes = [P, P, I32, I64, P]
+        L.oracle_slq_dequantize_mean_int4.restype = None
         _lib = L
     return _lib
 
@@ -118,6 +120,15 @@ def dequantize_mean(qs, scales) -> np.ndarray:
     sc = np.ascontiguousarray(scales, dtype=np.float32)
     out = np.empty(n, np.float32)
     lib().oracle_slq_dequantize_mean(arr, _ptr(sc), len(qs), n, _ptr(out))
+    return out
+
+
+def dequantize_mean_int4(packed_rows, scales, n: int) -> np.ndarray:
+    ps = [np.ascontiguousarray(p).view(np.uint8).reshape(-1) for p in packed_rows]
+    arr = (ctypes.c_void_p * len(ps))(*[p.ctypes.data for p in ps])
+    sc = np.ascontiguousarray(scales, dtype=np.float32)
+    out = np.empty(n, np.float32)
+    lib().oracle_slq_dequantize_mean_int4(arr, _ptr(sc), len(ps), n, _ptr(out))
     return out
 
 

@@ -1,0 +1,92 @@
+"""CPU: the C-ABI library loads and exports every symbol include/adfl_slq.h declares; argument checks
+and host-side chunk planning work without a GPU (no kernel is launched by any call here)."""
+
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from adfl_amd import _lib
+from adfl_amd._build import LIB_PATH
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "adfl_slq.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b(adfl_\w+)\s*\(", text, flags=re.M)))
+
+
+def test_header_declares_the_binding_table():
+    assert declared_functions() == sorted(_lib.SIGNATURES)
+
+
+def test_library_exports_every_declared_symbol():
+    raw = ctypes.CDLL(LIB_PATH)
+    for name in declared_functions():
+        assert hasattr(raw, name), name
+
+
+def test_exports_via_nm():
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (adfl_\w+)", out))
+    assert exported == set(declared_functions())
+
+
+def test_abi_version_and_constants():
+    lib = _lib.load()
+    assert lib.adfl_slq_abi_version() == _lib.ABI_VERSION
+    assert lib.adfl_slq_workspace_bytes() >= (2048 + 1) * 4
+    text = open(HEADER).read()
+    assert f"#define ADFL_SLQ_ALIGN_ELEMS {_lib.ALIGN_ELEMS}" in text
+    assert f"#define ADFL_SLQ_CHUNK_ELEMS {_lib.CHUNK_ELEMS}" in text
+    assert ctypes.sizeof(_lib.Chunk) == 24
+
+
+@pytest.mark.parametrize("code,frag", [(0, "ok"), (-1, "invalid argument"), (-2, "bits"), (-3, "aligned"),
+                                       (-4, "workspace")])
+def test_strerror(code, frag):
+    assert frag in _lib.load().adfl_slq_strerror(code).decode()
+
+
+def test_argument_errors_return_codes_without_launching():
+    lib = _lib.load()
+    assert lib.adfl_slq_encode(None, 10, 8, None, None, None, 0, None) == -1
+    assert lib.adfl_slq_encode(16, 10, 0, 16, 16, 16, 1 << 20, None) == -2       # bits checked first
+    assert lib.adfl_slq_encode(16, 10, 17, 16, 16, 16, 1 << 20, None) == -2
+    assert lib.adfl_slq_absmax(20, 10, 16, 1 << 20, None) == -3                  # misaligned x
+    assert lib.adfl_slq_absmax(16, 10, 16, 16, None) == -4                       # workspace too small
+    assert lib.adfl_slq_absmax(16, 0, 16, 1 << 20, None) == -1                   # empty
+    assert lib.adfl_slq_dequantize(16, 10, 16, 20, None) == -3
+    assert lib.adfl_slq_dequantize_mean(16, 8, 2, 10, 16, 1, 16, None) == -1    # row stride < n
+    assert lib.adfl_slq_dequantize_mean(16, 24, 2, 10, 16, 1, 16, None) == -3   # row stride % 16
+    assert lib.adfl_slq_encode_batched(16, 16, 0, 8, 16, 16, 16, None) == -1
+    with pytest.raises(_lib.AdflError, match="bits"):
+        _lib.check(-2)
+
+
+def test_build_chunks_host_planning():
+    lib = _lib.load()
+    sizes = np.array([10, 8192, 8193, 64, 3 * 8192 + 5], np.int64)
+    offsets = np.array([0, 64, 8256, 16512, 16576], np.int64)
+    n = lib.adfl_slq_build_chunks(offsets.ctypes.data, sizes.ctypes.data, len(sizes), None, 0)
+    assert n == 1 + 1 + 2 + 1 + 4
+    chunks = (_lib.Chunk * n)()
+    assert lib.adfl_slq_build_chunks(offsets.ctypes.data, sizes.ctypes.data, len(sizes), chunks, n) == n
+    rows = [(c.start, c.len, c.tensor, c.first_chunk, c.nchunks) for c in chunks]
+    assert rows[2] == (8256, 8192, 2, 2, 2) and rows[3] == (16448, 1, 2, 2, 2)
+    assert rows[-1] == (16576 + 3 * 8192, 5, 4, 5, 4)
+    covered = {t: sum(c.len for c in chunks if c.tensor == t) for t in range(len(sizes))}
+    assert [covered[t] for t in range(len(sizes))] == sizes.tolist()
+    # capacity too small, misaligned offset, empty tensor
+    assert lib.adfl_slq_build_chunks(offsets.ctypes.data, sizes.ctypes.data, len(sizes), chunks, n - 1) == -1
+    bad = offsets.copy()
+    bad[1] = 65
+    assert lib.adfl_slq_build_chunks(bad.ctypes.data, sizes.ctypes.data, len(sizes), None, 0) == -1
+    zero = sizes.copy()
+    zero[0] = 0
+    assert lib.adfl_slq_build_chunks(offsets.ctypes.data, zero.ctypes.data, len(sizes), None, 0) == -1

@@ -45,7 +45,7 @@ def test_c1_two_client_round_trip_matches_golden():
         assert same_f32(dec["fc.weight"].numpy(), A["c1_fc_weight_b8__deq"])
         assert dec["fc.weight"].dtype == torch.float32 and dec["fc.weight"].shape == w.shape
         dec["fc.weight"].add_(1.0)  # owned and writable, as strategies require
-        assert dec["fc.bias"] is b
+        assert dec["fc.bias"].data_ptr() == b.data_ptr()
 
 
 @pytest.mark.parametrize("bits", [8, 4, 2])
