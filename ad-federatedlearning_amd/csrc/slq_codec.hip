@@ -8,19 +8,26 @@
 //   int4    Src/ADFL/compression.py:35-66      pack_4bit / unpack_4bit nibble layout
 //   mean    Examples/ray_ad.py:188             stack(updates).mean(0) after the peer exchange
 //
-// Design (DESIGN.md has the byte accounting): the codec is a pure HBM stream, ~6 VALU ops per
-// element, so every kernel is built for bandwidth — 16-byte loads and stores per lane (1 KiB per
-// wave-instruction), grid-stride loops sized to fill 256 CUs x 8 resident 256-thread blocks, no
-// atomics and no inter-workgroup hand-off inside a launch. The one grid-wide dependency (the scale
-// needs max|x| over the whole tensor) is a kernel boundary: pass 1 writes one absmax partial per
-// block, pass 2 re-reduces those partials (<= 8 KiB, L2-resident) in every block's prologue.
-// Pass 2 walks the tensor in the opposite direction to pass 1, so its first ~200 MB are the bytes
-// pass 1 read last and are still resident in the 256 MiB Infinity Cache; decode walks opposite to
-// pass 2 for the same reason on the payload. Outputs do not depend on traversal order.
+// Design (DESIGN.md has the byte accounting and the measurements behind every choice): the codec is a
+// pure HBM stream with ~6 VALU ops per element, so every kernel is built for bandwidth.
+//  * Wave tiles. A wave owns a tile of 1024 elements (int4: 2048). Every global access is a 16-byte
+//    per-lane access that is contiguous across the wave (1 KiB per wave-instruction). Where the natural
+//    per-lane shape differs between input and output (4 floats in, 4 bytes out), the wave transposes
+//    through 1 KiB of LDS, so both the loads and the stores stay fully coalesced.
+//  * The one grid-wide dependency (scale needs max|x| over the whole tensor) is a kernel boundary:
+//    pass 1 writes one absmax partial per block, pass 2 re-reduces them (<= 8 KiB, L2) in every block's
+//    prologue. No atomics, no in-launch hand-off, deterministic.
+//  * Cache policy per stream (MI355X 256 MiB Infinity Cache): pass 1 reads x block-contiguously with
+//    non-temporal loads except for the last kCacheKeepBytes, which it reads with allocating loads;
+//    pass 2 walks x backwards, so it starts on exactly those bytes. Pass 2 reads x non-temporally
+//    (x is dead afterwards) and writes the payload backwards with allocating stores; decode reads the
+//    payload forwards, starting on the bytes pass 2 wrote last. Decode writes its fp32 output with
+//    non-temporal stores (nothing re-reads it soon; it must not evict the next pass's lines).
+//    None of this changes a single output bit.
 //
 // Numerics: no fast-math, fp32 denormals preserved (gfx950 default), -ffp-contract=off. Scale and
-// reciprocal are computed as fp64 quotients rounded once to fp32, which equals the correctly
-// rounded fp32 quotient (53 >= 2*24+2), independent of the compiler's fp32 division lowering.
+// reciprocal are fp64 quotients rounded once to fp32 = the correctly rounded fp32 quotient (53 >= 2*24+2),
+// independent of the compiler's fp32 division lowering.
 
 #include <hip/hip_runtime.h>
 
@@ -31,10 +38,34 @@
 
 namespace {
 
-constexpr int kBlock = 256;                 // 4 waves of 64
-constexpr int kMaxFlatBlocks = 2048;        // 256 CUs x 8 resident blocks
-constexpr int kCountSlot = kMaxFlatBlocks;  // workspace word holding pass 1's partial count
-constexpr int64_t kWorkspaceBytes = 16384;  // >= (kMaxFlatBlocks + 1) * 4, padded
+constexpr int kBlock = 256;                        // 4 waves of 64
+constexpr int kWaves = kBlock / 64;
+constexpr int kTile = 1024;                        // int8 path: elements per wave tile
+constexpr int kTile4 = 2048;                       // int4 path: elements per wave tile
+constexpr int kMaxFlatBlocks = 2048;               // 256 CUs x 8 resident 256-thread blocks
+constexpr int kAbsmaxBlocks = 1024;                // pass-1 grid (block-contiguous ranges)
+constexpr int kCountSlot = kMaxFlatBlocks;         // workspace word holding pass 1's partial count
+constexpr int64_t kWorkspaceBytes = 16384;         // >= (kMaxFlatBlocks + 1) * 4, padded
+constexpr int64_t kCacheKeepBytes = 192ll << 20;   // tail of x pass 1 leaves in the Infinity Cache
+
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------------------------------------
+// memory helpers
+// ------------------------------------------------------------------------------------------------
+template <bool NT>
+__device__ __forceinline__ float4 load4(const float4* p) {
+  if (NT) {
+    const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+  }
+  return *p;
+}
+
+__device__ __forceinline__ void store4_nt(float4* p, float4 d) {
+  const f4v v = {d.x, d.y, d.z, d.w};
+  __builtin_nontemporal_store(v, reinterpret_cast<f4v*>(p));
+}
 
 // ------------------------------------------------------------------------------------------------
 // element helpers
@@ -74,10 +105,9 @@ __device__ __forceinline__ uint32_t pack_pair(int hi, int lo) {
   return ((uint32_t(hi + 8) << 4) | uint32_t(lo + 8)) & 0xffu;
 }
 
-// 8 quantized elements (two float4) -> 4 packed bytes.
-__device__ __forceinline__ uint32_t quant8_int4(float4 a, float4 b, float inv) {
-  return pack_pair(quant1(a.x, inv), quant1(a.y, inv)) | (pack_pair(quant1(a.z, inv), quant1(a.w, inv)) << 8) |
-         (pack_pair(quant1(b.x, inv), quant1(b.y, inv)) << 16) | (pack_pair(quant1(b.z, inv), quant1(b.w, inv)) << 24);
+// 4 elements -> 2 packed bytes (high nibble = even element).
+__device__ __forceinline__ uint32_t quant4_int4(float4 v, float inv) {
+  return pack_pair(quant1(v.x, inv), quant1(v.y, inv)) | (pack_pair(quant1(v.z, inv), quant1(v.w, inv)) << 8);
 }
 
 // unpack_4bit (compression.py:60-61) on one packed byte: high nibble = even element.
@@ -86,11 +116,20 @@ __device__ __forceinline__ void dequant_byte_int4(uint32_t b, float s, float& e0
   e1 = s * (float)((int)(b & 0xfu) - 8);
 }
 
-__device__ __forceinline__ void dequant8_int4(uint32_t w, float s, float4& a, float4& b) {
-  dequant_byte_int4(w & 0xffu, s, a.x, a.y);
-  dequant_byte_int4((w >> 8) & 0xffu, s, a.z, a.w);
-  dequant_byte_int4((w >> 16) & 0xffu, s, b.x, b.y);
-  dequant_byte_int4(w >> 24, s, b.z, b.w);
+// 2 packed bytes -> 4 elements.
+__device__ __forceinline__ float4 dequant2_int4(uint32_t h, float s) {
+  float4 r;
+  dequant_byte_int4(h & 0xffu, s, r.x, r.y);
+  dequant_byte_int4((h >> 8) & 0xffu, s, r.z, r.w);
+  return r;
+}
+
+__device__ __forceinline__ float4 add4(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
+
+// fp32 mean = correctly rounded acc / K (torch: sum then true division).
+__device__ __forceinline__ float4 div4(float4 a, double k) {
+  return make_float4((float)((double)a.x / k), (float)((double)a.y / k), (float)((double)a.z / k),
+                     (float)((double)a.w / k));
 }
 
 // scale = fp32(absmax / q_max) (quant.py:99-100: fp32 tensor / Python int, i.e. / float(q_max));
@@ -117,7 +156,7 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 
 // Block-wide max, result broadcast to every thread.
 __device__ __forceinline__ uint32_t block_max(uint32_t v) {
-  __shared__ uint32_t red[kBlock / 64];
+  __shared__ uint32_t red[kWaves];
   v = wave_max(v);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
@@ -134,134 +173,169 @@ __device__ __forceinline__ uint32_t reduce_partials(const uint32_t* __restrict__
 }
 
 // ------------------------------------------------------------------------------------------------
+// wave-tile bodies (shared by the flat and the bucketed kernels)
+//   lane l, instruction j in 0..3 of an int8 tile: elements 4*(j*64 + l) .. +3 (float4 j*64+l), whose
+//   payload is dword j*64+l of the tile's 1 KiB; the LDS transpose hands lane l dwords 4l..4l+3.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void quantize_tile(const float4* __restrict__ x4, uint4* __restrict__ q16, float inv,
+                                              uint32_t* __restrict__ lds, int lane) {
+  float4 v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = load4<true>(x4 + j * 64 + lane);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) lds[j * 64 + lane] = quant4(v[j], inv);
+  __builtin_amdgcn_wave_barrier();
+  const uint4 o = reinterpret_cast<const uint4*>(lds)[lane];
+  __builtin_amdgcn_wave_barrier();
+  q16[lane] = o;
+}
+
+__device__ __forceinline__ void dequantize_tile(const uint4* __restrict__ q16, float4* __restrict__ o4, float s,
+                                                uint32_t* __restrict__ lds, int lane) {
+  reinterpret_cast<uint4*>(lds)[lane] = q16[lane];
+  __builtin_amdgcn_wave_barrier();
+  uint32_t w[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) w[j] = lds[j * 64 + lane];
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int j = 0; j < 4; ++j) store4_nt(o4 + j * 64 + lane, dequant4(w[j], s));
+}
+
+// ------------------------------------------------------------------------------------------------
 // flat kernels (one tensor)
 // ------------------------------------------------------------------------------------------------
-template <int U>
-__global__ __launch_bounds__(kBlock) void k_absmax_flat(const float* __restrict__ x, int64_t n,
-                                                        uint32_t* __restrict__ partials) {
-  const float4* x4 = reinterpret_cast<const float4*>(x);
-  const int64_t n4 = n >> 2;
-  const int64_t stride = (int64_t)gridDim.x * kBlock;
-  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+template <int U, bool NT>
+__device__ __forceinline__ uint32_t absmax_range(const float4* __restrict__ x4, int64_t b0, int64_t b1) {
   uint32_t m = 0;
-  for (; i + (U - 1) * stride < n4; i += U * stride) {
+  int64_t i = b0 + threadIdx.x;
+  for (; i + (U - 1) * kBlock < b1; i += U * kBlock) {
     float4 v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = x4[i + u * stride];
+    for (int u = 0; u < U; ++u) v[u] = load4<NT>(x4 + i + u * kBlock);
 #pragma unroll
     for (int u = 0; u < U; ++u) m = max(m, abs_bits4(v[u]));
   }
-  for (; i < n4; i += stride) m = max(m, abs_bits4(x4[i]));
+  for (; i < b1; i += kBlock) m = max(m, abs_bits4(load4<NT>(x4 + i)));
+  return m;
+}
+
+// Pass 1: block b owns float4s [b*per, (b+1)*per). Blocks wholly before the last keep4 float4s read
+// non-temporally; the rest with allocating loads (they stay in the Infinity Cache for pass 2).
+__global__ __launch_bounds__(kBlock) void k_absmax_flat(const float* __restrict__ x, int64_t n, int64_t keep4,
+                                                        uint32_t* __restrict__ partials) {
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  const int64_t n4 = n >> 2;
+  const int64_t per = ((n4 + gridDim.x - 1) / gridDim.x + kBlock - 1) / kBlock * kBlock;
+  const int64_t b0 = (int64_t)blockIdx.x * per;
+  const int64_t b1 = min(n4, b0 + per);
+  uint32_t m = (b1 <= n4 - keep4) ? absmax_range<8, true>(x4, b0, b1) : absmax_range<8, false>(x4, b0, b1);
   if (blockIdx.x == 0 && threadIdx.x < (n & 3)) m = max(m, abs_bits(x[(n4 << 2) + threadIdx.x]));
   m = block_max(m);
   if (threadIdx.x == 0) partials[blockIdx.x] = m;
   if (blockIdx.x == 0 && threadIdx.x == 0) partials[kCountSlot] = gridDim.x;  // self-describing workspace
 }
 
-// One lane = one 16-element group: four 16-byte loads, one 16-byte store.
-template <bool REVERSE>
+// Pass 2: tiles walked from the END of x (Infinity Cache reuse of pass 1's tail).
 __global__ __launch_bounds__(kBlock) void k_quantize_flat(const float* __restrict__ x, int64_t n, float qmax,
                                                           const uint32_t* __restrict__ partials,
                                                           int8_t* __restrict__ q, float* __restrict__ scale_out) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kWaves][kTile / 4];
   const ScaleInv si = make_scale(reduce_partials(partials, (int)partials[kCountSlot]), qmax);
   if (blockIdx.x == 0 && threadIdx.x == 0) *scale_out = si.scale;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const float4* x4 = reinterpret_cast<const float4*>(x);
   uint4* q16 = reinterpret_cast<uint4*>(q);
-  const int64_t ng = n >> 4;
-  const int64_t stride = (int64_t)gridDim.x * kBlock;
-  for (int64_t g0 = (int64_t)blockIdx.x * kBlock + threadIdx.x; g0 < ng; g0 += stride) {
-    const int64_t g = REVERSE ? ng - 1 - g0 : g0;
-    const float4 a = x4[4 * g], b = x4[4 * g + 1], c = x4[4 * g + 2], d = x4[4 * g + 3];
-    q16[g] = make_uint4(quant4(a, si.inv), quant4(b, si.inv), quant4(c, si.inv), quant4(d, si.inv));
+  const int64_t ntiles = n / kTile;
+  const int64_t wstride = (int64_t)gridDim.x * kWaves;
+  for (int64_t t0 = (int64_t)blockIdx.x * kWaves + wave; t0 < ntiles; t0 += wstride) {
+    const int64_t t = ntiles - 1 - t0;
+    quantize_tile(x4 + t * (kTile / 4), q16 + t * (kTile / 16), si.inv, lds[wave], lane);
   }
   if (blockIdx.x == gridDim.x - 1)
-    for (int64_t i = (ng << 4) + threadIdx.x; i < n; i += kBlock) q[i] = (int8_t)quant1(x[i], si.inv);
+    for (int64_t i = ntiles * kTile + threadIdx.x; i < n; i += kBlock) q[i] = (int8_t)quant1(x[i], si.inv);
 }
 
-// One lane = one 16-element group: one 16-byte load, four 16-byte stores.
-template <bool REVERSE>
+// Decode: tiles walked forwards (pass 2 wrote the head of the payload last).
 __global__ __launch_bounds__(kBlock) void k_dequantize_flat(const int8_t* __restrict__ q, int64_t n,
                                                             const float* __restrict__ scale_p,
                                                             float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kWaves][kTile / 4];
   const float s = *scale_p;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint4* q16 = reinterpret_cast<const uint4*>(q);
   float4* o4 = reinterpret_cast<float4*>(out);
-  const int64_t ng = n >> 4;
-  const int64_t stride = (int64_t)gridDim.x * kBlock;
-  for (int64_t g0 = (int64_t)blockIdx.x * kBlock + threadIdx.x; g0 < ng; g0 += stride) {
-    const int64_t g = REVERSE ? ng - 1 - g0 : g0;
-    const uint4 p = q16[g];
-    o4[4 * g] = dequant4(p.x, s);
-    o4[4 * g + 1] = dequant4(p.y, s);
-    o4[4 * g + 2] = dequant4(p.z, s);
-    o4[4 * g + 3] = dequant4(p.w, s);
-  }
+  const int64_t ntiles = n / kTile;
+  const int64_t wstride = (int64_t)gridDim.x * kWaves;
+  for (int64_t t = (int64_t)blockIdx.x * kWaves + wave; t < ntiles; t += wstride)
+    dequantize_tile(q16 + t * (kTile / 16), o4 + t * (kTile / 4), s, lds[wave], lane);
   if (blockIdx.x == gridDim.x - 1)
-    for (int64_t i = (ng << 4) + threadIdx.x; i < n; i += kBlock) out[i] = s * (float)q[i];
+    for (int64_t i = ntiles * kTile + threadIdx.x; i < n; i += kBlock) out[i] = s * (float)q[i];
 }
 
-// int4: one lane = one 32-element group: eight 16-byte loads, one 16-byte store of packed nibbles.
-template <bool REVERSE>
+// int4 pass 2: a wave tile is 2048 elements = 8 coalesced 16-byte loads per lane -> 16 packed bytes per
+// lane, transposed through 1 KiB of LDS (lane l, load j packs float4 j*64+l into halfword j*64+l).
 __global__ __launch_bounds__(kBlock) void k_quantize_int4_flat(const float* __restrict__ x, int64_t n, float qmax,
                                                                const uint32_t* __restrict__ partials,
                                                                uint8_t* __restrict__ packed,
                                                                float* __restrict__ scale_out) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[kWaves][kTile4 / 4];
   const ScaleInv si = make_scale(reduce_partials(partials, (int)partials[kCountSlot]), qmax);
   if (blockIdx.x == 0 && threadIdx.x == 0) *scale_out = si.scale;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const float4* x4 = reinterpret_cast<const float4*>(x);
   uint4* p16 = reinterpret_cast<uint4*>(packed);
-  const int64_t ng = n >> 5;
-  const int64_t stride = (int64_t)gridDim.x * kBlock;
-  for (int64_t g0 = (int64_t)blockIdx.x * kBlock + threadIdx.x; g0 < ng; g0 += stride) {
-    const int64_t g = REVERSE ? ng - 1 - g0 : g0;
-    const float4* s = x4 + 8 * g;
-    const float4 v0 = s[0], v1 = s[1], v2 = s[2], v3 = s[3], v4 = s[4], v5 = s[5], v6 = s[6], v7 = s[7];
-    p16[g] = make_uint4(quant8_int4(v0, v1, si.inv), quant8_int4(v2, v3, si.inv), quant8_int4(v4, v5, si.inv),
-                        quant8_int4(v6, v7, si.inv));
+  const int64_t ntiles = n / kTile4;
+  const int64_t wstride = (int64_t)gridDim.x * kWaves;
+  for (int64_t t0 = (int64_t)blockIdx.x * kWaves + wave; t0 < ntiles; t0 += wstride) {
+    const int64_t t = ntiles - 1 - t0;
+    const float4* xs = x4 + t * (kTile4 / 4);
+    float4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = load4<true>(xs + j * 64 + lane);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) lds[wave][j * 64 + lane] = (uint16_t)quant4_int4(v[j], si.inv);
+    __builtin_amdgcn_wave_barrier();
+    const uint4 o = reinterpret_cast<const uint4*>(lds[wave])[lane];
+    __builtin_amdgcn_wave_barrier();
+    p16[t * 64 + lane] = o;
   }
   if (blockIdx.x == gridDim.x - 1) {
     const int64_t np = (n + 1) >> 1;
-    for (int64_t j = (ng << 4) + threadIdx.x; j < np; j += kBlock) {
+    for (int64_t j = ntiles * (kTile4 / 2) + threadIdx.x; j < np; j += kBlock) {
       const int hi = quant1(x[2 * j], si.inv);
-      const int lo = (2 * j + 1 < n) ? quant1(x[2 * j + 1], si.inv) : 0;  // pad with one zero (compression.py:42-43)
+      const int lo = (2 * j + 1 < n) ? quant1(x[2 * j + 1], si.inv) : 0;  // pad one zero (compression.py:42-43)
       packed[j] = (uint8_t)pack_pair(hi, lo);
     }
   }
 }
 
-// int4 decode: one lane = one 32-element group: one 16-byte load, eight 16-byte stores.
-template <bool REVERSE>
+// int4 decode: lane loads 16 packed bytes (coalesced), LDS transpose, 8 coalesced float4 NT stores.
 __global__ __launch_bounds__(kBlock) void k_dequantize_int4_flat(const uint8_t* __restrict__ packed, int64_t n,
                                                                  const float* __restrict__ scale_p,
                                                                  float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[kWaves][kTile4 / 4];
   const float s = *scale_p;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint4* p16 = reinterpret_cast<const uint4*>(packed);
   float4* o4 = reinterpret_cast<float4*>(out);
-  const int64_t ng = n >> 5;
-  const int64_t stride = (int64_t)gridDim.x * kBlock;
-  for (int64_t g0 = (int64_t)blockIdx.x * kBlock + threadIdx.x; g0 < ng; g0 += stride) {
-    const int64_t g = REVERSE ? ng - 1 - g0 : g0;
-    const uint4 p = p16[g];
-    float4 a, b;
-    float4* d = o4 + 8 * g;
-    dequant8_int4(p.x, s, a, b);
-    d[0] = a;
-    d[1] = b;
-    dequant8_int4(p.y, s, a, b);
-    d[2] = a;
-    d[3] = b;
-    dequant8_int4(p.z, s, a, b);
-    d[4] = a;
-    d[5] = b;
-    dequant8_int4(p.w, s, a, b);
-    d[6] = a;
-    d[7] = b;
+  const int64_t ntiles = n / kTile4;
+  const int64_t wstride = (int64_t)gridDim.x * kWaves;
+  for (int64_t t = (int64_t)blockIdx.x * kWaves + wave; t < ntiles; t += wstride) {
+    reinterpret_cast<uint4*>(lds[wave])[lane] = p16[t * 64 + lane];
+    __builtin_amdgcn_wave_barrier();
+    uint32_t h[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) h[j] = lds[wave][j * 64 + lane];
+    __builtin_amdgcn_wave_barrier();
+    float4* d = o4 + t * (kTile4 / 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) store4_nt(d + j * 64 + lane, dequant2_int4(h[j], s));
   }
   if (blockIdx.x == gridDim.x - 1)
-    for (int64_t i = (ng << 5) + threadIdx.x; i < n; i += kBlock) {
-      const uint32_t b = packed[i >> 1];
+    for (int64_t i = ntiles * kTile4 + threadIdx.x; i < n; i += kBlock) {
       float e0, e1;
-      dequant_byte_int4(b, s, e0, e1);
+      dequant_byte_int4(packed[i >> 1], s, e0, e1);
       out[i] = (i & 1) ? e1 : e0;
     }
 }
@@ -287,85 +361,71 @@ __global__ __launch_bounds__(kBlock) void k_unpack_int4(const uint8_t* __restric
   }
 }
 
-// Peer-exchange epilogue: mean of K dequantized rows, fp32, rows summed in order then / K.
+// Peer-exchange epilogue: mean of K dequantized int8 rows, rows summed in order (fp32), then / K.
+// Per row: one coalesced 16-byte load per lane + LDS transpose; output: coalesced NT float4 stores.
 __global__ __launch_bounds__(kBlock) void k_dequantize_mean(const int8_t* __restrict__ q, int64_t row_stride, int k,
                                                             int64_t n, const float* __restrict__ scales,
                                                             int64_t scale_stride, float* __restrict__ out) {
-  const int64_t ng = n >> 4;
-  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kWaves][kTile / 4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t ntiles = n / kTile;
+  const int64_t wstride = (int64_t)gridDim.x * kWaves;
   const double dk = (double)k;
-  for (int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x; g < ng; g += stride) {
-    float acc[16];
-    {
-      const uint4 p = *reinterpret_cast<const uint4*>(q + 16 * g);
-      const float s = scales[0];
-      const uint32_t w[4] = {p.x, p.y, p.z, p.w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float4 v = dequant4(w[j], s);
-        acc[4 * j] = v.x;
-        acc[4 * j + 1] = v.y;
-        acc[4 * j + 2] = v.z;
-        acc[4 * j + 3] = v.w;
-      }
-    }
-    for (int r = 1; r < k; ++r) {
-      const uint4 p = *reinterpret_cast<const uint4*>(q + r * row_stride + 16 * g);
+  for (int64_t t = (int64_t)blockIdx.x * kWaves + wave; t < ntiles; t += wstride) {
+    float4 acc[4];
+    for (int r = 0; r < k; ++r) {
+      const uint4* q16 = reinterpret_cast<const uint4*>(q + r * row_stride) + t * (kTile / 16);
       const float s = scales[r * scale_stride];
-      const uint32_t w[4] = {p.x, p.y, p.z, p.w};
+      reinterpret_cast<uint4*>(lds[wave])[lane] = q16[lane];
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float4 v = dequant4(w[j], s);
-        acc[4 * j] += v.x;
-        acc[4 * j + 1] += v.y;
-        acc[4 * j + 2] += v.z;
-        acc[4 * j + 3] += v.w;
+        const float4 v = dequant4(lds[wave][j * 64 + lane], s);
+        acc[j] = (r == 0) ? v : add4(acc[j], v);
       }
+      __builtin_amdgcn_wave_barrier();
     }
-    float4* o4 = reinterpret_cast<float4*>(out + 16 * g);
+    float4* o4 = reinterpret_cast<float4*>(out) + t * (kTile / 4);
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      o4[j] = make_float4((float)((double)acc[4 * j] / dk), (float)((double)acc[4 * j + 1] / dk),
-                          (float)((double)acc[4 * j + 2] / dk), (float)((double)acc[4 * j + 3] / dk));
+    for (int j = 0; j < 4; ++j) store4_nt(o4 + j * 64 + lane, div4(acc[j], dk));
   }
   if (blockIdx.x == gridDim.x - 1)
-    for (int64_t i = (ng << 4) + threadIdx.x; i < n; i += kBlock) {
+    for (int64_t i = ntiles * kTile + threadIdx.x; i < n; i += kBlock) {
       float acc = scales[0] * (float)q[i];
       for (int r = 1; r < k; ++r) acc += scales[r * scale_stride] * (float)q[r * row_stride + i];
       out[i] = (float)((double)acc / dk);
     }
 }
 
-// int4 variant of the exchange epilogue: K packed rows (ceil(n/2) bytes each), one lane = 32 elements.
+// Same over K int4-packed rows (2048-element wave tiles, 1 KiB of packed bytes per row per tile).
 __global__ __launch_bounds__(kBlock) void k_dequantize_mean_int4(const uint8_t* __restrict__ p, int64_t row_stride,
                                                                  int k, int64_t n, const float* __restrict__ scales,
                                                                  int64_t scale_stride, float* __restrict__ out) {
-  const int64_t ng = n >> 5;
-  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[kWaves][kTile4 / 4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t ntiles = n / kTile4;
+  const int64_t wstride = (int64_t)gridDim.x * kWaves;
   const double dk = (double)k;
-  for (int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x; g < ng; g += stride) {
-    float acc[32];
+  for (int64_t t = (int64_t)blockIdx.x * kWaves + wave; t < ntiles; t += wstride) {
+    float4 acc[8];
     for (int r = 0; r < k; ++r) {
-      const uint4 w = *reinterpret_cast<const uint4*>(p + r * row_stride + 16 * g);
+      const uint4* p16 = reinterpret_cast<const uint4*>(p + r * row_stride) + t * 64;
       const float s = scales[r * scale_stride];
-      const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+      reinterpret_cast<uint4*>(lds[wave])[lane] = p16[lane];
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float4 a, b;
-        dequant8_int4(ws[j], s, a, b);
-        const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc[8 * j + e] = (r == 0) ? v[e] : acc[8 * j + e] + v[e];
+      for (int j = 0; j < 8; ++j) {
+        const float4 v = dequant2_int4(lds[wave][j * 64 + lane], s);
+        acc[j] = (r == 0) ? v : add4(acc[j], v);
       }
+      __builtin_amdgcn_wave_barrier();
     }
-    float4* o4 = reinterpret_cast<float4*>(out + 32 * g);
+    float4* o4 = reinterpret_cast<float4*>(out) + t * (kTile4 / 4);
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      o4[j] = make_float4((float)((double)acc[4 * j] / dk), (float)((double)acc[4 * j + 1] / dk),
-                          (float)((double)acc[4 * j + 2] / dk), (float)((double)acc[4 * j + 3] / dk));
+    for (int j = 0; j < 8; ++j) store4_nt(o4 + j * 64 + lane, div4(acc[j], dk));
   }
   if (blockIdx.x == gridDim.x - 1)
-    for (int64_t i = (ng << 5) + threadIdx.x; i < n; i += kBlock) {
+    for (int64_t i = ntiles * kTile4 + threadIdx.x; i < n; i += kBlock) {
       float acc = 0.0f;
       for (int r = 0; r < k; ++r) {
         float e0, e1;
@@ -377,21 +437,20 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_mean_int4(const uint8_t* 
 }
 
 // ------------------------------------------------------------------------------------------------
-// bucketed kernels (many tensors, one block per chunk of <= 8192 elements)
+// bucketed kernels (many tensors, one block per chunk of <= 8192 elements = 8 wave tiles)
 // ------------------------------------------------------------------------------------------------
+// Pass 1 keeps default (allocating) loads: a bucketed update (e.g. 46.8 MB for ResNet-18) fits the
+// Infinity Cache whole, so pass 2 re-reads it on-die.
 __global__ __launch_bounds__(kBlock) void k_absmax_batched(const float* __restrict__ x,
                                                            const adfl_slq_chunk* __restrict__ chunks,
                                                            uint32_t* __restrict__ partials) {
   const adfl_slq_chunk c = chunks[blockIdx.x];
   const float* xc = x + c.start;
   const float4* x4 = reinterpret_cast<const float4*>(xc);
-  const int ng = c.len >> 4;
+  const int n4 = c.len >> 2;
   uint32_t m = 0;
-  for (int g = threadIdx.x; g < ng; g += kBlock) {
-    const float4 a = x4[4 * g], b = x4[4 * g + 1], d = x4[4 * g + 2], e = x4[4 * g + 3];
-    m = max(m, max(max(abs_bits4(a), abs_bits4(b)), max(abs_bits4(d), abs_bits4(e))));
-  }
-  for (int i = (ng << 4) + threadIdx.x; i < c.len; i += kBlock) m = max(m, abs_bits(xc[i]));
+  for (int i = threadIdx.x; i < n4; i += kBlock) m = max(m, abs_bits4(x4[i]));
+  if (threadIdx.x < (c.len & 3)) m = max(m, abs_bits(xc[(n4 << 2) + threadIdx.x]));
   m = block_max(m);
   if (threadIdx.x == 0) partials[blockIdx.x] = m;
 }
@@ -401,41 +460,36 @@ __global__ __launch_bounds__(kBlock) void k_quantize_batched(const float* __rest
                                                              int64_t nchunks, float qmax,
                                                              const uint32_t* __restrict__ partials,
                                                              int8_t* __restrict__ q, float* __restrict__ scales) {
-  const int64_t ci = nchunks - 1 - (int64_t)blockIdx.x;  // reverse of pass 1 (Infinity Cache reuse)
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kWaves][kTile / 4];
+  const int64_t ci = nchunks - 1 - (int64_t)blockIdx.x;  // reverse of pass 1
   const adfl_slq_chunk c = chunks[ci];
   const ScaleInv si = make_scale(reduce_partials(partials + c.first_chunk, c.nchunks), qmax);
   if (ci == c.first_chunk && threadIdx.x == 0) scales[c.tensor] = si.scale;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const float* xc = x + c.start;
   int8_t* qc = q + c.start;
-  const float4* x4 = reinterpret_cast<const float4*>(xc);
-  uint4* q16 = reinterpret_cast<uint4*>(qc);
-  const int ng = c.len >> 4;
-  for (int g = threadIdx.x; g < ng; g += kBlock) {
-    const float4 a = x4[4 * g], b = x4[4 * g + 1], d = x4[4 * g + 2], e = x4[4 * g + 3];
-    q16[g] = make_uint4(quant4(a, si.inv), quant4(b, si.inv), quant4(d, si.inv), quant4(e, si.inv));
-  }
-  for (int i = (ng << 4) + threadIdx.x; i < c.len; i += kBlock) qc[i] = (int8_t)quant1(xc[i], si.inv);
+  const int ntiles = c.len / kTile;
+  for (int t = wave; t < ntiles; t += kWaves)
+    quantize_tile(reinterpret_cast<const float4*>(xc) + t * (kTile / 4), reinterpret_cast<uint4*>(qc) + t * (kTile / 16),
+                  si.inv, lds[wave], lane);
+  for (int i = ntiles * kTile + threadIdx.x; i < c.len; i += kBlock) qc[i] = (int8_t)quant1(xc[i], si.inv);
 }
 
 __global__ __launch_bounds__(kBlock) void k_dequantize_batched(const int8_t* __restrict__ q,
                                                                const adfl_slq_chunk* __restrict__ chunks,
                                                                const float* __restrict__ scales,
                                                                float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kWaves][kTile / 4];
   const adfl_slq_chunk c = chunks[blockIdx.x];
   const float s = scales[c.tensor];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int8_t* qc = q + c.start;
   float* oc = out + c.start;
-  const uint4* q16 = reinterpret_cast<const uint4*>(qc);
-  float4* o4 = reinterpret_cast<float4*>(oc);
-  const int ng = c.len >> 4;
-  for (int g = threadIdx.x; g < ng; g += kBlock) {
-    const uint4 p = q16[g];
-    o4[4 * g] = dequant4(p.x, s);
-    o4[4 * g + 1] = dequant4(p.y, s);
-    o4[4 * g + 2] = dequant4(p.z, s);
-    o4[4 * g + 3] = dequant4(p.w, s);
-  }
-  for (int i = (ng << 4) + threadIdx.x; i < c.len; i += kBlock) oc[i] = s * (float)qc[i];
+  const int ntiles = c.len / kTile;
+  for (int t = wave; t < ntiles; t += kWaves)
+    dequantize_tile(reinterpret_cast<const uint4*>(qc) + t * (kTile / 16), reinterpret_cast<float4*>(oc) + t * (kTile / 4),
+                    s, lds[wave], lane);
+  for (int i = ntiles * kTile + threadIdx.x; i < c.len; i += kBlock) oc[i] = s * (float)qc[i];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -443,11 +497,12 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_batched(const int8_t* __r
 // ------------------------------------------------------------------------------------------------
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-inline int grid_for(int64_t work_items) {
-  int64_t g = (work_items + kBlock - 1) / kBlock;
-  if (g < 1) g = 1;
-  return (int)(g > kMaxFlatBlocks ? kMaxFlatBlocks : g);
-}
+inline int clamp_grid(int64_t g, int cap) { return (int)(g < 1 ? 1 : (g > cap ? cap : g)); }
+
+// grid for a wave-tile kernel over `tiles` tiles (4 tiles per block per sweep)
+inline int tile_grid(int64_t tiles) { return clamp_grid((tiles + kWaves - 1) / kWaves, kMaxFlatBlocks); }
+
+inline int absmax_grid(int64_t n) { return clamp_grid((n >> 2) / (8 * kBlock), kAbsmaxBlocks); }
 
 inline int check_bits(int bits) { return (bits >= 1 && bits <= 16) ? ADFL_OK : ADFL_E_BITS; }
 
@@ -458,9 +513,6 @@ inline int launch_status() {
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? ADFL_OK : (int)e;
 }
-
-// Pass-1 grid for a flat tensor: the partial count pass 2 must reduce.
-inline int absmax_grid(int64_t n) { return grid_for(((n >> 2) + 3) / 4); }
 
 }  // namespace
 
@@ -488,8 +540,8 @@ int adfl_slq_absmax(const float* d_x, int64_t n, void* d_workspace, int64_t work
   if (!d_x || !d_workspace || n < 1) return ADFL_E_ARG;
   if (!aligned16(d_x) || !aligned16(d_workspace)) return ADFL_E_ALIGN;
   if (workspace_bytes < kWorkspaceBytes) return ADFL_E_WORKSPACE;
-  hipLaunchKernelGGL(k_absmax_flat<4>, dim3(absmax_grid(n)), dim3(kBlock), 0, (hipStream_t)stream, d_x, n,
-                     (uint32_t*)d_workspace);
+  hipLaunchKernelGGL(k_absmax_flat, dim3(absmax_grid(n)), dim3(kBlock), 0, (hipStream_t)stream, d_x, n,
+                     (int64_t)(kCacheKeepBytes / 16), (uint32_t*)d_workspace);
   return launch_status();
 }
 
@@ -498,7 +550,7 @@ int adfl_slq_quantize(const float* d_x, int64_t n, int bits, const void* d_works
   if (!d_x || !d_workspace || !d_q || !d_scale || n < 1) return ADFL_E_ARG;
   if (int s = check_bits(bits)) return s;
   if (!aligned16(d_x) || !aligned16(d_q)) return ADFL_E_ALIGN;
-  hipLaunchKernelGGL(k_quantize_flat<true>, dim3(grid_for(n >> 4)), dim3(kBlock), 0, (hipStream_t)stream, d_x, n,
+  hipLaunchKernelGGL(k_quantize_flat, dim3(tile_grid(n / kTile)), dim3(kBlock), 0, (hipStream_t)stream, d_x, n,
                      qmax_f(bits), (const uint32_t*)d_workspace, d_q, d_scale);
   return launch_status();
 }
@@ -513,7 +565,7 @@ int adfl_slq_encode(const float* d_x, int64_t n, int bits, int8_t* d_q, float* d
 int adfl_slq_dequantize(const int8_t* d_q, int64_t n, const float* d_scale, float* d_out, void* stream) {
   if (!d_q || !d_scale || !d_out || n < 1) return ADFL_E_ARG;
   if (!aligned16(d_q) || !aligned16(d_out)) return ADFL_E_ALIGN;
-  hipLaunchKernelGGL(k_dequantize_flat<false>, dim3(grid_for(n >> 4)), dim3(kBlock), 0, (hipStream_t)stream, d_q, n,
+  hipLaunchKernelGGL(k_dequantize_flat, dim3(tile_grid(n / kTile)), dim3(kBlock), 0, (hipStream_t)stream, d_q, n,
                      d_scale, d_out);
   return launch_status();
 }
@@ -570,8 +622,8 @@ int adfl_slq_quantize_int4(const float* d_x, int64_t n, int bits, const void* d_
   if (!d_x || !d_workspace || !d_packed || !d_scale || n < 1) return ADFL_E_ARG;
   if (int s = check_bits(bits)) return s;
   if (!aligned16(d_x) || !aligned16(d_packed)) return ADFL_E_ALIGN;
-  hipLaunchKernelGGL(k_quantize_int4_flat<true>, dim3(grid_for(n >> 5)), dim3(kBlock), 0, (hipStream_t)stream, d_x,
-                     n, qmax_f(bits), (const uint32_t*)d_workspace, d_packed, d_scale);
+  hipLaunchKernelGGL(k_quantize_int4_flat, dim3(tile_grid(n / kTile4)), dim3(kBlock), 0, (hipStream_t)stream, d_x, n,
+                     qmax_f(bits), (const uint32_t*)d_workspace, d_packed, d_scale);
   return launch_status();
 }
 
@@ -585,21 +637,22 @@ int adfl_slq_encode_int4(const float* d_x, int64_t n, int bits, uint8_t* d_packe
 int adfl_slq_dequantize_int4(const uint8_t* d_packed, int64_t n, const float* d_scale, float* d_out, void* stream) {
   if (!d_packed || !d_scale || !d_out || n < 1) return ADFL_E_ARG;
   if (!aligned16(d_packed) || !aligned16(d_out)) return ADFL_E_ALIGN;
-  hipLaunchKernelGGL(k_dequantize_int4_flat<false>, dim3(grid_for(n >> 5)), dim3(kBlock), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(k_dequantize_int4_flat, dim3(tile_grid(n / kTile4)), dim3(kBlock), 0, (hipStream_t)stream,
                      d_packed, n, d_scale, d_out);
   return launch_status();
 }
 
 int adfl_pack_int4(const int8_t* d_q, int64_t n, uint8_t* d_packed, void* stream) {
   if (!d_q || !d_packed || n < 1) return ADFL_E_ARG;
-  hipLaunchKernelGGL(k_pack_int4, dim3(grid_for((n + 1) >> 1)), dim3(kBlock), 0, (hipStream_t)stream, d_q, n,
-                     d_packed);
+  hipLaunchKernelGGL(k_pack_int4, dim3(clamp_grid((((n + 1) >> 1) + kBlock - 1) / kBlock, kMaxFlatBlocks)),
+                     dim3(kBlock), 0, (hipStream_t)stream, d_q, n, d_packed);
   return launch_status();
 }
 
 int adfl_unpack_int4(const uint8_t* d_packed, int64_t n, int8_t* d_q, void* stream) {
   if (!d_packed || !d_q || n < 1) return ADFL_E_ARG;
-  hipLaunchKernelGGL(k_unpack_int4, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, d_packed, n, d_q);
+  hipLaunchKernelGGL(k_unpack_int4, dim3(clamp_grid((n + kBlock - 1) / kBlock, kMaxFlatBlocks)), dim3(kBlock), 0,
+                     (hipStream_t)stream, d_packed, n, d_q);
   return launch_status();
 }
 
@@ -607,7 +660,7 @@ int adfl_slq_dequantize_mean(const int8_t* d_q, int64_t row_stride_bytes, int32_
                              const float* d_scales, int64_t scale_stride, float* d_out, void* stream) {
   if (!d_q || !d_scales || !d_out || n < 1 || k < 1 || row_stride_bytes < n || scale_stride < 1) return ADFL_E_ARG;
   if (!aligned16(d_q) || !aligned16(d_out) || (row_stride_bytes & 15) != 0) return ADFL_E_ALIGN;
-  hipLaunchKernelGGL(k_dequantize_mean, dim3(grid_for(n >> 4)), dim3(kBlock), 0, (hipStream_t)stream, d_q,
+  hipLaunchKernelGGL(k_dequantize_mean, dim3(tile_grid(n / kTile)), dim3(kBlock), 0, (hipStream_t)stream, d_q,
                      row_stride_bytes, (int)k, n, d_scales, scale_stride, d_out);
   return launch_status();
 }
@@ -617,8 +670,8 @@ int adfl_slq_dequantize_mean_int4(const uint8_t* d_packed, int64_t row_stride_by
   if (!d_packed || !d_scales || !d_out || n < 1 || k < 1 || row_stride_bytes < (n + 1) / 2 || scale_stride < 1)
     return ADFL_E_ARG;
   if (!aligned16(d_packed) || !aligned16(d_out) || (row_stride_bytes & 15) != 0) return ADFL_E_ALIGN;
-  hipLaunchKernelGGL(k_dequantize_mean_int4, dim3(grid_for(n >> 5)), dim3(kBlock), 0, (hipStream_t)stream, d_packed,
-                     row_stride_bytes, (int)k, n, d_scales, scale_stride, d_out);
+  hipLaunchKernelGGL(k_dequantize_mean_int4, dim3(tile_grid(n / kTile4)), dim3(kBlock), 0, (hipStream_t)stream,
+                     d_packed, row_stride_bytes, (int)k, n, d_scales, scale_stride, d_out);
   return launch_status();
 }
 
