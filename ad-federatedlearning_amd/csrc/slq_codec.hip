@@ -18,12 +18,11 @@
 //    pass 1 writes one absmax partial per block, pass 2 re-reduces them (<= 8 KiB, L2) in every block's
 //    prologue. No atomics, no in-launch hand-off, deterministic.
 //  * Cache policy per stream (MI355X 256 MiB Infinity Cache): pass 1 reads x block-contiguously with
-//    non-temporal loads except for the last kCacheKeepBytes, which it reads with allocating loads;
-//    pass 2 walks x backwards, so it starts on exactly those bytes. Pass 2 reads x non-temporally
-//    (x is dead afterwards) and writes the payload backwards with allocating stores; decode reads the
-//    payload forwards, starting on the bytes pass 2 wrote last. Decode writes its fp32 output with
-//    non-temporal stores (nothing re-reads it soon; it must not evict the next pass's lines).
-//    None of this changes a single output bit.
+//    non-temporal loads (kCacheKeepBytes = 0: keeping x's tail on-die for pass 2 measured slower).
+//    Pass 2 reads x non-temporally (x is dead afterwards) and writes the payload backwards with
+//    allocating stores; decode reads the payload forwards, starting on the bytes pass 2 wrote last,
+//    which are still in the Infinity Cache. Decode writes its fp32 output with non-temporal stores
+//    (nothing re-reads it soon; it must not evict the next pass's lines). No output bit depends on it.
 //
 // Numerics: no fast-math, fp32 denormals preserved (gfx950 default), -ffp-contract=off. Scale and
 // reciprocal are fp64 quotients rounded once to fp32 = the correctly rounded fp32 quotient (53 >= 2*24+2),
@@ -46,7 +45,7 @@ constexpr int kMaxFlatBlocks = 2048;               // 256 CUs x 8 resident 256-t
 constexpr int kAbsmaxBlocks = 1024;                // pass-1 grid (block-contiguous ranges)
 constexpr int kCountSlot = kMaxFlatBlocks;         // workspace word holding pass 1's partial count
 constexpr int64_t kWorkspaceBytes = 16384;         // >= (kMaxFlatBlocks + 1) * 4, padded
-constexpr int64_t kCacheKeepBytes = 192ll << 20;   // tail of x pass 1 leaves in the Infinity Cache
+constexpr int64_t kCacheKeepBytes = 0;             // tail of x pass 1 leaves in the Infinity Cache
 
 typedef float f4v __attribute__((ext_vector_type(4)));
 
@@ -60,6 +59,26 @@ __device__ __forceinline__ float4 load4(const float4* p) {
     return make_float4(v.x, v.y, v.z, v.w);
   }
   return *p;
+}
+
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ uint4 load16(const uint4* p) {
+  if (NT) {
+    const u4v v = __builtin_nontemporal_load(reinterpret_cast<const u4v*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  }
+  return *p;
+}
+
+template <bool NT>
+__device__ __forceinline__ void store16(uint4* p, uint4 d) {
+  if (NT) {
+    const u4v v = {d.x, d.y, d.z, d.w};
+    __builtin_nontemporal_store(v, reinterpret_cast<u4v*>(p));
+  } else {
+    *p = d;
+  }
 }
 
 __device__ __forceinline__ void store4_nt(float4* p, float4 d) {
@@ -177,22 +196,34 @@ __device__ __forceinline__ uint32_t reduce_partials(const uint32_t* __restrict__
 //   lane l, instruction j in 0..3 of an int8 tile: elements 4*(j*64 + l) .. +3 (float4 j*64+l), whose
 //   payload is dword j*64+l of the tile's 1 KiB; the LDS transpose hands lane l dwords 4l..4l+3.
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ void quantize_tile(const float4* __restrict__ x4, uint4* __restrict__ q16, float inv,
-                                              uint32_t* __restrict__ lds, int lane) {
-  float4 v[4];
+__device__ __forceinline__ void load_tile(const float4* __restrict__ x4, float4 (&v)[4], int lane) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) v[j] = load4<true>(x4 + j * 64 + lane);
+}
+
+template <bool ST_NT = false>
+__device__ __forceinline__ void quantize_tile_regs(const float4 (&v)[4], uint4* __restrict__ q16, float inv,
+                                                   uint32_t* __restrict__ lds, int lane) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) lds[j * 64 + lane] = quant4(v[j], inv);
   __builtin_amdgcn_wave_barrier();
   const uint4 o = reinterpret_cast<const uint4*>(lds)[lane];
   __builtin_amdgcn_wave_barrier();
-  q16[lane] = o;
+  store16<ST_NT>(q16 + lane, o);
 }
 
+template <bool ST_NT = false>
+__device__ __forceinline__ void quantize_tile(const float4* __restrict__ x4, uint4* __restrict__ q16, float inv,
+                                              uint32_t* __restrict__ lds, int lane) {
+  float4 v[4];
+  load_tile(x4, v, lane);
+  quantize_tile_regs<ST_NT>(v, q16, inv, lds, lane);
+}
+
+template <bool LD_NT = false>
 __device__ __forceinline__ void dequantize_tile(const uint4* __restrict__ q16, float4* __restrict__ o4, float s,
                                                 uint32_t* __restrict__ lds, int lane) {
-  reinterpret_cast<uint4*>(lds)[lane] = q16[lane];
+  reinterpret_cast<uint4*>(lds)[lane] = load16<LD_NT>(q16 + lane);
   __builtin_amdgcn_wave_barrier();
   uint32_t w[4];
 #pragma unroll
@@ -221,7 +252,10 @@ __device__ __forceinline__ uint32_t absmax_range(const float4* __restrict__ x4, 
 }
 
 // Pass 1: block b owns float4s [b*per, (b+1)*per). Blocks wholly before the last keep4 float4s read
-// non-temporally; the rest with allocating loads (they stay in the Infinity Cache for pass 2).
+// non-temporally; the rest with allocating loads (they stay in the Infinity Cache for pass 2). The
+// product uses keep4 = 0 (kCacheKeepBytes): measured, the non-temporal read's speed-up outweighs what
+// pass 2 gains from finding x's tail on-die (profiles/r01/microbench_keep_sweep.txt).
+template <int U>
 __global__ __launch_bounds__(kBlock) void k_absmax_flat(const float* __restrict__ x, int64_t n, int64_t keep4,
                                                         uint32_t* __restrict__ partials) {
   const float4* x4 = reinterpret_cast<const float4*>(x);
@@ -229,34 +263,43 @@ __global__ __launch_bounds__(kBlock) void k_absmax_flat(const float* __restrict_
   const int64_t per = ((n4 + gridDim.x - 1) / gridDim.x + kBlock - 1) / kBlock * kBlock;
   const int64_t b0 = (int64_t)blockIdx.x * per;
   const int64_t b1 = min(n4, b0 + per);
-  uint32_t m = (b1 <= n4 - keep4) ? absmax_range<8, true>(x4, b0, b1) : absmax_range<8, false>(x4, b0, b1);
+  uint32_t m = (b1 <= n4 - keep4) ? absmax_range<U, true>(x4, b0, b1) : absmax_range<U, false>(x4, b0, b1);
   if (blockIdx.x == 0 && threadIdx.x < (n & 3)) m = max(m, abs_bits(x[(n4 << 2) + threadIdx.x]));
   m = block_max(m);
   if (threadIdx.x == 0) partials[blockIdx.x] = m;
   if (blockIdx.x == 0 && threadIdx.x == 0) partials[kCountSlot] = gridDim.x;  // self-describing workspace
 }
 
-// Pass 2: tiles walked from the END of x (Infinity Cache reuse of pass 1's tail).
+// Pass 2: tiles walked from the END of x, so decode (which walks forwards) starts on the payload bytes
+// written last. Template knobs exist for tools/microbench.hip; the ABI uses <true, false>.
+template <bool REVERSE, bool ST_NT>
 __global__ __launch_bounds__(kBlock) void k_quantize_flat(const float* __restrict__ x, int64_t n, float qmax,
                                                           const uint32_t* __restrict__ partials,
                                                           int8_t* __restrict__ q, float* __restrict__ scale_out) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kWaves][kTile / 4];
-  const ScaleInv si = make_scale(reduce_partials(partials, (int)partials[kCountSlot]), qmax);
-  if (blockIdx.x == 0 && threadIdx.x == 0) *scale_out = si.scale;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const float4* x4 = reinterpret_cast<const float4*>(x);
   uint4* q16 = reinterpret_cast<uint4*>(q);
   const int64_t ntiles = n / kTile;
   const int64_t wstride = (int64_t)gridDim.x * kWaves;
-  for (int64_t t0 = (int64_t)blockIdx.x * kWaves + wave; t0 < ntiles; t0 += wstride) {
-    const int64_t t = ntiles - 1 - t0;
-    quantize_tile(x4 + t * (kTile / 4), q16 + t * (kTile / 16), si.inv, lds[wave], lane);
+  int64_t t0 = (int64_t)blockIdx.x * kWaves + wave;
+  // The first tile's loads do not need the scale: issue them before the partial reduction, whose
+  // latency they then hide.
+  float4 v[4];
+  if (t0 < ntiles) load_tile(x4 + (REVERSE ? ntiles - 1 - t0 : t0) * (kTile / 4), v, lane);
+  const ScaleInv si = make_scale(reduce_partials(partials, (int)partials[kCountSlot]), qmax);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *scale_out = si.scale;
+  for (; t0 < ntiles; t0 += wstride) {
+    const int64_t t = REVERSE ? ntiles - 1 - t0 : t0;
+    if (t0 != (int64_t)blockIdx.x * kWaves + wave) load_tile(x4 + t * (kTile / 4), v, lane);
+    quantize_tile_regs<ST_NT>(v, q16 + t * (kTile / 16), si.inv, lds[wave], lane);
   }
   if (blockIdx.x == gridDim.x - 1)
     for (int64_t i = ntiles * kTile + threadIdx.x; i < n; i += kBlock) q[i] = (int8_t)quant1(x[i], si.inv);
 }
 
-// Decode: tiles walked forwards (pass 2 wrote the head of the payload last).
+// Decode: tiles walked forwards (pass 2 wrote the head of the payload last). ABI: <false, false>.
+template <bool REVERSE, bool LD_NT>
 __global__ __launch_bounds__(kBlock) void k_dequantize_flat(const int8_t* __restrict__ q, int64_t n,
                                                             const float* __restrict__ scale_p,
                                                             float* __restrict__ out) {
@@ -267,8 +310,10 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_flat(const int8_t* __rest
   float4* o4 = reinterpret_cast<float4*>(out);
   const int64_t ntiles = n / kTile;
   const int64_t wstride = (int64_t)gridDim.x * kWaves;
-  for (int64_t t = (int64_t)blockIdx.x * kWaves + wave; t < ntiles; t += wstride)
-    dequantize_tile(q16 + t * (kTile / 16), o4 + t * (kTile / 4), s, lds[wave], lane);
+  for (int64_t t0 = (int64_t)blockIdx.x * kWaves + wave; t0 < ntiles; t0 += wstride) {
+    const int64_t t = REVERSE ? ntiles - 1 - t0 : t0;
+    dequantize_tile<LD_NT>(q16 + t * (kTile / 16), o4 + t * (kTile / 4), s, lds[wave], lane);
+  }
   if (blockIdx.x == gridDim.x - 1)
     for (int64_t i = ntiles * kTile + threadIdx.x; i < n; i += kBlock) out[i] = s * (float)q[i];
 }
@@ -540,7 +585,7 @@ int adfl_slq_absmax(const float* d_x, int64_t n, void* d_workspace, int64_t work
   if (!d_x || !d_workspace || n < 1) return ADFL_E_ARG;
   if (!aligned16(d_x) || !aligned16(d_workspace)) return ADFL_E_ALIGN;
   if (workspace_bytes < kWorkspaceBytes) return ADFL_E_WORKSPACE;
-  hipLaunchKernelGGL(k_absmax_flat, dim3(absmax_grid(n)), dim3(kBlock), 0, (hipStream_t)stream, d_x, n,
+  hipLaunchKernelGGL(k_absmax_flat<8>, dim3(absmax_grid(n)), dim3(kBlock), 0, (hipStream_t)stream, d_x, n,
                      (int64_t)(kCacheKeepBytes / 16), (uint32_t*)d_workspace);
   return launch_status();
 }
@@ -550,7 +595,7 @@ int adfl_slq_quantize(const float* d_x, int64_t n, int bits, const void* d_works
   if (!d_x || !d_workspace || !d_q || !d_scale || n < 1) return ADFL_E_ARG;
   if (int s = check_bits(bits)) return s;
   if (!aligned16(d_x) || !aligned16(d_q)) return ADFL_E_ALIGN;
-  hipLaunchKernelGGL(k_quantize_flat, dim3(tile_grid(n / kTile)), dim3(kBlock), 0, (hipStream_t)stream, d_x, n,
+  hipLaunchKernelGGL((k_quantize_flat<true, false>), dim3(tile_grid(n / kTile)), dim3(kBlock), 0, (hipStream_t)stream, d_x, n,
                      qmax_f(bits), (const uint32_t*)d_workspace, d_q, d_scale);
   return launch_status();
 }
@@ -565,7 +610,7 @@ int adfl_slq_encode(const float* d_x, int64_t n, int bits, int8_t* d_q, float* d
 int adfl_slq_dequantize(const int8_t* d_q, int64_t n, const float* d_scale, float* d_out, void* stream) {
   if (!d_q || !d_scale || !d_out || n < 1) return ADFL_E_ARG;
   if (!aligned16(d_q) || !aligned16(d_out)) return ADFL_E_ALIGN;
-  hipLaunchKernelGGL(k_dequantize_flat, dim3(tile_grid(n / kTile)), dim3(kBlock), 0, (hipStream_t)stream, d_q, n,
+  hipLaunchKernelGGL((k_dequantize_flat<false, false>), dim3(tile_grid(n / kTile)), dim3(kBlock), 0, (hipStream_t)stream, d_q, n,
                      d_scale, d_out);
   return launch_status();
 }

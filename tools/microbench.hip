@@ -38,6 +38,94 @@ __global__ __launch_bounds__(256) void k_write_nt(float4* __restrict__ out, int6
   const int64_t s = (int64_t)gridDim.x * 256;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += s) store4_nt(out + i, make_float4(1.f, 2.f, 3.f, 4.f));
 }
+// quantize with the first tiles' loads issued before the partial reduction (hides its latency) and UT
+// tiles in flight per wave iteration.
+template <int UT, bool PREFETCH>
+__global__ __launch_bounds__(kBlock) void k_quant_pf(const float* __restrict__ x, int64_t n, float qmax,
+                                                    const uint32_t* __restrict__ partials, int8_t* __restrict__ q,
+                                                    float* __restrict__ scale_out) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kWaves][UT][kTile / 4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  uint4* q16 = reinterpret_cast<uint4*>(q);
+  const int64_t ntiles = n / kTile;
+  const int64_t wstride = (int64_t)gridDim.x * kWaves * UT;
+  int64_t t0 = ((int64_t)blockIdx.x * kWaves + wave) * UT;
+  float4 v[UT][4];
+  auto issue = [&](int64_t tb) {
+#pragma unroll
+    for (int u = 0; u < UT; ++u)
+      if (tb + u < ntiles) {
+        const int64_t t = ntiles - 1 - (tb + u);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[u][j] = load4<true>(x4 + t * 256 + j * 64 + lane);
+      }
+  };
+  if (PREFETCH) issue(t0);
+  const ScaleInv si = make_scale(reduce_partials(partials, (int)partials[kCountSlot]), qmax);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *scale_out = si.scale;
+  if (!PREFETCH) issue(t0);
+  for (; t0 < ntiles; t0 += wstride) {
+#pragma unroll
+    for (int u = 0; u < UT; ++u)
+      if (t0 + u < ntiles) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) lds[wave][u][j * 64 + lane] = quant4(v[u][j], si.inv);
+      }
+    __builtin_amdgcn_wave_barrier();
+    uint4 o[UT];
+#pragma unroll
+    for (int u = 0; u < UT; ++u) o[u] = reinterpret_cast<const uint4*>(lds[wave][u])[lane];
+    __builtin_amdgcn_wave_barrier();
+    issue(t0 + wstride);  // next iteration's loads before this iteration's stores
+#pragma unroll
+    for (int u = 0; u < UT; ++u)
+      if (t0 + u < ntiles) q16[(ntiles - 1 - (t0 + u)) * 64 + lane] = o[u];
+  }
+  if (blockIdx.x == gridDim.x - 1)
+    for (int64_t i = ntiles * kTile + threadIdx.x; i < n; i += kBlock) q[i] = (int8_t)quant1(x[i], si.inv);
+}
+
+// dequantize with the next tile's payload load issued before the current tile's stores.
+template <int UT>
+__global__ __launch_bounds__(kBlock) void k_deq_pf(const int8_t* __restrict__ q, int64_t n, const float* __restrict__ scale_p,
+                                                  float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kWaves][UT][kTile / 4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint4* q16 = reinterpret_cast<const uint4*>(q);
+  float4* o4 = reinterpret_cast<float4*>(out);
+  const int64_t ntiles = n / kTile;
+  const int64_t wstride = (int64_t)gridDim.x * kWaves * UT;
+  int64_t t0 = ((int64_t)blockIdx.x * kWaves + wave) * UT;
+  uint4 p[UT];
+  auto issue = [&](int64_t tb) {
+#pragma unroll
+    for (int u = 0; u < UT; ++u)
+      if (tb + u < ntiles) p[u] = q16[(tb + u) * 64 + lane];
+  };
+  issue(t0);
+  const float s = *scale_p;
+  for (; t0 < ntiles; t0 += wstride) {
+#pragma unroll
+    for (int u = 0; u < UT; ++u) reinterpret_cast<uint4*>(lds[wave][u])[lane] = p[u];
+    __builtin_amdgcn_wave_barrier();
+    uint32_t w[UT][4];
+#pragma unroll
+    for (int u = 0; u < UT; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[u][j] = lds[wave][u][j * 64 + lane];
+    __builtin_amdgcn_wave_barrier();
+    issue(t0 + wstride);
+#pragma unroll
+    for (int u = 0; u < UT; ++u)
+      if (t0 + u < ntiles) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) store4_nt(o4 + (t0 + u) * 256 + j * 64 + lane, dequant4(w[u][j], s));
+      }
+  }
+  if (blockIdx.x == gridDim.x - 1)
+    for (int64_t i = ntiles * kTile + threadIdx.x; i < n; i += kBlock) out[i] = s * (float)q[i];
+}
 }  // namespace mb
 
 static float med(std::vector<float> v) {
@@ -77,31 +165,81 @@ int main(int argc, char** argv) {
     return t;
   };
 
-  // ---- 1. KEEP sweep on the int8 round trip (absmax -> quantize -> dequantize)
-  std::vector<int64_t> keeps = {0, 64ll << 20, 128ll << 20, 192ll << 20, 256ll << 20, n * 4};
+  // ---- 1. variant matrix on the int8 round trip (absmax -> quantize -> dequantize)
+  using L = std::function<void()>;
+  struct V { std::string name; L fn; };
+  const int tg = tile_grid(n / kTile);
+  auto agrid = [&](int cap) { return clamp_grid((n >> 2) / (8 * kBlock), cap); };
+  std::vector<V> A = {
+      {"abs_U8_g1024", [&] { hipLaunchKernelGGL(k_absmax_flat<8>, dim3(agrid(1024)), dim3(kBlock), 0, st, x, n, (int64_t)0, ws); }},
+  };
+  std::vector<V> Q = {
+      {"q_rev", [&] { hipLaunchKernelGGL((k_quantize_flat<true, false>), dim3(tg), dim3(kBlock), 0, st, x, n, 127.f, ws, q, scale); }},
+      {"q_pf1", [&] { hipLaunchKernelGGL((mb::k_quant_pf<1, true>), dim3(tg), dim3(kBlock), 0, st, x, n, 127.f, ws, q, scale); }},
+      {"q_pf2", [&] { hipLaunchKernelGGL((mb::k_quant_pf<2, true>), dim3(tg), dim3(kBlock), 0, st, x, n, 127.f, ws, q, scale); }},
+      {"q_nopf2", [&] { hipLaunchKernelGGL((mb::k_quant_pf<2, false>), dim3(tg), dim3(kBlock), 0, st, x, n, 127.f, ws, q, scale); }},
+      {"q_pf2_g1024", [&] { hipLaunchKernelGGL((mb::k_quant_pf<2, true>), dim3(1024), dim3(kBlock), 0, st, x, n, 127.f, ws, q, scale); }},
+      {"q_pf4_g1024", [&] { hipLaunchKernelGGL((mb::k_quant_pf<4, true>), dim3(1024), dim3(kBlock), 0, st, x, n, 127.f, ws, q, scale); }},
+  };
+  std::vector<V> D = {
+      {"d_fwd", [&] { hipLaunchKernelGGL((k_dequantize_flat<false, false>), dim3(tg), dim3(kBlock), 0, st, q, n, scale, out); }},
+      {"d_pf1", [&] { hipLaunchKernelGGL((mb::k_deq_pf<1>), dim3(tg), dim3(kBlock), 0, st, q, n, scale, out); }},
+      {"d_pf2", [&] { hipLaunchKernelGGL((mb::k_deq_pf<2>), dim3(tg), dim3(kBlock), 0, st, q, n, scale, out); }},
+      {"d_pf2_g1024", [&] { hipLaunchKernelGGL((mb::k_deq_pf<2>), dim3(1024), dim3(kBlock), 0, st, q, n, scale, out); }},
+  };
+  {  // correctness of every variant against the product kernels
+    adfl_slq_encode(x, n, 8, q, scale, ws, 16384, st);
+    adfl_slq_dequantize(q, n, scale, out, st);
+    CK(hipStreamSynchronize(st));
+    std::vector<int8_t> q_ref(n), q_h(n);
+    std::vector<float> d_ref(n), d_h(n);
+    CK(hipMemcpy(q_ref.data(), q, n, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(d_ref.data(), out, n * 4, hipMemcpyDeviceToHost));
+    for (auto& v : Q) {
+      CK(hipMemset(q, 0, n));
+      v.fn();
+      CK(hipStreamSynchronize(st));
+      CK(hipMemcpy(q_h.data(), q, n, hipMemcpyDeviceToHost));
+      printf("check %-14s %s\n", v.name.c_str(), memcmp(q_h.data(), q_ref.data(), n) ? "MISMATCH" : "ok");
+    }
+    for (auto& v : D) {
+      CK(hipMemset(out, 0, n * 4));
+      v.fn();
+      CK(hipStreamSynchronize(st));
+      CK(hipMemcpy(d_h.data(), out, n * 4, hipMemcpyDeviceToHost));
+      printf("check %-14s %s\n", v.name.c_str(), memcmp(d_h.data(), d_ref.data(), n * 4) ? "MISMATCH" : "ok");
+    }
+  }
   struct Row { std::string name; std::vector<float> a, q, d; };
   std::vector<Row> rows;
-  for (auto k : keeps) rows.push_back({"keep=" + std::to_string(k >> 20) + "MiB", {}, {}, {}});
-  const int ROUNDS = 6, STEPS = 8;
-  for (int r = 0; r < ROUNDS; ++r)
-    for (size_t i = 0; i < keeps.size(); ++i)
+  for (auto& a : A) for (auto& qk : Q) for (auto& d : D) rows.push_back({a.name + " > " + qk.name + " > " + d.name, {}, {}, {}});
+  const int ROUNDS = 5, STEPS = 6;
+  for (int r = 0; r < ROUNDS; ++r) {
+    size_t i = 0;
+    for (auto& a : A) for (auto& qk : Q) for (auto& d : D) {
       for (int s = 0; s < STEPS; ++s) {
         (void)hipEventRecord(ev[0], st);
-        hipLaunchKernelGGL(k_absmax_flat, dim3(absmax_grid(n)), dim3(kBlock), 0, st, x, n, keeps[i] / 16, ws);
+        a.fn();
         (void)hipEventRecord(ev[1], st);
-        adfl_slq_quantize(x, n, 8, ws, q, scale, st);
+        qk.fn();
         (void)hipEventRecord(ev[2], st);
-        adfl_slq_dequantize(q, n, scale, out, st);
+        d.fn();
         (void)hipEventRecord(ev[3], st);
         CK(hipEventSynchronize(ev[3]));
         rows[i].a.push_back(ms(ev[0], ev[1]));
         rows[i].q.push_back(ms(ev[1], ev[2]));
         rows[i].d.push_back(ms(ev[2], ev[3]));
       }
-  printf("%-20s %8s %8s %8s | %8s %6s\n", "int8 round trip", "absmax", "quant", "deq", "sum ms", "frac");
+      ++i;
+    }
+  }
+  std::sort(rows.begin(), rows.end(), [&](const Row& u, const Row& v) {
+    return med(u.a) + med(u.q) + med(u.d) < med(v.a) + med(v.q) + med(v.d);
+  });
+  printf("%-44s %8s %8s %8s | %8s %6s\n", "int8 round trip", "absmax", "quant", "deq", "sum ms", "frac");
   for (auto& R : rows) {
     const float t = med(R.a) + med(R.q) + med(R.d);
-    printf("%-20s %8.4f %8.4f %8.4f | %8.4f %6.3f\n", R.name.c_str(), med(R.a), med(R.q), med(R.d), t,
+    printf("%-44s %8.4f %8.4f %8.4f | %8.4f %6.3f\n", R.name.c_str(), med(R.a), med(R.q), med(R.d), t,
            14.0 * gb / (t * 1e-3) / 8000.0);
   }
 
