@@ -1,0 +1,67 @@
+"""GPU: the peer exchange's HIP path (HipCodec + RCCL all-gather + fused decode-mean) on one rank.
+
+Multi-rank behaviour of the protocol is covered by tests/test_exchange_gloo.py (world_size 2, gloo,
+oracle codec); here the real device codec and the RCCL collective run end to end (world_size 1 on the
+single-GPU test box), and the rows a K-rank gather would deliver are fed to the mean kernel directly."""
+
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+
+import slq_oracle as oracle
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module")
+def rccl_world1():
+    pytest.importorskip("adfl_amd")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=DEV)
+    yield
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("numel,bits,packed,chunks", [(1 << 20, 8, False, 1), (1000003, 8, False, 3),
+                                                      (1 << 22, 4, True, 4), (4097, 4, True, 2),
+                                                      (70000, 2, False, 1)])
+def test_exchange_world1_matches_oracle(rccl_world1, numel, bits, packed, chunks):
+    from adfl_amd.exchange import PeerExchange
+    rng = np.random.default_rng(numel)
+    x = rng.standard_normal(numel, dtype=np.float32) * np.float32(1e-3)
+    ex = PeerExchange(numel, bits=bits, packed=packed, chunks=chunks, device=DEV)
+    got = ex.exchange_mean(torch.from_numpy(x).to(DEV)).cpu().numpy()
+    q, s = oracle.encode(x, bits)
+    want = oracle.decode_int4(oracle.pack_int4(q), numel, s) if packed else oracle.decode(q, s)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    # the gathered message rows carry payload + scale exactly as the protocol lays them out
+    for (c0, c1), rows, pb in zip(ex.bounds, ex.gathered, ex.payload):
+        r = rows.cpu().numpy()[0]
+        scale = r[(pb + 15) // 16 * 16:(pb + 15) // 16 * 16 + 4].view(np.float32)[0]
+        assert np.float32(scale).view(np.uint32) == np.float32(s).view(np.uint32)
+
+
+def test_exchange_k8_rows_mean(rccl_world1):
+    """What rank r computes after an 8-way gather: decode-mean over 8 rows of a real exchange layout."""
+    from adfl_amd import ops
+    k, n = 8, 300007
+    rng = np.random.default_rng(8)
+    xs = [rng.standard_normal(n, dtype=np.float32) * np.float32(10.0 ** -r) for r in range(k)]
+    enc = [oracle.encode(x, 8) for x in xs]
+    row = (n + 15) // 16 * 16 + 16
+    rows = np.zeros((k, row), np.uint8)
+    for r, (q, s) in enumerate(enc):
+        rows[r, :n] = q.view(np.uint8)
+        rows[r, row - 16:row - 12] = np.array([s], np.float32).view(np.uint8)
+    rows_d = torch.from_numpy(rows).to(DEV)
+    scales = rows_d[:, row - 16:].view(torch.float32)[:, :1]
+    got = ops.dequantize_mean(rows_d.view(torch.int8), scales.contiguous(), n).cpu().numpy()
+    want = oracle.dequantize_mean([q for q, _ in enc], [s for _, s in enc])
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))

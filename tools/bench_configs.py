@@ -1,0 +1,226 @@
+"""Secondary measurements for BASELINE.json's other configs (one JSON line each).
+
+bench.py measures the headline (C2). This tool measures the rest on the same codec:
+
+  c3        ResNet-18-sized update: 11,689,512 fp32 in 256 tensors, per-tensor scales, bucketed
+            (one launch per pass), device-resident; with and without an Infinity-Cache flush
+  c5_int4   4 GiB fp32 gradient per GPU (2^30 elements), SLQ bits=4 with pack_4bit layout,
+            device-resident round trip (13 B/element algorithmic)
+  exchange  one simulated client per GPU: encode -> RCCL all-gather -> fused decode+mean
+            (--packed --chunks 8 --elems 1073741824 for C5's int4 pipelined variant). torchrun N>1.
+  pcie      the same 1 GiB round trip starting and ending in pinned host memory
+            (H2D 4N, D2H N, H2D N, D2H 4N), the rate DESIGN.md reports next to the device-resident one
+
+    python tools/bench_configs.py --mode c3
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 tools/bench_configs.py --mode exchange
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "ad-federatedlearning_amd"))
+
+from bench import GIB, HBM_PEAK_GBS, barrier, dist_setup, max_over_ranks  # noqa: E402
+
+RESNET18 = 11_689_512
+
+
+def events(k):
+    return [[torch.cuda.Event(enable_timing=True) for _ in range(k)] for _ in range(2)]
+
+
+def timed(step, steps, warmup, world, nev):
+    """Run `step(ev)` (ev: list of nev events to record, or None) warmup+steps times; return
+    (max-over-ranks wall seconds for `steps`, per-step event lists)."""
+    for _ in range(warmup):
+        step(None)
+    torch.cuda.synchronize()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(nev)] for _ in range(steps)]
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    barrier(world)
+    return max_over_ranks(time.perf_counter() - t0, world), evs
+
+
+def seg_ms(evs, i, j):
+    return sum(e[i].elapsed_time(e[j]) for e in evs) / len(evs)
+
+
+def mode_c3(args, world, rank, dev):
+    from adfl_amd import _lib, ops
+    lib = _lib.load()
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    base, rem = divmod(RESNET18, 256)
+    sizes = [base + (1 if i < rem else 0) for i in range(256)]
+    lay = ops.BucketLayout(sizes)
+    g = torch.Generator(device=dev).manual_seed(rank)
+    x = torch.randn(lay.total, device=dev, generator=g) * 1e-3
+    q = torch.empty(lay.total, dtype=torch.int8, device=dev)
+    scales = torch.empty(lay.ntensors, device=dev)
+    partials = torch.empty(lay.nchunks, dtype=torch.int32, device=dev)
+    out = torch.empty(lay.total, device=dev)
+    chunks = lay.device_chunks(dev)
+    junk = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
+    res = {}
+    for flush in (False, True):
+        def step(ev):
+            if flush:
+                junk.fill_(1)  # evicts the Infinity Cache (256 MiB) before the codec; outside the timed events
+            if ev is not None:
+                ev[0].record()
+            _lib.check(lib.adfl_slq_encode_batched(x.data_ptr(), chunks.data_ptr(), lay.nchunks, 8, q.data_ptr(),
+                                                   scales.data_ptr(), partials.data_ptr(), sh))
+            if ev is not None:
+                ev[1].record()
+            _lib.check(lib.adfl_slq_dequantize_batched(q.data_ptr(), chunks.data_ptr(), lay.nchunks,
+                                                       scales.data_ptr(), out.data_ptr(), sh))
+            if ev is not None:
+                ev[2].record()
+        _, evs = timed(step, args.steps, args.warmup, world, 3)
+        enc, dec = seg_ms(evs, 0, 1), seg_ms(evs, 1, 2)
+        gib = RESNET18 * 4 / GIB
+        res["flushed" if flush else "cache_resident"] = {
+            "encode_ms": round(enc, 4), "decode_ms": round(dec, 4), "round_trip_ms": round(enc + dec, 4),
+            "GiB_per_s": round(gib / ((enc + dec) * 1e-3), 1),
+            "hbm_frac": round(14 * RESNET18 / ((enc + dec) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    return {"metric": "C3 bucketed round trip, 11,689,512 fp32 in 256 tensors (per-tensor scales)", "unit": "GiB/s",
+            "value": res["flushed"]["GiB_per_s"], "launches_per_round_trip": 3, "chunks": lay.nchunks, **res}
+
+
+def mode_c5_int4(args, world, rank, dev):
+    from adfl_amd import _lib, ops
+    lib = _lib.load()
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    n = args.elems or (1 << 30)
+    g = torch.Generator(device=dev).manual_seed(rank)
+    x = torch.randn(n, device=dev, generator=g) * 1e-3
+    packed = torch.empty((n + 1) // 2, dtype=torch.uint8, device=dev)
+    scale = torch.empty(1, device=dev)
+    ws = ops.new_workspace(dev)
+    out = torch.empty(n, device=dev)
+
+    def step(ev):
+        if ev is not None:
+            ev[0].record()
+        _lib.check(lib.adfl_slq_absmax(x.data_ptr(), n, ws.data_ptr(), ws.numel(), sh))
+        if ev is not None:
+            ev[1].record()
+        _lib.check(lib.adfl_slq_quantize_int4(x.data_ptr(), n, 4, ws.data_ptr(), packed.data_ptr(),
+                                              scale.data_ptr(), sh))
+        if ev is not None:
+            ev[2].record()
+        _lib.check(lib.adfl_slq_dequantize_int4(packed.data_ptr(), n, scale.data_ptr(), out.data_ptr(), sh))
+        if ev is not None:
+            ev[3].record()
+    elapsed, evs = timed(step, args.steps, args.warmup, world, 4)
+    ms = {k: round(seg_ms(evs, i, i + 1), 4) for i, k in enumerate(("absmax", "quantize_int4", "dequantize_int4"))}
+    t = elapsed / args.steps
+    return {"metric": "C5 int4 device-resident round trip, 4 GiB fp32 per GPU", "unit": "GiB/s",
+            "value": round(world * n * 4 / GIB / t, 2), "n_gpus": world, "ms_per_step": round(t * 1e3, 4),
+            "kernels_ms": ms, "hbm_frac": round(13 * n / (sum(ms.values()) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
+
+def mode_exchange(args, world, rank, dev):
+    from adfl_amd.exchange import PeerExchange
+    import torch.distributed as dist
+    if world == 1 and not dist.is_initialized():
+        dist.init_process_group("nccl", init_method="tcp://127.0.0.1:29577", rank=0, world_size=1,
+                                device_id=dev)
+    n = args.elems or (1 << 28)
+    bits = 4 if args.packed else 8
+    ex = PeerExchange(n, bits=bits, packed=args.packed, chunks=args.chunks, device=dev)
+    g = torch.Generator(device=dev).manual_seed(rank)
+    x = torch.randn(n, device=dev, generator=g) * 1e-3
+    out = torch.empty(n, device=dev)
+
+    def step(ev):
+        ex.exchange_mean(x, out)
+    elapsed, _ = timed(step, args.steps, args.warmup, world, 1)
+    t = elapsed / args.steps
+    moved = ex.bytes_per_rank * (world - 1)  # bytes each rank receives over xGMI
+    return {"metric": f"C4/C5 peer exchange: SLQ encode + RCCL all-gather + fused decode-mean, bits={bits}"
+                      f"{' packed' if args.packed else ''}, chunks={args.chunks}", "unit": "GiB/s",
+            "value": round(world * n * 4 / GIB / t, 2), "n_gpus": world, "ms_per_step": round(t * 1e3, 4),
+            "elements_per_rank": n, "bytes_per_rank_on_wire": ex.bytes_per_rank,
+            "allgather_algbw_GBs": round(moved / t / 1e9, 1) if world > 1 else None}
+
+
+def mode_pcie(args, world, rank, dev):
+    from adfl_amd import _lib, ops
+    lib = _lib.load()
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    n = args.elems or (1 << 28)
+    x_h = (torch.randn(n) * 1e-3).pin_memory()
+    q_h = torch.empty(n, dtype=torch.int8).pin_memory()
+    out_h = torch.empty(n).pin_memory()
+    s_h = torch.empty(1).pin_memory()
+    x = torch.empty(n, device=dev)
+    q = torch.empty(n, dtype=torch.int8, device=dev)
+    q2 = torch.empty(n, dtype=torch.int8, device=dev)
+    s = torch.empty(1, device=dev)
+    out = torch.empty(n, device=dev)
+    ws = ops.new_workspace(dev)
+
+    def step(ev):
+        if ev is not None:
+            ev[0].record()
+        x.copy_(x_h, non_blocking=True)
+        if ev is not None:
+            ev[1].record()
+        _lib.check(lib.adfl_slq_encode(x.data_ptr(), n, 8, q.data_ptr(), s.data_ptr(), ws.data_ptr(), ws.numel(), sh))
+        if ev is not None:
+            ev[2].record()
+        q_h.copy_(q, non_blocking=True)
+        s_h.copy_(s, non_blocking=True)
+        q2.copy_(q_h, non_blocking=True)   # the payload comes back over the host "wire"
+        if ev is not None:
+            ev[3].record()
+        _lib.check(lib.adfl_slq_dequantize(q2.data_ptr(), n, s.data_ptr(), out.data_ptr(), sh))
+        if ev is not None:
+            ev[4].record()
+        out_h.copy_(out, non_blocking=True)
+        if ev is not None:
+            ev[5].record()
+    elapsed, evs = timed(step, args.steps, args.warmup, world, 6)
+    t = elapsed / args.steps
+    segs = {k: round(seg_ms(evs, i, i + 1), 4) for i, k in
+            enumerate(("h2d_x", "encode", "d2h_h2d_payload", "decode", "d2h_out"))}
+    pcie_ms = segs["h2d_x"] + segs["d2h_h2d_payload"] + segs["d2h_out"]
+    return {"metric": "PCIe-inclusive SLQ round trip, 1 GiB fp32 from and to pinned host memory", "unit": "GiB/s",
+            "value": round(n * 4 / GIB / t, 2), "ms_per_step": round(t * 1e3, 4), "segments_ms": segs,
+            "pcie_GBs": round(10 * n / (pcie_ms * 1e-3) / 1e9, 1)}
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--mode", choices=["c3", "c5_int4", "exchange", "pcie"], required=True)
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--elems", type=int, default=0)
+    p.add_argument("--packed", action="store_true")
+    p.add_argument("--chunks", type=int, default=1)
+    args = p.parse_args()
+    world, rank, local = dist_setup(args)
+    dev = torch.device("cuda", local)
+    line = {"c3": mode_c3, "c5_int4": mode_c5_int4, "exchange": mode_exchange, "pcie": mode_pcie}[args.mode](
+        args, world, rank, dev)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if torch.distributed.is_initialized():
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
