@@ -78,6 +78,35 @@ def _staging() -> _DeviceStaging:
     return st
 
 
+def _gather(tensors: List[torch.Tensor], lay: ops.BucketLayout, out: torch.Tensor) -> None:
+    """Copy `tensors` (all on out's device) into the 1-D bucket `out` at lay.offsets: ONE torch.cat
+    with zero pads between tensors (instead of one copy per tensor)."""
+    zeros = torch.zeros(ops.ALIGN_ELEMS, dtype=out.dtype, device=out.device)
+    pieces = []
+    for t, n, padded in zip(tensors, lay.sizes.tolist(), lay.padded.tolist()):
+        pieces.append(t.reshape(-1))
+        if padded > n:
+            pieces.append(zeros[:padded - n])
+    torch.cat(pieces, out=out)
+
+
+def _stage_in(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _DeviceStaging, key: str,
+              dtype: torch.dtype) -> torch.Tensor:
+    """The bucket on the device: one gather + one H2D for CPU tensors, one device gather otherwise."""
+    dev_buf = st.buf(key, lay.total, dtype)
+    kinds = {t.is_cuda for t in tensors}
+    if kinds == {False}:
+        host = st.buf(key + "_host", lay.total, dtype, pinned=True)
+        _gather(tensors, lay, host)
+        dev_buf.copy_(host, non_blocking=True)
+    elif kinds == {True}:
+        _gather([t.to(st.device) for t in tensors], lay, dev_buf)
+    else:  # mixed host / device dict: per-tensor copies (rare)
+        for t, off, n in zip(tensors, lay.offsets.tolist(), lay.sizes.tolist()):
+            dev_buf[off:off + n].view(t.shape).copy_(t)
+    return dev_buf
+
+
 def _encode_dict(params: Parameters, names: List[str], bits: int):
     """Encode the ndim>1 tensors `names` of `params` in one bucketed pass.
 
@@ -85,71 +114,61 @@ def _encode_dict(params: Parameters, names: List[str], bits: int):
     st = _staging()
     dev = st.device
     tensors = [params[n] for n in names]
-    sizes = tuple(int(t.numel()) for t in tensors)
-    lay = st.layout(sizes)
-    x_dev = st.buf("x", lay.total, torch.float32)
-    on_cpu = [not t.is_cuda for t in tensors]
-    if any(on_cpu):
-        x_host = st.buf("x_host", lay.total, torch.float32, pinned=True)
-        for t, off, n, cpu in zip(tensors, lay.offsets, lay.sizes, on_cpu):
-            if cpu:
-                x_host[int(off):int(off) + int(n)].view(t.shape).copy_(t)
-        x_dev.copy_(x_host, non_blocking=True)  # one H2D for the whole bucket
-    for t, off, n, cpu in zip(tensors, lay.offsets, lay.sizes, on_cpu):
-        if not cpu:  # after the H2D, which would overwrite these slices
-            x_dev[int(off):int(off) + int(n)].view(t.shape).copy_(t)
+    lay = st.layout(tuple(int(t.numel()) for t in tensors))
+    x_dev = _stage_in(tensors, lay, st, "x", torch.float32)
     q_dev, s_dev = ops.encode_batched(x_dev, lay, bits, q=st.buf("q", lay.total, torch.int8),
                                       scales=st.buf("scales", lay.ntensors, torch.float32),
                                       partials=st.buf("partials", lay.nchunks, torch.int32))
     scales_host = st.buf("scales_host", lay.ntensors, torch.float32, pinned=True)
     scales_host.copy_(s_dev, non_blocking=True)
+    on_cpu = [not t.is_cuda for t in tensors]
     if any(on_cpu):
         q_host = st.buf("q_host", lay.total, torch.int8, pinned=True)
         q_host.copy_(q_dev, non_blocking=True)
     torch.cuda.current_stream(dev).synchronize()
+    scales = scales_host.tolist()
+    padded = lay.padded.tolist()
+    parts_host = torch.split(q_host, padded) if any(on_cpu) else None
+    parts_dev = torch.split(q_dev, padded) if not all(on_cpu) else None
     out = {}
-    for i, (name, t, off, n, cpu) in enumerate(zip(names, tensors, lay.offsets, lay.sizes, on_cpu)):
-        scale = float(scales_host[i])
-        src = (q_host if cpu else q_dev)[int(off):int(off) + int(n)]
-        qt = torch._make_per_tensor_quantized_tensor(src.clone().view(t.shape), scale, 0)
-        out[name] = (qt, scale)
+    for i, (name, t, n, cpu) in enumerate(zip(names, tensors, lay.sizes.tolist(), on_cpu)):
+        src = (parts_host if cpu else parts_dev)[i][:n].view(t.shape)
+        # _make_per_tensor_quantized_tensor copies into a fresh qint8 storage: every payload tensor owns
+        # its bytes (compact pickles; the staging buffer is reused by the next call).
+        out[name] = (torch._make_per_tensor_quantized_tensor(src, scales[i], 0), scales[i])
     return out
+
+
+def _int8_view(q: torch.Tensor) -> torch.Tensor:
+    """The int8 bytes of a qint8 tensor without the copy `int_repr()` makes."""
+    return torch.empty(0, dtype=torch.int8, device=q.device).set_(q.untyped_storage(), q.storage_offset(),
+                                                                  q.shape, q.stride())
 
 
 def _decode_dict(items: List[Tuple[str, torch.Tensor]]) -> Dict[str, torch.Tensor]:
     """Decode qint8 tensors (per-tensor affine, zero point 0) in one bucketed pass."""
     st = _staging()
     dev = st.device
-    sizes = tuple(int(q.numel()) for _, q in items)
-    lay = st.layout(sizes)
-    on_cpu = [not q.is_cuda for _, q in items]
-    q_dev = st.buf("dq", lay.total, torch.int8)
-    if any(on_cpu):
-        q_host = st.buf("dq_host", lay.total, torch.int8, pinned=True)
-    scales_host = st.buf("dscales_host", lay.ntensors, torch.float32, pinned=True)
-    for i, ((name, q), off, n, cpu) in enumerate(zip(items, lay.offsets, lay.sizes, on_cpu)):
+    for name, q in items:
         if q.qscheme() != torch.per_tensor_affine or q.dtype != torch.qint8 or q.q_zero_point() != 0:
             raise ValueError(f"SLQChannel: '{name}' is not a per-tensor qint8 payload with zero point 0")
-        scales_host[i] = q.q_scale()  # rounds to the fp32 scale fbgemm's dequantize uses
-        if cpu:
-            q_host[int(off):int(off) + int(n)].view(q.shape).copy_(q.int_repr())
+    lay = st.layout(tuple(int(q.numel()) for _, q in items))
+    q_dev = _stage_in([_int8_view(q) for _, q in items], lay, st, "dq", torch.int8)
+    # q_scale() is a double; fbgemm's dequantize uses it as fp32 (quant.py:110), so round it the same way
+    s_dev = torch.tensor([q.q_scale() for _, q in items], dtype=torch.float32).to(dev, non_blocking=True)
+    on_cpu = [not q.is_cuda for _, q in items]
+    # fresh outputs (the caching allocators make this cheap): decoded tensors are handed to the caller,
+    # owned and writable; strategies mutate them in place (Src/ADFL/Strategy/fed_buff.py:75,90)
+    out_dev = ops.decode_batched(q_dev, s_dev, lay, out=torch.empty(lay.total, dtype=torch.float32, device=dev))
     if any(on_cpu):
-        q_dev.copy_(q_host, non_blocking=True)  # one H2D for the whole bucket
-    for (name, q), off, n, cpu in zip(items, lay.offsets, lay.sizes, on_cpu):
-        if not cpu:
-            q_dev[int(off):int(off) + int(n)].view(q.shape).copy_(q.int_repr())
-    s_dev = st.buf("dscales", lay.ntensors, torch.float32)
-    s_dev.copy_(scales_host, non_blocking=True)
-    out_dev = ops.decode_batched(q_dev, s_dev, lay, out=st.buf("dout", lay.total, torch.float32))
-    if any(on_cpu):
-        out_host = st.buf("dout_host", lay.total, torch.float32, pinned=True)
+        out_host = torch.empty(lay.total, dtype=torch.float32, pin_memory=True)
         out_host.copy_(out_dev, non_blocking=True)
     torch.cuda.current_stream(dev).synchronize()
-    res = {}
-    for (name, q), off, n, cpu in zip(items, lay.offsets, lay.sizes, on_cpu):
-        src = (out_host if cpu else out_dev)[int(off):int(off) + int(n)]
-        res[name] = src.clone().view(q.shape)  # owned and writable (strategies mutate in place)
-    return res
+    padded = lay.padded.tolist()
+    parts_host = torch.split(out_host, padded) if any(on_cpu) else None
+    parts_dev = torch.split(out_dev, padded) if not all(on_cpu) else None
+    return {name: (parts_host if cpu else parts_dev)[i][:n].view(q.shape)
+            for i, ((name, q), n, cpu) in enumerate(zip(items, lay.sizes.tolist(), on_cpu))}
 
 
 class SLQChannel(Channel):

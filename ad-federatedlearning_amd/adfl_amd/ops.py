@@ -155,6 +155,7 @@ class BucketLayout:
             raise ValueError("BucketLayout: every tensor needs at least one element")
         self.sizes = np.asarray(sizes, dtype=np.int64)
         padded = (self.sizes + ALIGN_ELEMS - 1) // ALIGN_ELEMS * ALIGN_ELEMS
+        self.padded = padded.astype(np.int64)  # per-tensor slot size (size rounded up to the alignment)
         self.offsets = np.concatenate([[0], np.cumsum(padded)[:-1]]).astype(np.int64)
         self.total = int(padded.sum())
         self.ntensors = len(sizes)

@@ -48,14 +48,18 @@ def parse():
     return p.parse_args()
 
 
-def dist_setup(args):
+def dist_setup(args, backend: str = "nccl"):
+    """One process per GPU (torchrun env: RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*). `backend` is
+    "nccl" (= RCCL) for the bench; tests drive the same code with "gloo" on CPU."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    if backend == "nccl":
+        torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        kw = {"device_id": torch.device("cuda", local)} if backend == "nccl" else {}
+        dist.init_process_group(backend, **kw)
     return world, rank, local
 
 
@@ -66,10 +70,12 @@ def barrier(world):
 
 
 def max_over_ranks(v: float, world: int) -> float:
+    """The slowest rank's value (the step time the whole job sees)."""
     if world == 1:
         return v
     import torch.distributed as dist
-    t = torch.tensor([v], dtype=torch.float64, device="cuda")
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([v], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 

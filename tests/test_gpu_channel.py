@@ -113,6 +113,42 @@ def test_device_resident_dict_stays_on_device():
     assert dec["w"].is_cuda and torch.equal(dec["w"].cpu(), dec["cpu_w"])
 
 
+def test_all_device_dict_and_c3_loguniform_vs_golden():
+    """C3 (loguniform layout) as a CUDA-resident state dict through the Channel: golden scales and SHA."""
+    case = [c for c in manifest()["bucket"] if c["layout"] == "loguniform"][0]
+    tensors = recipes.bucket_tensors(case["layout"], case["seed"], case["mult"])
+    params = {k: torch.from_numpy(v).cuda() for k, v in tensors.items()}
+    qp, _ = SLQChannel(8).on_client_send(params)
+    dec, _ = SLQChannel(8).on_server_receive(qp)
+    names = list(params)
+    assert all(qp.params[k].data.is_cuda and dec[k].is_cuda for k in names)
+    for k, b in zip(names, case["scale_bits"]):
+        assert same_scale(qp.params[k].scale, b), k
+    q_cat = np.concatenate([qp.params[k].data.int_repr().cpu().numpy().reshape(-1) for k in names])
+    d_cat = np.concatenate([dec[k].cpu().numpy().reshape(-1) for k in names])
+    assert recipes.sha256(q_cat) == case["q_sha256"]
+    assert recipes.sha256(d_cat) == case["deq_sha256"]
+
+
+def test_results_survive_later_calls():
+    """Staging buffers are reused between calls; returned payloads and decoded tensors must not be."""
+    ch = SLQChannel(8)
+    a = {"w": torch.randn(300, 41), "v": torch.randn(7, 3)}
+    b = {"w": torch.randn(300, 41) * 5, "v": torch.randn(7, 3) * 5}
+    qa, _ = ch.on_client_send(a)
+    qa_bytes = {k: p.data.int_repr().clone() for k, p in qa.params.items()}
+    da, _ = ch.on_server_receive(qa)
+    da_copy = {k: v.clone() for k, v in da.items()}
+    qb, _ = ch.on_client_send(b)
+    db, _ = ch.on_server_receive(qb)
+    for k in a:
+        assert torch.equal(qa.params[k].data.int_repr(), qa_bytes[k])
+        assert torch.equal(da[k], da_copy[k])
+        assert not torch.equal(da[k], db[k])
+    da["w"].mul_(2.0)  # writable; does not touch the other decoded tensors
+    assert torch.equal(da["v"], da_copy["v"])
+
+
 def test_channel_pickles_without_device_state():
     ch = SLQChannel(8)
     SLQChannel(8).on_client_send({"w": torch.randn(4, 4)})  # warm the per-process cache

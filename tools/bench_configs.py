@@ -202,9 +202,61 @@ def mode_pcie(args, world, rank, dev):
             "pcie_GBs": round(10 * n / (pcie_ms * 1e-3) / 1e9, 1)}
 
 
+def mode_channel(args, world, rank, dev):
+    """ADFL's own call pattern: a CPU state dict through SLQChannel.on_client_send / on_server_receive
+    (what Src/ADFL/Client/worker.py:176 and Src/ADFL/Server/async_sc.py:209 do), against the reference's
+    per-tensor ATen loop (quant.py:74-112) on the same host and dict."""
+    from adfl_amd.Channel import SLQChannel
+    base, rem = divmod(RESNET18, 256)
+    g = torch.Generator().manual_seed(0)
+    params = {}
+    for i in range(256):
+        params[f"layer{i}.weight"] = torch.randn(1, base + (1 if i < rem else 0), generator=g) * 1e-3
+        params[f"layer{i}.bias"] = torch.randn(64, generator=g) * 1e-3
+    ch = SLQChannel(bits=8)
+
+    def ours():
+        t0 = time.perf_counter()
+        qp, _ = ch.on_client_send(params)
+        t1 = time.perf_counter()
+        d, _ = ch.on_server_receive(qp)
+        return t1 - t0, time.perf_counter() - t1, qp, d
+
+    def reference():  # quant.py:74-104 then :67-71,107-112 — the reference's loop, ATen CPU ops
+        t0 = time.perf_counter()
+        enc = {}
+        for name, t in params.items():
+            if t.ndim > 1:
+                scale = torch.max(torch.abs(t)) / 127
+                enc[name] = torch.quantize_per_tensor(t, float(scale), 0, dtype=torch.qint8)
+            else:
+                enc[name] = t
+        t1 = time.perf_counter()
+        dec = {name: (q.dequantize() if q.ndim > 1 else q.data) for name, q in enc.items()}
+        return t1 - t0, time.perf_counter() - t1, enc, dec
+
+    for _ in range(args.warmup):
+        ours()
+        reference()
+    o = [ours()[:2] for _ in range(args.steps)]
+    r = [reference()[:2] for _ in range(max(3, args.steps // 4))]
+    _, _, qp, d = ours()
+    _, _, enc, dec = reference()
+    same = all(torch.equal(qp.params[k].data.int_repr(), enc[k].int_repr()) and torch.equal(d[k], dec[k])
+               for k in params if params[k].ndim > 1)
+    best = lambda xs, i: min(x[i] for x in xs) * 1e3  # noqa: E731
+    gib = sum(t.numel() for t in params.values()) * 4 / GIB
+    return {"metric": "SLQChannel on a CPU ResNet-18-sized state dict (256 weights + 256 biases), host to host",
+            "unit": "ms", "ours_encode_ms": round(best(o, 0), 3), "ours_decode_ms": round(best(o, 1), 3),
+            "reference_encode_ms": round(best(r, 0), 3), "reference_decode_ms": round(best(r, 1), 3),
+            "ours_GiB_s": round(gib / ((best(o, 0) + best(o, 1)) * 1e-3), 2),
+            "reference_GiB_s": round(gib / ((best(r, 0) + best(r, 1)) * 1e-3), 2),
+            "reference_threads": torch.get_num_threads(), "identical_output": same}
+
+
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--mode", choices=["c3", "c5_int4", "exchange", "pcie"], required=True)
+    p.add_argument("--mode", choices=["c3", "c5_int4", "exchange", "pcie", "channel"], required=True)
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
@@ -214,7 +266,8 @@ def main():
     args = p.parse_args()
     world, rank, local = dist_setup(args)
     dev = torch.device("cuda", local)
-    line = {"c3": mode_c3, "c5_int4": mode_c5_int4, "exchange": mode_exchange, "pcie": mode_pcie}[args.mode](
+    line = {"c3": mode_c3, "c5_int4": mode_c5_int4, "exchange": mode_exchange, "pcie": mode_pcie,
+            "channel": mode_channel}[args.mode](
         args, world, rank, dev)
     if rank == 0:
         print(json.dumps(line), flush=True)
