@@ -3,7 +3,7 @@
 ``SLQChannel`` / ``USLQChannel`` keep the reference's names, constructor, six-method surface,
 ``to_json`` output, ``simulate_bandwidth`` formula, payload types and error behaviour. What changes is
 where the arithmetic runs: the reference loops over the state dict calling ATen CPU ops per tensor
-(quant.py:74-112); here the whole dict is bucketed into one 64-element-aligned flat buffer, moved to
+(quant.py:74-112); here the whole dict is packed back to back into one flat buffer, moved to
 the GPU once, encoded by two HIP launches (absmax partials -> scale + quantize, per-tensor scales),
 and the int8 payload comes back in one copy. Decode is one HIP launch. Output is bit-identical to the
 reference: int8 payload, fp32 scale and dequantized floats (tests/golden).
@@ -57,7 +57,7 @@ class _DeviceStaging:
     def layout(self, sizes: Tuple[int, ...]) -> ops.BucketLayout:
         lay = self.layouts.get(sizes)
         if lay is None:
-            lay = ops.BucketLayout(sizes)
+            lay = ops.BucketLayout(sizes, align=1)  # compact: the host gather is one concatenation
             self.layouts[sizes] = lay
             if len(self.layouts) > _LAYOUT_CACHE_MAX:
                 self.layouts.popitem(last=False)
@@ -79,9 +79,12 @@ def _staging() -> _DeviceStaging:
 
 
 def _gather(tensors: List[torch.Tensor], lay: ops.BucketLayout, out: torch.Tensor) -> None:
-    """Copy `tensors` (all on out's device) into the 1-D bucket `out` at lay.offsets: ONE torch.cat
-    with zero pads between tensors (instead of one copy per tensor)."""
-    zeros = torch.zeros(ops.ALIGN_ELEMS, dtype=out.dtype, device=out.device)
+    """Copy `tensors` (all on out's device) into the 1-D bucket `out` at lay.offsets with ONE torch.cat
+    (zero pads between tensors only for an aligned layout; the Channel's compact layout has none)."""
+    if lay.align == 1:
+        torch.cat([t.reshape(-1) for t in tensors], out=out)
+        return
+    zeros = torch.zeros(lay.align, dtype=out.dtype, device=out.device)
     pieces = []
     for t, n, padded in zip(tensors, lay.sizes.tolist(), lay.padded.tolist()):
         pieces.append(t.reshape(-1))

@@ -146,15 +146,22 @@ def dequantize_mean(q_rows: torch.Tensor, scales: torch.Tensor, n: int, *,
 # bucketed codec (one launch per pass for a whole state dict)
 # ------------------------------------------------------------------------------------------------
 class BucketLayout:
-    """Placement of T tensors in one flat buffer: tensor t at a 64-element-aligned offset, plus the
-    chunk table the bucketed kernels walk (one 256-thread block per <= 8192-element chunk)."""
+    """Placement of T tensors in one flat buffer, plus the chunk table the bucketed kernels walk (one
+    256-thread block per <= 8192-element chunk).
 
-    def __init__(self, sizes: Sequence[int]):
+    align=64 (default) starts every tensor on a 64-element boundary (pads between tensors);
+    align=1 packs them back to back (compact: what the Channel stages through host memory, so the
+    host-side gather is one plain concatenation)."""
+
+    def __init__(self, sizes: Sequence[int], align: int = ALIGN_ELEMS):
         sizes = [int(s) for s in sizes]
         if not sizes or min(sizes) < 1:
             raise ValueError("BucketLayout: every tensor needs at least one element")
+        if align < 1:
+            raise ValueError("BucketLayout: align must be >= 1")
+        self.align = align
         self.sizes = np.asarray(sizes, dtype=np.int64)
-        padded = (self.sizes + ALIGN_ELEMS - 1) // ALIGN_ELEMS * ALIGN_ELEMS
+        padded = (self.sizes + align - 1) // align * align
         self.padded = padded.astype(np.int64)  # per-tensor slot size (size rounded up to the alignment)
         self.offsets = np.concatenate([[0], np.cumsum(padded)[:-1]]).astype(np.int64)
         self.total = int(padded.sum())

@@ -484,6 +484,13 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_mean_int4(const uint8_t* 
 // ------------------------------------------------------------------------------------------------
 // bucketed kernels (many tensors, one block per chunk of <= 8192 elements = 8 wave tiles)
 // ------------------------------------------------------------------------------------------------
+// Chunks may start anywhere (a compact bucket packs tensors back to back): the first `head` elements
+// up to the next `align`-element boundary are done element-wise, the rest in vector units.
+__device__ __forceinline__ int chunk_head(int64_t start, int len, int align) {
+  const int h = (int)((align - (start % align)) % align);
+  return h < len ? h : len;
+}
+
 // Pass 1 keeps default (allocating) loads: a bucketed update (e.g. 46.8 MB for ResNet-18) fits the
 // Infinity Cache whole, so pass 2 re-reads it on-die.
 __global__ __launch_bounds__(kBlock) void k_absmax_batched(const float* __restrict__ x,
@@ -491,11 +498,14 @@ __global__ __launch_bounds__(kBlock) void k_absmax_batched(const float* __restri
                                                            uint32_t* __restrict__ partials) {
   const adfl_slq_chunk c = chunks[blockIdx.x];
   const float* xc = x + c.start;
-  const float4* x4 = reinterpret_cast<const float4*>(xc);
-  const int n4 = c.len >> 2;
+  const int head = chunk_head(c.start, c.len, 4);
+  const float4* x4 = reinterpret_cast<const float4*>(xc + head);
+  const int n4 = (c.len - head) >> 2;
   uint32_t m = 0;
+  if (threadIdx.x < head) m = abs_bits(xc[threadIdx.x]);
   for (int i = threadIdx.x; i < n4; i += kBlock) m = max(m, abs_bits4(x4[i]));
-  if (threadIdx.x < (c.len & 3)) m = max(m, abs_bits(xc[(n4 << 2) + threadIdx.x]));
+  const int tail = head + (n4 << 2);
+  if (threadIdx.x < c.len - tail) m = max(m, abs_bits(xc[tail + threadIdx.x]));
   m = block_max(m);
   if (threadIdx.x == 0) partials[blockIdx.x] = m;
 }
@@ -513,11 +523,13 @@ __global__ __launch_bounds__(kBlock) void k_quantize_batched(const float* __rest
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const float* xc = x + c.start;
   int8_t* qc = q + c.start;
-  const int ntiles = c.len / kTile;
+  const int head = chunk_head(c.start, c.len, 16);  // 16 elements: 64-B x and 16-B payload alignment
+  if (threadIdx.x < head) qc[threadIdx.x] = (int8_t)quant1(xc[threadIdx.x], si.inv);
+  const int ntiles = (c.len - head) / kTile;
   for (int t = wave; t < ntiles; t += kWaves)
-    quantize_tile(reinterpret_cast<const float4*>(xc) + t * (kTile / 4), reinterpret_cast<uint4*>(qc) + t * (kTile / 16),
-                  si.inv, lds[wave], lane);
-  for (int i = ntiles * kTile + threadIdx.x; i < c.len; i += kBlock) qc[i] = (int8_t)quant1(xc[i], si.inv);
+    quantize_tile(reinterpret_cast<const float4*>(xc + head) + t * (kTile / 4),
+                  reinterpret_cast<uint4*>(qc + head) + t * (kTile / 16), si.inv, lds[wave], lane);
+  for (int i = head + ntiles * kTile + threadIdx.x; i < c.len; i += kBlock) qc[i] = (int8_t)quant1(xc[i], si.inv);
 }
 
 __global__ __launch_bounds__(kBlock) void k_dequantize_batched(const int8_t* __restrict__ q,
@@ -530,11 +542,13 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_batched(const int8_t* __r
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int8_t* qc = q + c.start;
   float* oc = out + c.start;
-  const int ntiles = c.len / kTile;
+  const int head = chunk_head(c.start, c.len, 16);
+  if (threadIdx.x < head) oc[threadIdx.x] = s * (float)qc[threadIdx.x];
+  const int ntiles = (c.len - head) / kTile;
   for (int t = wave; t < ntiles; t += kWaves)
-    dequantize_tile(reinterpret_cast<const uint4*>(qc) + t * (kTile / 16), reinterpret_cast<float4*>(oc) + t * (kTile / 4),
-                    s, lds[wave], lane);
-  for (int i = ntiles * kTile + threadIdx.x; i < c.len; i += kBlock) oc[i] = s * (float)qc[i];
+    dequantize_tile(reinterpret_cast<const uint4*>(qc + head) + t * (kTile / 16),
+                    reinterpret_cast<float4*>(oc + head) + t * (kTile / 4), s, lds[wave], lane);
+  for (int i = head + ntiles * kTile + threadIdx.x; i < c.len; i += kBlock) oc[i] = s * (float)qc[i];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -620,7 +634,7 @@ int64_t adfl_slq_build_chunks(const int64_t* offsets, const int64_t* sizes, int3
   if (!offsets || !sizes || ntensors < 1) return ADFL_E_ARG;
   int64_t count = 0;
   for (int32_t t = 0; t < ntensors; ++t) {
-    if (sizes[t] < 1 || offsets[t] < 0 || offsets[t] % ADFL_SLQ_ALIGN_ELEMS != 0) return ADFL_E_ARG;
+    if (sizes[t] < 1 || offsets[t] < 0) return ADFL_E_ARG;
     const int64_t nc = (sizes[t] + ADFL_SLQ_CHUNK_ELEMS - 1) / ADFL_SLQ_CHUNK_ELEMS;
     if (nc > INT32_MAX || count + nc > INT32_MAX) return ADFL_E_ARG;
     if (chunks) {

@@ -68,9 +68,11 @@ int adfl_slq_dequantize(const int8_t* d_q, int64_t n, const float* d_scale, floa
  * Bucketed (multi-tensor) codec — SLQChannel._quantize_params / _receive over a whole state dict
  * (quant.py:74-94, :67-71): one launch per pass for all tensors, per-tensor scales.
  *
- * Layout: tensor t owns elements [offset_t, offset_t + size_t) of the flat x / q / out buffers, with
- * every offset_t a multiple of ADFL_SLQ_ALIGN_ELEMS. The work is described by a chunk table built
- * on the host by adfl_slq_build_chunks() and copied to the device once per layout.
+ * Layout: tensor t owns elements [offset_t, offset_t + size_t) of the flat x / q / out buffers (the
+ * base pointers 16-byte aligned). Offsets may be anything: tensors packed back to back (a compact
+ * bucket, what the Channel uses) run their first elements up to a 16-element boundary element-wise;
+ * offsets that are multiples of ADFL_SLQ_ALIGN_ELEMS never do. The work is described by a chunk table
+ * built on the host by adfl_slq_build_chunks() and copied to the device once per layout.
  * ------------------------------------------------------------------------------------------- */
 #define ADFL_SLQ_ALIGN_ELEMS 64
 #define ADFL_SLQ_CHUNK_ELEMS 8192

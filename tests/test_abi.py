@@ -85,8 +85,10 @@ def test_build_chunks_host_planning():
     # capacity too small, misaligned offset, empty tensor
     assert lib.adfl_slq_build_chunks(offsets.ctypes.data, sizes.ctypes.data, len(sizes), chunks, n - 1) == -1
     bad = offsets.copy()
-    bad[1] = 65
+    bad[1] = -1
     assert lib.adfl_slq_build_chunks(bad.ctypes.data, sizes.ctypes.data, len(sizes), None, 0) == -1
+    bad[1] = 65  # unaligned offsets are valid (compact buckets)
+    assert lib.adfl_slq_build_chunks(bad.ctypes.data, sizes.ctypes.data, len(sizes), None, 0) == n
     zero = sizes.copy()
     zero[0] = 0
     assert lib.adfl_slq_build_chunks(offsets.ctypes.data, zero.ctypes.data, len(sizes), None, 0) == -1

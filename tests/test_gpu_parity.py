@@ -125,10 +125,12 @@ def test_bucketed_c3_vs_golden(case):
     assert recipes.sha256(d_cat) == case["deq_sha256"]
 
 
-def test_bucketed_ragged_and_specials_vs_oracle():
+@pytest.mark.parametrize("align", [64, 1, 3])
+def test_bucketed_ragged_and_specials_vs_oracle(align):
+    """Aligned and compact (back-to-back, every chunk start misaligned) buckets."""
     rng = np.random.default_rng(11)
-    sizes = [1, 17, 8191, 8192, 8193, 64, 3, 20000, 5]
-    lay = ops.BucketLayout(sizes)
+    sizes = [1, 17, 8191, 8192, 8193, 64, 3, 20000, 5, 1023, 1025, 16]
+    lay = ops.BucketLayout(sizes, align=align)
     flat = np.zeros(lay.total, np.float32)
     for i, (o, n) in enumerate(zip(lay.offsets, lay.sizes)):
         flat[o:o + n] = rng.standard_normal(n, dtype=np.float32) * np.float32(10.0 ** -i)
@@ -194,6 +196,38 @@ def test_dequantize_mean_vs_oracle_and_torch(k):
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
     torch_mean = torch.stack([torch.from_numpy(oracle.decode(q[:n], s)) for q, s in zip(qs, scales)]).mean(0)
     np.testing.assert_allclose(got, torch_mean.numpy(), rtol=1e-6, atol=0)  # north_star tolerance
+
+
+def test_round_trip_is_graph_capturable():
+    """The C ABI allocates nothing and never synchronises: a whole round trip captured in a HIP graph
+    replays correctly on new data (include/adfl_slq.h contract)."""
+    from adfl_amd import _lib
+    lib = _lib.load()
+    n = (1 << 20) + 37
+    x = torch.empty(n, device=DEV)
+    q = torch.empty(n, dtype=torch.int8, device=DEV)
+    s = torch.empty(1, device=DEV)
+    ws = ops.new_workspace(DEV)
+    out = torch.empty(n, device=DEV)
+    x.copy_(torch.randn(n, device=DEV))
+    g = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(g):
+            sh = torch.cuda.current_stream().cuda_stream
+            assert lib.adfl_slq_encode(x.data_ptr(), n, 8, q.data_ptr(), s.data_ptr(), ws.data_ptr(),
+                                       ws.numel(), sh) == 0
+            assert lib.adfl_slq_dequantize(q.data_ptr(), n, s.data_ptr(), out.data_ptr(), sh) == 0
+    torch.cuda.current_stream().wait_stream(side)
+    for seed in (1, 2):
+        xn = np.random.default_rng(seed).standard_normal(n, dtype=np.float32) * np.float32(seed)
+        x.copy_(torch.from_numpy(xn))
+        g.replay()
+        torch.cuda.synchronize()
+        q_ref, s_ref = oracle.encode(xn, 8)
+        assert np.array_equal(q.cpu().numpy(), q_ref)
+        assert same_f32(out.cpu().numpy(), oracle.decode(q_ref, s_ref))
 
 
 def test_custom_ops_registered():

@@ -129,6 +129,9 @@ def test_bucket_layout():
     lay = ops.BucketLayout([10, 8192, 8193, 64])
     assert lay.offsets.tolist() == [0, 64, 8256, 16512] and lay.total == 16576
     assert lay.nchunks == 5 and all(o % 64 == 0 for o in lay.offsets)
+    compact = ops.BucketLayout([10, 8192, 8193, 64], align=1)
+    assert compact.offsets.tolist() == [0, 10, 8202, 16395] and compact.total == 16459
+    assert [c.start for c in compact.chunks] == [0, 10, 8202, 16394, 16395]
     lay = ops.BucketLayout(recipes.bucket_sizes("loguniform"))
     assert sum(recipes.bucket_sizes("loguniform")) == recipes.RESNET18_PARAMS
     assert lay.ntensors == 256 and lay.total >= recipes.RESNET18_PARAMS
