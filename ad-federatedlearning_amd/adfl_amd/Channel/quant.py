@@ -22,6 +22,7 @@ Contract kept from the reference:
 There is no CPU fallback: without a GPU and the built HIP library these methods raise.
 """
 
+import threading
 import time
 from collections import OrderedDict
 from typing import Dict, List, Tuple
@@ -40,6 +41,7 @@ class _DeviceStaging:
 
     def __init__(self, device: torch.device):
         self.device = device
+        self.lock = threading.RLock()
         self._bufs: Dict[str, torch.Tensor] = {}
         self.layouts: "OrderedDict[Tuple[int, ...], ops.BucketLayout]" = OrderedDict()
 
@@ -69,13 +71,27 @@ class _DeviceStaging:
 _STAGING: Dict[int, _DeviceStaging] = {}
 
 
+_STAGING_LOCK = threading.Lock()
+
+
 def _staging() -> _DeviceStaging:
     idx = torch.cuda.current_device()
-    st = _STAGING.get(idx)
-    if st is None:
-        st = _DeviceStaging(torch.device("cuda", idx))
-        _STAGING[idx] = st
+    with _STAGING_LOCK:
+        st = _STAGING.get(idx)
+        if st is None:
+            st = _DeviceStaging(torch.device("cuda", idx))
+            _STAGING[idx] = st
     return st
+
+
+def _serialized(fn):
+    """Staging buffers are per device and reused: calls from several threads of one actor (ADFL's peer
+    clients receive on one thread while training on another, Examples/ray_ad.py) take turns."""
+    def wrapper(*args, **kwargs):
+        with _staging().lock:
+            return fn(*args, **kwargs)
+    wrapper.__name__, wrapper.__doc__ = fn.__name__, fn.__doc__
+    return wrapper
 
 
 def _gather(tensors: List[torch.Tensor], lay: ops.BucketLayout, out: torch.Tensor) -> None:
@@ -110,6 +126,7 @@ def _stage_in(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _DeviceSta
     return dev_buf
 
 
+@_serialized
 def _encode_dict(params: Parameters, names: List[str], bits: int):
     """Encode the ndim>1 tensors `names` of `params` in one bucketed pass.
 
@@ -148,6 +165,7 @@ def _int8_view(q: torch.Tensor) -> torch.Tensor:
                                                                   q.shape, q.stride())
 
 
+@_serialized
 def _decode_dict(items: List[Tuple[str, torch.Tensor]]) -> Dict[str, torch.Tensor]:
     """Decode qint8 tensors (per-tensor affine, zero point 0) in one bucketed pass."""
     st = _staging()

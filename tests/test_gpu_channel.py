@@ -149,6 +149,36 @@ def test_results_survive_later_calls():
     assert torch.equal(da["v"], da_copy["v"])
 
 
+def test_concurrent_threads_share_one_device_safely():
+    """ADFL's peer clients decode on a receive thread while the training thread encodes
+    (Examples/ray_ad.py): the per-device staging is serialised, results stay exact."""
+    import threading
+    import slq_oracle as oracle
+    ch = SLQChannel(8)
+    errors = []
+
+    def work(seed):
+        try:
+            g = torch.Generator().manual_seed(seed)
+            params = {f"w{i}": torch.randn(64 + seed, 33 + i, generator=g) * (seed + 1) for i in range(5)}
+            for _ in range(5):
+                qp, _ = ch.on_client_send(params)
+                dec, _ = ch.on_server_receive(qp)
+                for k, v in params.items():
+                    q_ref, s_ref = oracle.encode(v.numpy(), 8)
+                    assert np.array_equal(qp.params[k].data.int_repr().numpy(), q_ref)
+                    assert same_f32(dec[k].numpy(), oracle.decode(q_ref, s_ref))
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    threads = [threading.Thread(target=work, args=(s,)) for s in range(4)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    assert not errors, errors
+
+
 def test_channel_pickles_without_device_state():
     ch = SLQChannel(8)
     SLQChannel(8).on_client_send({"w": torch.randn(4, 4)})  # warm the per-process cache
