@@ -56,15 +56,17 @@ class _DeviceStaging:
             self._bufs[key] = t
         return t[:numel]
 
-    def layout(self, sizes: Tuple[int, ...]) -> ops.BucketLayout:
-        lay = self.layouts.get(sizes)
+    def layout(self, sizes: Tuple[int, ...], align: int = 1) -> ops.BucketLayout:
+        """align=1: compact (the host gather is one concatenation); align=2 for packed int4 buckets."""
+        key = (sizes, align)
+        lay = self.layouts.get(key)
         if lay is None:
-            lay = ops.BucketLayout(sizes, align=1)  # compact: the host gather is one concatenation
-            self.layouts[sizes] = lay
+            lay = ops.BucketLayout(sizes, align=align)
+            self.layouts[key] = lay
             if len(self.layouts) > _LAYOUT_CACHE_MAX:
                 self.layouts.popitem(last=False)
         else:
-            self.layouts.move_to_end(sizes)
+            self.layouts.move_to_end(key)
         return lay
 
 
@@ -192,6 +194,60 @@ def _decode_dict(items: List[Tuple[str, torch.Tensor]]) -> Dict[str, torch.Tenso
             for i, ((name, q), n, cpu) in enumerate(zip(items, lay.sizes.tolist(), on_cpu))}
 
 
+@_serialized
+def _encode_dict_packed(params: Parameters, names: List[str], bits: int):
+    """Packed int4 variant of _encode_dict: {name: (int8 tensor of ceil(n/2) packed bytes, scale)}."""
+    st = _staging()
+    dev = st.device
+    tensors = [params[n] for n in names]
+    lay = st.layout(tuple(int(t.numel()) for t in tensors), align=2)
+    x_dev = _stage_in(tensors, lay, st, "x", torch.float32)
+    p_dev, s_dev = ops.encode_batched_int4(x_dev, lay, bits, packed=st.buf("p", lay.total // 2, torch.uint8),
+                                           scales=st.buf("scales", lay.ntensors, torch.float32),
+                                           partials=st.buf("partials", lay.nchunks, torch.int32))
+    scales_host = st.buf("scales_host", lay.ntensors, torch.float32, pinned=True)
+    scales_host.copy_(s_dev, non_blocking=True)
+    on_cpu = [not t.is_cuda for t in tensors]
+    if any(on_cpu):
+        p_host = st.buf("p_host", lay.total // 2, torch.uint8, pinned=True)
+        p_host.copy_(p_dev, non_blocking=True)
+    torch.cuda.current_stream(dev).synchronize()
+    scales = scales_host.tolist()
+    half = (lay.padded // 2).tolist()
+    parts_host = torch.split(p_host, half) if any(on_cpu) else None
+    parts_dev = torch.split(p_dev, half) if not all(on_cpu) else None
+    # int8, as compression.py:pack_4bit returns; each tensor owns its bytes (the staging is reused)
+    return {name: ((parts_host if cpu else parts_dev)[i].clone().view(torch.int8), scales[i])
+            for i, (name, cpu) in enumerate(zip(names, on_cpu))}
+
+
+@_serialized
+def _decode_dict_packed(items: List[Tuple[str, torch.Tensor, torch.Size, float]]) -> Dict[str, torch.Tensor]:
+    """Decode packed int4 payloads (name, packed int8 [ceil(n/2)], original shape, scale)."""
+    st = _staging()
+    dev = st.device
+    sizes = tuple(int(torch.Size(shape).numel()) for _, _, shape, _ in items)
+    lay = st.layout(sizes, align=2)
+    for (name, p, _, _), n in zip(items, sizes):
+        if p.numel() != (n + 1) // 2:
+            raise ValueError(f"PackedSLQChannel: '{name}' holds {p.numel()} packed bytes, expected {(n + 1) // 2}")
+    # with align=2 every tensor's slot is exactly ceil(n/2) packed bytes: the gather is one concatenation
+    p_lay = st.layout(tuple((n + 1) // 2 for n in sizes), align=1)
+    p_dev = _stage_in([p.view(torch.uint8) for _, p, _, _ in items], p_lay, st, "dp", torch.uint8)
+    s_dev = torch.tensor([s for _, _, _, s in items], dtype=torch.float32).to(dev, non_blocking=True)
+    on_cpu = [not p.is_cuda for _, p, _, _ in items]
+    out_dev = ops.decode_batched_int4(p_dev, s_dev, lay, out=torch.empty(lay.total, dtype=torch.float32, device=dev))
+    if any(on_cpu):
+        out_host = torch.empty(lay.total, dtype=torch.float32, pin_memory=True)
+        out_host.copy_(out_dev, non_blocking=True)
+    torch.cuda.current_stream(dev).synchronize()
+    padded = lay.padded.tolist()
+    parts_host = torch.split(out_host, padded) if any(on_cpu) else None
+    parts_dev = torch.split(out_dev, padded) if not all(on_cpu) else None
+    return {name: (parts_host if cpu else parts_dev)[i][:n].view(shape)
+            for i, ((name, _, shape, _), n, cpu) in enumerate(zip(items, sizes, on_cpu))}
+
+
 class SLQChannel(Channel):
     """Bi-directional symmetric linear quantization (quant.py:15-112) on the MI355X HIP codec."""
 
@@ -273,6 +329,50 @@ class USLQChannel(SLQChannel):
 
     def to_json(self) -> Dict:
         return {"name": self.__class__.__name__, "bits": self.bits}
+
+
+class PackedSLQChannel(SLQChannel):
+    """SLQ with the 4-bit payload actually packed two values per byte — the end-to-end int4 path the
+    reference meant to provide but cannot run (Src/ADFL/compression.py:91-94 passes a qint8 tensor to
+    pack_4bit and raises; its dequantize_tensor never unpacks, :71-74).
+
+    Encode = SLQ quantize (bit-exact with SLQChannel(bits)) + pack_4bit's nibble layout
+    (compression.py:35-48); decode = unpack_4bit (:51-66) + dequantize. Payload entries:
+    QuantParameter(data = int8 tensor of ceil(n/2) packed bytes, bits, scale, shape = original shape,
+    dtype = float32, q_dtype = int8) — what compression.quantize_params builds for bits == 4 (:86-110).
+    bits must be <= 4 (larger codes do not fit a nibble). Values 127 from an all-zero / NaN tensor alias
+    exactly as pack_4bit makes them alias (nibbles 7, -1); they dequantize to +-0.0 / NaN."""
+
+    def __init__(self, bits: int) -> None:
+        if not 1 <= bits <= 4:
+            raise ValueError(f"PackedSLQChannel: bits must be in [1, 4], got {bits}")
+        super().__init__(bits)
+
+    @staticmethod
+    def _is_packed(p: QuantParameter) -> bool:
+        return p.dtype == torch.float32 and p.q_dtype == torch.int8 and len(p.shape) > 1 and p.data.ndim == 1
+
+    def _receive(self, c_params: CompressedParameters) -> Tuple[Parameters, float]:
+        assert isinstance(c_params, QuantParameters)
+        s_time = time.perf_counter()
+        packed = [(name, p.data, p.shape, p.scale) for name, p in c_params.params.items() if self._is_packed(p)]
+        decoded = _decode_dict_packed(packed) if packed else {}
+        params = {name: decoded[name] if name in decoded else p.data.data for name, p in c_params.params.items()}
+        return params, time.perf_counter() - s_time
+
+    def _quantize_params(self, params: Parameters, bits: int) -> QuantParameters:
+        names = [name for name, p in params.items() if p.ndim > 1]
+        for name in names:
+            ops.require_quantizable(params[name])
+        encoded = _encode_dict_packed(params, names, bits) if names else {}
+        q_params = QuantParameters({}, 0)
+        for name, param in params.items():
+            q_param, scale = encoded[name] if name in encoded else (param, 1)
+            q_params.params[name] = QuantParameter(
+                data=q_param, bits=bits, scale=scale, signs=torch.zeros(1, dtype=torch.uint8),
+                shape=param.shape, dtype=param.dtype, q_dtype=q_param.dtype)
+            q_params.size += q_param.nbytes
+        return q_params
 
 
 HipSLQChannel = SLQChannel

@@ -18,6 +18,6 @@ from . import _lib
 _lib.load()
 
 from . import model, ops  # noqa: E402
-from .Channel import Channel, IdentityChannel, SLQChannel, USLQChannel  # noqa: E402
+from .Channel import Channel, IdentityChannel, PackedSLQChannel, SLQChannel, USLQChannel  # noqa: E402
 
-__all__ = ["Channel", "IdentityChannel", "SLQChannel", "USLQChannel", "model", "ops"]
+__all__ = ["Channel", "IdentityChannel", "SLQChannel", "USLQChannel", "PackedSLQChannel", "model", "ops"]

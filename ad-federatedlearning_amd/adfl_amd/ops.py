@@ -218,6 +218,43 @@ def decode_batched(q: torch.Tensor, scales: torch.Tensor, layout: BucketLayout, 
     return out
 
 
+def _require_even_offsets(layout: BucketLayout) -> None:
+    if layout.align % 2 or (layout.offsets % 2).any():
+        raise ValueError("int4 buckets need even tensor offsets (BucketLayout(align=2) or a multiple of 2)")
+
+
+def encode_batched_int4(flat: torch.Tensor, layout: BucketLayout, bits: int = 4, *,
+                        packed: Optional[torch.Tensor] = None, scales: Optional[torch.Tensor] = None,
+                        partials: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Per-tensor SLQ encode fused with pack_4bit over a bucket: packed byte e/2 holds flat elements
+    e, e+1 (layout.total // 2 bytes); per-tensor fp32 scales."""
+    if flat.dtype != torch.float32:
+        raise RuntimeError(f"Quantize only works on Float Tensor, got {_TORCH_TYPE_NAMES.get(flat.dtype, flat.dtype)}")
+    _require_even_offsets(layout)
+    flat = _dev(flat, "flat")
+    dev = flat.device
+    packed = torch.empty(layout.total // 2, dtype=torch.uint8, device=dev) if packed is None else packed
+    scales = torch.empty(layout.ntensors, dtype=torch.float32, device=dev) if scales is None else scales
+    partials = torch.empty(layout.nchunks, dtype=torch.int32, device=dev) if partials is None else partials
+    check(_lib.load().adfl_slq_encode_batched_int4(flat.data_ptr(), layout.device_chunks(dev).data_ptr(),
+                                                   layout.nchunks, bits, packed.data_ptr(), scales.data_ptr(),
+                                                   partials.data_ptr(), _stream(dev)))
+    return packed, scales
+
+
+def decode_batched_int4(packed: torch.Tensor, scales: torch.Tensor, layout: BucketLayout, *,
+                        out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """unpack_4bit + dequantize over a bucket (layout of encode_batched_int4)."""
+    _require_even_offsets(layout)
+    packed = _dev(packed, "packed")
+    dev = packed.device
+    out = torch.empty(layout.total, dtype=torch.float32, device=dev) if out is None else out
+    check(_lib.load().adfl_slq_dequantize_batched_int4(packed.data_ptr(), layout.device_chunks(dev).data_ptr(),
+                                                       layout.nchunks, scales.data_ptr(), out.data_ptr(),
+                                                       _stream(dev)))
+    return out
+
+
 # ------------------------------------------------------------------------------------------------
 # torch.ops.adfl.* custom ops (device tensors; fake impls for tracing / meta shapes)
 # ------------------------------------------------------------------------------------------------

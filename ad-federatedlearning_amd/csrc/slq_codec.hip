@@ -318,8 +318,35 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_flat(const int8_t* __rest
     for (int64_t i = ntiles * kTile + threadIdx.x; i < n; i += kBlock) out[i] = s * (float)q[i];
 }
 
-// int4 pass 2: a wave tile is 2048 elements = 8 coalesced 16-byte loads per lane -> 16 packed bytes per
-// lane, transposed through 1 KiB of LDS (lane l, load j packs float4 j*64+l into halfword j*64+l).
+// int4 wave tile: 2048 elements = 8 coalesced 16-byte loads per lane -> 16 packed bytes per lane,
+// transposed through 1 KiB of LDS (lane l, load j packs float4 j*64+l into halfword j*64+l).
+__device__ __forceinline__ void quantize_tile_int4(const float4* __restrict__ xs, uint4* __restrict__ p16, float inv,
+                                                   uint16_t* __restrict__ lds, int lane) {
+  float4 v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = load4<true>(xs + j * 64 + lane);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) lds[j * 64 + lane] = (uint16_t)quant4_int4(v[j], inv);
+  __builtin_amdgcn_wave_barrier();
+  const uint4 o = reinterpret_cast<const uint4*>(lds)[lane];
+  __builtin_amdgcn_wave_barrier();
+  p16[lane] = o;
+}
+
+// int4 decode tile: one coalesced 16-byte load per lane, LDS transpose, 8 coalesced float4 NT stores.
+__device__ __forceinline__ void dequantize_tile_int4(const uint4* __restrict__ p16, float4* __restrict__ o4, float s,
+                                                     uint16_t* __restrict__ lds, int lane) {
+  reinterpret_cast<uint4*>(lds)[lane] = p16[lane];
+  __builtin_amdgcn_wave_barrier();
+  uint32_t h[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) h[j] = lds[j * 64 + lane];
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int j = 0; j < 8; ++j) store4_nt(o4 + j * 64 + lane, dequant2_int4(h[j], s));
+}
+
+// int4 pass 2 (flat).
 __global__ __launch_bounds__(kBlock) void k_quantize_int4_flat(const float* __restrict__ x, int64_t n, float qmax,
                                                                const uint32_t* __restrict__ partials,
                                                                uint8_t* __restrict__ packed,
@@ -334,16 +361,7 @@ __global__ __launch_bounds__(kBlock) void k_quantize_int4_flat(const float* __re
   const int64_t wstride = (int64_t)gridDim.x * kWaves;
   for (int64_t t0 = (int64_t)blockIdx.x * kWaves + wave; t0 < ntiles; t0 += wstride) {
     const int64_t t = ntiles - 1 - t0;
-    const float4* xs = x4 + t * (kTile4 / 4);
-    float4 v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = load4<true>(xs + j * 64 + lane);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) lds[wave][j * 64 + lane] = (uint16_t)quant4_int4(v[j], si.inv);
-    __builtin_amdgcn_wave_barrier();
-    const uint4 o = reinterpret_cast<const uint4*>(lds[wave])[lane];
-    __builtin_amdgcn_wave_barrier();
-    p16[t * 64 + lane] = o;
+    quantize_tile_int4(x4 + t * (kTile4 / 4), p16 + t * 64, si.inv, lds[wave], lane);
   }
   if (blockIdx.x == gridDim.x - 1) {
     const int64_t np = (n + 1) >> 1;
@@ -355,7 +373,7 @@ __global__ __launch_bounds__(kBlock) void k_quantize_int4_flat(const float* __re
   }
 }
 
-// int4 decode: lane loads 16 packed bytes (coalesced), LDS transpose, 8 coalesced float4 NT stores.
+// int4 decode (flat).
 __global__ __launch_bounds__(kBlock) void k_dequantize_int4_flat(const uint8_t* __restrict__ packed, int64_t n,
                                                                  const float* __restrict__ scale_p,
                                                                  float* __restrict__ out) {
@@ -366,17 +384,8 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_int4_flat(const uint8_t* 
   float4* o4 = reinterpret_cast<float4*>(out);
   const int64_t ntiles = n / kTile4;
   const int64_t wstride = (int64_t)gridDim.x * kWaves;
-  for (int64_t t = (int64_t)blockIdx.x * kWaves + wave; t < ntiles; t += wstride) {
-    reinterpret_cast<uint4*>(lds[wave])[lane] = p16[t * 64 + lane];
-    __builtin_amdgcn_wave_barrier();
-    uint32_t h[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) h[j] = lds[wave][j * 64 + lane];
-    __builtin_amdgcn_wave_barrier();
-    float4* d = o4 + t * (kTile4 / 4);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) store4_nt(d + j * 64 + lane, dequant2_int4(h[j], s));
-  }
+  for (int64_t t = (int64_t)blockIdx.x * kWaves + wave; t < ntiles; t += wstride)
+    dequantize_tile_int4(p16 + t * 64, o4 + t * (kTile4 / 4), s, lds[wave], lane);
   if (blockIdx.x == gridDim.x - 1)
     for (int64_t i = ntiles * kTile4 + threadIdx.x; i < n; i += kBlock) {
       float e0, e1;
@@ -551,6 +560,69 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_batched(const int8_t* __r
   for (int i = head + ntiles * kTile + threadIdx.x; i < c.len; i += kBlock) oc[i] = s * (float)qc[i];
 }
 
+// int4 buckets: every tensor offset is even, so flat element e's nibble lives in packed byte e/2 (high
+// nibble = even element) and an odd-sized tensor's last byte pairs its last element with a zero pad
+// (compression.py:42-43). Vector tiles need 32-element alignment (16-B packed, 64-B x).
+__device__ __forceinline__ void quantize_pairs_int4(const float* __restrict__ xc, uint8_t* __restrict__ pc, int a,
+                                                    int b, int len, float inv) {
+  for (int i = a + 2 * (int)threadIdx.x; i < b; i += 2 * kBlock) {
+    const int hi = quant1(xc[i], inv);
+    const int lo = (i + 1 < len) ? quant1(xc[i + 1], inv) : 0;
+    pc[i >> 1] = (uint8_t)pack_pair(hi, lo);
+  }
+}
+
+__device__ __forceinline__ void dequantize_elems_int4(const uint8_t* __restrict__ pc, float* __restrict__ oc, int a,
+                                                      int b, float s) {
+  for (int i = a + (int)threadIdx.x; i < b; i += kBlock) {
+    float e0, e1;
+    dequant_byte_int4(pc[i >> 1], s, e0, e1);
+    oc[i] = (i & 1) ? e1 : e0;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_quantize_batched_int4(const float* __restrict__ x,
+                                                                  const adfl_slq_chunk* __restrict__ chunks,
+                                                                  int64_t nchunks, float qmax,
+                                                                  const uint32_t* __restrict__ partials,
+                                                                  uint8_t* __restrict__ packed,
+                                                                  float* __restrict__ scales) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[kWaves][kTile4 / 4];
+  const int64_t ci = nchunks - 1 - (int64_t)blockIdx.x;
+  const adfl_slq_chunk c = chunks[ci];
+  const ScaleInv si = make_scale(reduce_partials(partials + c.first_chunk, c.nchunks), qmax);
+  if (ci == c.first_chunk && threadIdx.x == 0) scales[c.tensor] = si.scale;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const float* xc = x + c.start;
+  uint8_t* pc = packed + (c.start >> 1);
+  const int head = chunk_head(c.start, c.len, 32);
+  quantize_pairs_int4(xc, pc, 0, head, c.len, si.inv);
+  const int ntiles = (c.len - head) / kTile4;
+  for (int t = wave; t < ntiles; t += kWaves)
+    quantize_tile_int4(reinterpret_cast<const float4*>(xc + head) + t * (kTile4 / 4),
+                       reinterpret_cast<uint4*>(pc + (head >> 1)) + t * 64, si.inv, lds[wave], lane);
+  quantize_pairs_int4(xc, pc, head + ntiles * kTile4, c.len, c.len, si.inv);
+}
+
+__global__ __launch_bounds__(kBlock) void k_dequantize_batched_int4(const uint8_t* __restrict__ packed,
+                                                                    const adfl_slq_chunk* __restrict__ chunks,
+                                                                    const float* __restrict__ scales,
+                                                                    float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[kWaves][kTile4 / 4];
+  const adfl_slq_chunk c = chunks[blockIdx.x];
+  const float s = scales[c.tensor];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint8_t* pc = packed + (c.start >> 1);
+  float* oc = out + c.start;
+  const int head = chunk_head(c.start, c.len, 32);
+  dequantize_elems_int4(pc, oc, 0, head, s);
+  const int ntiles = (c.len - head) / kTile4;
+  for (int t = wave; t < ntiles; t += kWaves)
+    dequantize_tile_int4(reinterpret_cast<const uint4*>(pc + (head >> 1)) + t * 64,
+                         reinterpret_cast<float4*>(oc + head) + t * (kTile4 / 4), s, lds[wave], lane);
+  dequantize_elems_int4(pc, oc, head + ntiles * kTile4, c.len, s);
+}
+
 // ------------------------------------------------------------------------------------------------
 // host helpers
 // ------------------------------------------------------------------------------------------------
@@ -673,6 +745,29 @@ int adfl_slq_dequantize_batched(const int8_t* d_q, const adfl_slq_chunk* d_chunk
   if (!aligned16(d_q) || !aligned16(d_out)) return ADFL_E_ALIGN;
   hipLaunchKernelGGL(k_dequantize_batched, dim3((unsigned)nchunks), dim3(kBlock), 0, (hipStream_t)stream, d_q,
                      d_chunks, d_scales, d_out);
+  return launch_status();
+}
+
+int adfl_slq_encode_batched_int4(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, int bits,
+                                 uint8_t* d_packed, float* d_scales, uint32_t* d_partials, void* stream) {
+  if (!d_x || !d_chunks || !d_packed || !d_scales || !d_partials || nchunks < 1 || nchunks > INT32_MAX)
+    return ADFL_E_ARG;
+  if (int s = check_bits(bits)) return s;
+  if (!aligned16(d_x) || !aligned16(d_packed)) return ADFL_E_ALIGN;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_absmax_batched, dim3((unsigned)nchunks), dim3(kBlock), 0, st, d_x, d_chunks, d_partials);
+  if (int s = launch_status()) return s;
+  hipLaunchKernelGGL(k_quantize_batched_int4, dim3((unsigned)nchunks), dim3(kBlock), 0, st, d_x, d_chunks, nchunks,
+                     qmax_f(bits), (const uint32_t*)d_partials, d_packed, d_scales);
+  return launch_status();
+}
+
+int adfl_slq_dequantize_batched_int4(const uint8_t* d_packed, const adfl_slq_chunk* d_chunks, int64_t nchunks,
+                                     const float* d_scales, float* d_out, void* stream) {
+  if (!d_packed || !d_chunks || !d_scales || !d_out || nchunks < 1 || nchunks > INT32_MAX) return ADFL_E_ARG;
+  if (!aligned16(d_packed) || !aligned16(d_out)) return ADFL_E_ALIGN;
+  hipLaunchKernelGGL(k_dequantize_batched_int4, dim3((unsigned)nchunks), dim3(kBlock), 0, (hipStream_t)stream,
+                     d_packed, d_chunks, d_scales, d_out);
   return launch_status();
 }
 

@@ -107,6 +107,13 @@ int adfl_slq_encode_int4(const float* d_x, int64_t n, int bits, uint8_t* d_packe
                          void* d_workspace, int64_t workspace_bytes, void* stream);
 int adfl_slq_dequantize_int4(const uint8_t* d_packed, int64_t n, const float* d_scale, float* d_out,
                              void* stream);
+/* Bucketed int4 (PackedSLQChannel): every tensor offset in the chunk table must be EVEN; flat element e
+ * then lives in packed byte e/2, so d_packed holds (total elements)/2 bytes, and an odd-sized tensor's
+ * last byte pairs its last element with a zero pad exactly as pack_4bit does per tensor. */
+int adfl_slq_encode_batched_int4(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, int bits,
+                                 uint8_t* d_packed, float* d_scales, uint32_t* d_partials, void* stream);
+int adfl_slq_dequantize_batched_int4(const uint8_t* d_packed, const adfl_slq_chunk* d_chunks, int64_t nchunks,
+                                     const float* d_scales, float* d_out, void* stream);
 int adfl_pack_int4(const int8_t* d_q, int64_t n, uint8_t* d_packed, void* stream);
 int adfl_unpack_int4(const uint8_t* d_packed, int64_t n, int8_t* d_q, void* stream);
 

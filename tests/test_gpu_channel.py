@@ -203,3 +203,45 @@ def test_reference_errors():
         ch.on_client_send({"w": torch.empty(0, 3)})
     with pytest.raises(AssertionError):
         ch.on_server_receive(ByteParameters({}, 0))
+
+
+@pytest.mark.parametrize("bits", [4, 2])
+def test_packed_channel_vs_golden(bits):
+    """PackedSLQChannel: every golden case of this width in one dict; payload = pack_4bit(reference SLQ
+    payload) (the reference's own layout functions, pinned by tests/golden/int4.npz), decode = unpack +
+    dequantize, half the bytes of SLQChannel's payload."""
+    import slq_oracle as oracle
+    from adfl_amd.Channel import PackedSLQChannel
+    cases = [c for g in ("raw", "edge") for c in manifest()[g] if c["bits"] == bits]
+    A = small()
+    params = {c["name"]: torch.from_numpy(A[c["name"] + "__x"].copy()) for c in cases}
+    params["bias"] = torch.randn(9)
+    ch = PackedSLQChannel(bits)
+    qp, _ = ch.on_client_send(params)
+    dec, _ = ch.on_server_receive(qp)
+    total = 0
+    for c in cases:
+        p = qp.params[c["name"]]
+        q_ref = A[c["name"] + "__q"]
+        p_ref = oracle.pack_int4(q_ref)
+        assert p.data.dtype == torch.int8 and p.data.ndim == 1 and p.q_dtype == torch.int8
+        assert tuple(p.shape) == q_ref.shape and p.dtype == torch.float32 and p.bits == bits
+        assert np.array_equal(p.data.numpy().view(np.uint8), p_ref), c["name"]
+        assert same_scale(p.scale, c["scale_bits"])
+        assert same_f32(dec[c["name"]].numpy(), oracle.decode_int4(p_ref, q_ref.size, p.scale)), c["name"]
+        total += p.data.nbytes
+    assert qp.params["bias"].data is params["bias"]
+    assert qp.size == total + params["bias"].nbytes
+    assert ch.to_json() == {"name": "PackedSLQChannel", "bits": bits}
+    blob = len(pickle.dumps(qp.params[cases[0]["name"]]))
+    assert blob < qp.params[cases[0]["name"]].data.nbytes + 2048
+
+
+def test_packed_channel_device_dict():
+    from adfl_amd.Channel import PackedSLQChannel
+    x = torch.randn(333, 77, device="cuda")
+    qp, _ = PackedSLQChannel(4).on_client_send({"w": x, "b": torch.randn(5, device="cuda")})
+    assert qp.params["w"].data.is_cuda and qp.params["w"].data.numel() == (333 * 77 + 1) // 2
+    dec, _ = PackedSLQChannel(4).on_server_receive(qp)
+    ref, _ = SLQChannel(4).on_server_receive(SLQChannel(4).on_client_send({"w": x.cpu()})[0])
+    assert torch.equal(dec["w"].cpu(), ref["w"])  # values in [-7, 7]: packing is lossless vs int8 SLQ

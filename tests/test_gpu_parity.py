@@ -252,3 +252,26 @@ def test_reference_errors():
     from adfl_amd._lib import AdflError
     with pytest.raises(AdflError, match="bits"):
         ops.encode(torch.randn(3, 3, device=DEV), 0)
+
+
+@pytest.mark.parametrize("align", [2, 64])
+@pytest.mark.parametrize("bits", [4, 2])
+def test_bucketed_int4_vs_oracle(align, bits):
+    """Packed int4 buckets (PackedSLQChannel's kernels): per tensor, pack_4bit(SLQ(x)) and its decode."""
+    rng = np.random.default_rng(40 + align + bits)
+    sizes = [1, 2, 3, 31, 32, 33, 2047, 2048, 2049, 8191, 8192, 8193, 20001, 5, 4096 * 3 + 7]
+    lay = ops.BucketLayout(sizes, align=align)
+    flat = np.zeros(lay.total, np.float32)
+    for i, (o, n) in enumerate(zip(lay.offsets, lay.sizes)):
+        flat[o:o + n] = rng.standard_normal(n, dtype=np.float32) * np.float32(2.0 ** -i)
+    flat[lay.offsets[3]:lay.offsets[3] + lay.sizes[3]] = 0.0          # aliasing tensor (payload 127)
+    flat[lay.offsets[7] + 5] = np.nan
+    packed, scales = ops.encode_batched_int4(torch.from_numpy(flat).to(DEV), lay, bits)
+    out = ops.decode_batched_int4(packed, scales, lay)
+    pn, sn, dn = packed.cpu().numpy(), scales.cpu().numpy(), out.cpu().numpy()
+    for t, (o, n) in enumerate(zip(lay.offsets, lay.sizes)):
+        q_ref, s_ref = oracle.encode(flat[o:o + n], bits)
+        p_ref = oracle.pack_int4(q_ref)
+        assert np.array_equal(pn[o // 2:o // 2 + p_ref.size], p_ref), (t, n)
+        assert same_f32(sn[t], s_ref), t
+        assert same_f32(dn[o:o + n], oracle.decode_int4(p_ref, n, s_ref)), t

@@ -149,3 +149,12 @@ def test_oracle_not_imported_by_product_package():
     import os
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     subprocess.run([sys.executable, "-c", code], check=True, cwd=repo)
+
+
+def test_packed_channel_host_rules():
+    from adfl_amd.Channel import PackedSLQChannel
+    with pytest.raises(ValueError, match="bits"):
+        PackedSLQChannel(8)
+    assert PackedSLQChannel(4).to_json() == {"name": "PackedSLQChannel", "bits": 4}
+    assert PackedSLQChannel(4).simulate_bandwidth(_bw_params(), 1e12) == SLQChannel(4).simulate_bandwidth(
+        _bw_params(), 1e12)
