@@ -45,6 +45,7 @@ SIGNATURES = {
     "adfl_slq_build_chunks": (I64, [P, P, I32, P, I64]),
     "adfl_slq_encode_batched": (INT, [P, P, I64, INT, P, P, P, P]),
     "adfl_slq_dequantize_batched": (INT, [P, P, I64, P, P, P]),
+    "adfl_slq_qerror_batched": (INT, [P, P, P, I64, P, P, P]),
     "adfl_slq_encode_batched_int4": (INT, [P, P, I64, INT, P, P, P, P]),
     "adfl_slq_dequantize_batched_int4": (INT, [P, P, I64, P, P, P]),
     "adfl_slq_quantize_int4": (INT, [P, I64, INT, P, P, P, P]),

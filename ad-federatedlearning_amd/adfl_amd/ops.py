@@ -218,6 +218,19 @@ def decode_batched(q: torch.Tensor, scales: torch.Tensor, layout: BucketLayout, 
     return out
 
 
+def qerror_batched(flat: torch.Tensor, q: torch.Tensor, scales: torch.Tensor,
+                   layout: BucketLayout) -> Tuple[float, float, float, float]:
+    """(sum (x-d)^2, sum x^2, sum x*d, sum d^2) over a bucket and its payload, d = fp32(scale*q), fp64
+    sums (synchronises: returns Python floats)."""
+    flat, q = _dev(flat, "flat"), _dev(q, "q")
+    dev = flat.device
+    partials = torch.empty(layout.nchunks * 4, dtype=torch.float64, device=dev)
+    check(_lib.load().adfl_slq_qerror_batched(flat.data_ptr(), q.data_ptr(), layout.device_chunks(dev).data_ptr(),
+                                              layout.nchunks, scales.data_ptr(), partials.data_ptr(),
+                                              _stream(dev)))
+    return tuple(partials.view(-1, 4).sum(0).tolist())
+
+
 def _require_even_offsets(layout: BucketLayout) -> None:
     if layout.align % 2 or (layout.offsets % 2).any():
         raise ValueError("int4 buckets need even tensor offsets (BucketLayout(align=2) or a multiple of 2)")

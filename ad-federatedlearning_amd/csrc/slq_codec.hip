@@ -560,6 +560,43 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_batched(const int8_t* __r
   for (int i = head + ntiles * kTile + threadIdx.x; i < c.len; i += kBlock) oc[i] = s * (float)qc[i];
 }
 
+// Quantization-error statistics of a bucket against its own payload (worker.py:186-189 computes
+// parameter_relative_mse and parameter_cosine_similarity from a full decode; here they are four sums
+// per chunk, fp64): S0 = sum (x - s*q)^2, S1 = sum x^2, S2 = sum x*(s*q), S3 = sum (s*q)^2.
+__global__ __launch_bounds__(kBlock) void k_qerror_batched(const float* __restrict__ x, const int8_t* __restrict__ q,
+                                                           const adfl_slq_chunk* __restrict__ chunks,
+                                                           const float* __restrict__ scales,
+                                                           double* __restrict__ partials) {
+  __shared__ double red[4][kWaves];
+  const adfl_slq_chunk c = chunks[blockIdx.x];
+  const float s = scales[c.tensor];
+  const float* xc = x + c.start;
+  const int8_t* qc = q + c.start;
+  double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+  for (int i = threadIdx.x; i < c.len; i += kBlock) {
+    const double xv = xc[i];
+    const double dv = (double)(s * (float)qc[i]);  // the dequantized fp32 value the reference compares
+    const double e = (double)(xc[i] - (float)dv);  // fp32 difference, as (a - b) in parameter_mse
+    a0 += e * e;
+    a1 += xv * xv;
+    a2 += xv * dv;
+    a3 += dv * dv;
+  }
+  double v[4] = {a0, a1, a2, a3};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
+    if ((threadIdx.x & 63) == 0) red[k][threadIdx.x >> 6] = v[k];
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    double t = 0;
+    for (int w = 0; w < kWaves; ++w) t += red[threadIdx.x][w];
+    partials[4 * (int64_t)blockIdx.x + threadIdx.x] = t;
+  }
+}
+
 // int4 buckets: every tensor offset is even, so flat element e's nibble lives in packed byte e/2 (high
 // nibble = even element) and an odd-sized tensor's last byte pairs its last element with a zero pad
 // (compression.py:42-43). Vector tiles need 32-element alignment (16-B packed, 64-B x).
@@ -745,6 +782,14 @@ int adfl_slq_dequantize_batched(const int8_t* d_q, const adfl_slq_chunk* d_chunk
   if (!aligned16(d_q) || !aligned16(d_out)) return ADFL_E_ALIGN;
   hipLaunchKernelGGL(k_dequantize_batched, dim3((unsigned)nchunks), dim3(kBlock), 0, (hipStream_t)stream, d_q,
                      d_chunks, d_scales, d_out);
+  return launch_status();
+}
+
+int adfl_slq_qerror_batched(const float* d_x, const int8_t* d_q, const adfl_slq_chunk* d_chunks, int64_t nchunks,
+                            const float* d_scales, double* d_partials, void* stream) {
+  if (!d_x || !d_q || !d_chunks || !d_scales || !d_partials || nchunks < 1 || nchunks > INT32_MAX) return ADFL_E_ARG;
+  hipLaunchKernelGGL(k_qerror_batched, dim3((unsigned)nchunks), dim3(kBlock), 0, (hipStream_t)stream, d_x, d_q,
+                     d_chunks, d_scales, d_partials);
   return launch_status();
 }
 

@@ -96,6 +96,13 @@ int adfl_slq_encode_batched(const float* d_x, const adfl_slq_chunk* d_chunks, in
 int adfl_slq_dequantize_batched(const int8_t* d_q, const adfl_slq_chunk* d_chunks, int64_t nchunks,
                                 const float* d_scales, float* d_out, void* stream);
 
+/* Quantization error of a bucket against its own payload without materialising the decode — the
+ * metrics Src/ADFL/Client/worker.py:186-189 computes with parameter_relative_mse /
+ * parameter_cosine_similarity (Src/ADFL/model.py:256-323). Per chunk, 4 fp64 sums into
+ * d_partials[4*c .. 4*c+3]: sum (x-d)^2, sum x^2, sum x*d, sum d^2 with d = fp32(scale*q). */
+int adfl_slq_qerror_batched(const float* d_x, const int8_t* d_q, const adfl_slq_chunk* d_chunks, int64_t nchunks,
+                            const float* d_scales, double* d_partials, void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * int4 packed variant — compression.py pack_4bit / unpack_4bit (Src/ADFL/compression.py:35-66)
  * fused with SLQ quantize / dequantize. Packed bytes = ceil(n/2); byte j = ((q[2j]+8)<<4) | (q[2j+1]+8)

@@ -179,6 +179,37 @@ def test_concurrent_threads_share_one_device_safely():
     assert not errors, errors
 
 
+def test_send_with_q_error_matches_reference_metrics():
+    """worker.py:176,186-189 in one call: payload identical to on_client_send, metrics equal to the
+    reference's parameter_relative_mse / parameter_cosine_similarity (exclude_bias=True) computed on
+    the decoded dict (restated here exactly as Src/ADFL/model.py:256-323 computes them)."""
+    g = torch.Generator().manual_seed(3)
+    params = {f"w{i}": torch.randn(50 + 17 * i, 31, generator=g) * 10.0 ** (-i) for i in range(6)}
+    params["bias"] = torch.randn(31, generator=g)
+    ch = SLQChannel(8)
+    qp, c_time, mse, cos = ch.send_with_q_error(params)
+    qp2, _ = ch.on_client_send(params)
+    for k in params:
+        a, b = qp.params[k].data, qp2.params[k].data
+        assert torch.equal(a.int_repr(), b.int_repr()) if a.is_quantized else a is b
+    dec, _ = ch.on_server_receive(qp)
+    keys = [k for k in params if params[k].ndim > 1]
+    num = sum(torch.sum((params[k] - dec[k]) ** 2).item() for k in keys)
+    den = sum(torch.sum((params[k] - torch.zeros_like(params[k])) ** 2).item() for k in keys)
+    ref_mse = num / den
+    ref_cos = torch.nn.functional.cosine_similarity(torch.cat([params[k].flatten() for k in keys]),
+                                                    torch.cat([dec[k].flatten() for k in keys]), dim=0).item()
+    # the reference reduces in fp32 (its own summation error is ~1e-6 here); ours sums in fp64
+    assert mse == pytest.approx(ref_mse, rel=1e-5)
+    assert cos == pytest.approx(ref_cos, rel=1e-5)
+    a64 = torch.cat([params[k].flatten().double() for k in keys])
+    b64 = torch.cat([dec[k].flatten().double() for k in keys])
+    e64 = torch.cat([(params[k] - dec[k]).flatten().double() for k in keys])  # fp32 difference, as model.py:280
+    assert mse == pytest.approx(((e64 ** 2).sum() / (a64 ** 2).sum()).item(), rel=1e-9)
+    assert cos == pytest.approx(((a64 * b64).sum() / (a64.norm() * b64.norm())).item(), rel=1e-12)
+    assert c_time > 0
+
+
 def test_channel_pickles_without_device_state():
     ch = SLQChannel(8)
     SLQChannel(8).on_client_send({"w": torch.randn(4, 4)})  # warm the per-process cache
