@@ -402,3 +402,7 @@ class PackedSLQChannel(SLQChannel):
 
 HipSLQChannel = SLQChannel
 HipUSLQChannel = USLQChannel
+
+# The stochastic channels live beside the reference's in quant.py's namespace (quant.py:140-570).
+from .stoch import (CNATChannel, QSGDChannel, RQSGDChannel, UCNATChannel, UQSGDChannel,  # noqa: E402,F401
+                    URQSGDChannel)

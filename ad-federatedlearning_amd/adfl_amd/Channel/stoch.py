@@ -1,0 +1,262 @@
+"""Stochastic-rounding channels backed by the MI355X HIP codec — drop-in for
+``Src/ADFL/Channel/quant.py:140-570`` (QSGD, UQSGD, RQSGD, URQSGD, CNAT, UCNAT).
+
+Same names, constructor (``bits``; ``levels = 2**bits - 1``), six-method surface, ``to_json`` output,
+``simulate_bandwidth`` formulas and payload layout as the reference:
+
+* ``QuantParameter.data`` = levels (uint8; CNAT: int8 exponents), ``signs`` = int8 sign plane,
+  ``scale`` = the norm as a Python float (``norm.item()``), ``scale_2`` = RQSGD's min|x|;
+* all-zero tensors take the reference's norm == 0 branch: uint8 zeros, int8 ones, ``scale`` = the 0-dim
+  fp32 tensor ``tensor(0.)`` (quant.py:227-228,368-369,513-514);
+* ``ndim <= 1`` tensors pass through (same object) with ``signs = zeros(1, uint8)`` and scale 0;
+* ``size`` counts only the level / exponent bytes, as the reference does (quant.py:218,359,504);
+* decode returns owned, writable fp32 tensors.
+
+What changes is where the arithmetic runs: the whole state dict is staged once into one flat bucket on
+the GPU and encoded / decoded by a few HIP launches for all tensors together (include/adfl_stoch.h).
+
+Randomness: the reference draws ``torch.rand_like`` from torch's CPU generator. Here each encode draws a
+fresh 62-bit seed from that same generator (so ``torch.manual_seed`` reproduces a run) and the kernels
+generate their uniforms from a Philox4x32-10 stream keyed by it. The uniforms are not the reference's
+mt19937 draws, so individual rounding decisions differ from a reference run; their distribution is the
+same (and with injected uniforms the codec is bit-identical: tests/test_gpu_stoch.py).
+
+Norms: L2 norms are the correctly rounded fp32 norm (fp64 accumulation of fp32 squares); torch's fp32
+accumulation is less accurate. There is no CPU fallback: without the HIP library these raise.
+"""
+
+import time
+from typing import Dict, List, Tuple
+
+import torch
+
+from .. import stoch as sops
+from ..model import CompressedParameters, Parameters, QuantParameter, QuantParameters, get_parameter_info
+from .channel import Channel, IdentityChannel
+from .quant import _serialized, _stage_in, _staging
+
+_CODECS = ("qsgd", "rqsgd", "cnat")
+
+
+def _require_fp32(name: str, t: torch.Tensor, cls: str) -> None:
+    if t.dtype != torch.float32:
+        raise ValueError(f"{cls}: '{name}' is {t.dtype}; the HIP stochastic codecs quantize fp32 tensors")
+
+
+def _owned(parts: List[torch.Tensor], shapes: List[torch.Size]) -> List[torch.Tensor]:
+    """Per-tensor copies: each payload tensor owns its bytes (it is pickled on its own; the staging
+    buffers are reused by the next call)."""
+    return [p.view(s).clone() for p, s in zip(parts, shapes)]
+
+
+@_serialized
+def _encode_stoch(params: Parameters, names: List[str], codec: str, bits: int, uniforms=None, seed=None):
+    """Encode the ndim > 1 fp32 tensors `names` of `params` in one bucketed pass.
+
+    Returns {name: (data, signs, scale, scale_2)} with CPU tensors for CPU inputs (device tensors for
+    device inputs). `uniforms`: optional fp32 device plane over the compact bucket (tests)."""
+    st = _staging()
+    dev = st.device
+    tensors = [params[n] for n in names]
+    lay = st.layout(tuple(int(t.numel()) for t in tensors))
+    x_dev = _stage_in(tensors, lay, st, "x", torch.float32)
+    if seed is None:
+        seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+    ws = st.buf("stoch_ws", lay.nchunks * 16, torch.uint8)
+    # staging buffers are cached by name: the level plane is always uint8 (CNAT views it as int8)
+    planes = dict(levels=st.buf("s_levels", lay.total, torch.uint8), signs=st.buf("s_signs", lay.total, torch.int8))
+    norms = st.buf("s_norms", lay.ntensors, torch.float32)
+    mins = None
+    if codec == "qsgd":
+        lv, sg, norms = sops.qsgd_encode_batched(x_dev, lay, bits, uniforms=uniforms, seed=seed, counter=0,
+                                                 levels=planes["levels"], signs=planes["signs"], norms=norms, ws=ws)
+    elif codec == "rqsgd":
+        mins = st.buf("s_mins", lay.ntensors, torch.float32)
+        lv, sg, norms, mins = sops.rqsgd_encode_batched(x_dev, lay, bits, uniforms=uniforms, seed=seed, counter=0,
+                                                        levels=planes["levels"], signs=planes["signs"],
+                                                        norms=norms, mins=mins, ws=ws)
+    else:
+        lv, sg, norms = sops.cnat_encode_batched(x_dev, lay, bits, uniforms=uniforms, seed=seed, counter=0,
+                                                 exps=planes["levels"].view(torch.int8), signs=planes["signs"],
+                                                 norms=norms, ws=ws)
+    nm_host = st.buf("s_norms_host", 2 * lay.ntensors, torch.float32, pinned=True)
+    nm_host[:lay.ntensors].copy_(norms, non_blocking=True)
+    if mins is not None:
+        nm_host[lay.ntensors:].copy_(mins, non_blocking=True)
+    on_cpu = [not t.is_cuda for t in tensors]
+    if any(on_cpu):
+        lv_h = st.buf("s_levels_host", lay.total, torch.uint8, pinned=True).view(lv.dtype)
+        sg_h = st.buf("s_signs_host", lay.total, torch.int8, pinned=True)
+        lv_h.copy_(lv, non_blocking=True)
+        sg_h.copy_(sg, non_blocking=True)
+    torch.cuda.current_stream(dev).synchronize()
+    nm = nm_host.tolist()
+    sizes, shapes = lay.sizes.tolist(), [t.shape for t in tensors]
+    split = lambda buf: [p[:n] for p, n in zip(torch.split(buf, lay.padded.tolist()), sizes)]  # noqa: E731
+    lv_parts = _owned(split(lv_h), shapes) if any(on_cpu) else None
+    sg_parts = _owned(split(sg_h), shapes) if any(on_cpu) else None
+    lv_dev = _owned(split(lv), shapes) if not all(on_cpu) else None
+    sg_dev = _owned(split(sg), shapes) if not all(on_cpu) else None
+    out = {}
+    for i, (name, cpu) in enumerate(zip(names, on_cpu)):
+        data = (lv_parts if cpu else lv_dev)[i]
+        signs = (sg_parts if cpu else sg_dev)[i]
+        norm = nm[i]
+        if norm == 0.0:  # the reference's norm == 0 branch: uint8 zeros, tensor(0.) scale
+            scale = torch.tensor(0.0)
+            data = data.view(torch.uint8)
+            scale_2 = 0
+        else:
+            scale = norm
+            scale_2 = nm[lay.ntensors + i] if codec == "rqsgd" else 0
+        out[name] = (data, signs, scale, scale_2)
+    return out
+
+
+@_serialized
+def _decode_stoch(items: List[Tuple[str, QuantParameter]], codec: str, bits: int) -> Dict[str, torch.Tensor]:
+    """Decode (levels, signs, norm[, min]) payloads of ndim > 1 tensors in one bucketed pass."""
+    st = _staging()
+    dev = st.device
+    lay = st.layout(tuple(int(p.data.numel()) for _, p in items))
+    lv_dev = _stage_in([p.data.view(torch.uint8) for _, p in items], lay, st, "d_levels", torch.uint8)
+    sg_dev = _stage_in([p.signs.view(torch.int8) for _, p in items], lay, st, "d_signs", torch.int8)
+    scales = [float(p.scale) for _, p in items]
+    ntens = len(items)
+    sc = torch.tensor(scales + ([float(p.scale_2) for _, p in items] if codec == "rqsgd" else []),
+                      dtype=torch.float32).to(dev, non_blocking=True)
+    out_dev = torch.empty(lay.total, dtype=torch.float32, device=dev)
+    if codec == "qsgd":
+        sops.qsgd_decode_batched(lv_dev, sg_dev, sc[:ntens], lay, bits, out=out_dev)
+    elif codec == "rqsgd":
+        sops.rqsgd_decode_batched(lv_dev, sg_dev, sc[:ntens], sc[ntens:], lay, bits, out=out_dev)
+    else:
+        sops.cnat_decode_batched(lv_dev.view(torch.int8), sg_dev, sc[:ntens], lay, out=out_dev)
+    on_cpu = [not p.data.is_cuda for _, p in items]
+    if any(on_cpu):
+        out_host = torch.empty(lay.total, dtype=torch.float32, pin_memory=True)
+        out_host.copy_(out_dev, non_blocking=True)
+    torch.cuda.current_stream(dev).synchronize()
+    padded = lay.padded.tolist()
+    parts_host = torch.split(out_host, padded) if any(on_cpu) else None
+    parts_dev = torch.split(out_dev, padded) if not all(on_cpu) else None
+    return {name: (parts_host if cpu else parts_dev)[i][:p.data.numel()].view(p.data.shape)
+            for i, ((name, p), cpu) in enumerate(zip(items, on_cpu))}
+
+
+class _StochChannel(Channel):
+    """Shared body of the three bi-directional stochastic channels."""
+
+    CODEC = "qsgd"
+    NORM_BYTES = 4  # per quantized tensor: the norm (RQSGD: norm + minimum factor)
+
+    def __init__(self, bits: int) -> None:
+        self.bits = bits
+        self.levels = 2 ** bits - 1
+
+    def on_server_send(self, params: Parameters) -> Tuple[CompressedParameters, float]:
+        return self._send(params)
+
+    def on_server_receive(self, c_params: CompressedParameters) -> Tuple[Parameters, float]:
+        return self._receive(c_params)
+
+    def on_client_send(self, params: Parameters) -> Tuple[CompressedParameters, float]:
+        return self._send(params)
+
+    def on_client_receive(self, c_params: CompressedParameters) -> Tuple[Parameters, float]:
+        return self._receive(c_params)
+
+    def to_json(self) -> Dict:
+        return {"name": self.__class__.__name__, "bits": self.bits}
+
+    def simulate_bandwidth(self, params: Parameters, mbps: float) -> float:
+        """self.bits + 1 for weights and signs, 32 bits for biases, norms (quant.py:173-184,313-324,459-470)."""
+        p_info = get_parameter_info(params)
+        num_bytes = p_info.num_non_bias_w * (self.bits + 1) / 8
+        num_bytes += p_info.num_bias_w * 4
+        num_bytes += p_info.num_non_bias_t * self.NORM_BYTES
+        transfer_time = num_bytes / (mbps * 1_000_000 / 8)
+        time.sleep(transfer_time)
+        return transfer_time
+
+    def _send(self, params: Parameters) -> Tuple[CompressedParameters, float]:
+        s_time = time.perf_counter()
+        q_params = self._quantize_params(params, self.bits)
+        return q_params, time.perf_counter() - s_time
+
+    def _receive(self, c_params: CompressedParameters) -> Tuple[Parameters, float]:
+        assert isinstance(c_params, QuantParameters)
+        s_time = time.perf_counter()
+        items = [(name, p) for name, p in c_params.params.items() if p.data.ndim > 1 and p.data.numel() > 0]
+        decoded = _decode_stoch(items, self.CODEC, self.bits) if items else {}
+        params = {}
+        for name, p in c_params.params.items():
+            if name in decoded:
+                params[name] = decoded[name]
+            elif p.data.ndim > 1:  # empty tensor: the reference's scale == 0 branch
+                params[name] = torch.zeros_like(p.data, dtype=torch.float32)
+            else:
+                params[name] = p.data.data  # passthrough
+        return params, time.perf_counter() - s_time
+
+    def _quantize_params(self, params: Parameters, bits: int, uniforms=None, seed=None) -> QuantParameters:
+        """Biases and running metrics (ndim <= 1) are not quantized."""
+        names = [name for name, p in params.items() if p.ndim > 1 and p.numel() > 0]
+        for name in names:
+            _require_fp32(name, params[name], self.__class__.__name__)
+        encoded = _encode_stoch(params, names, self.CODEC, bits, uniforms, seed) if names else {}
+        q_params = QuantParameters({}, 0)
+        for name, param in params.items():
+            if name in encoded:
+                data, signs, scale, scale_2 = encoded[name]
+            elif param.ndim > 1:  # empty: vector_norm is 0 -> zero branch
+                data = torch.zeros_like(param, dtype=torch.uint8)
+                signs, scale, scale_2 = torch.ones_like(param, dtype=torch.int8), torch.tensor(0.0), 0
+            else:
+                data, signs, scale, scale_2 = param, torch.zeros(1, dtype=torch.uint8), 0, 0
+            q_params.params[name] = QuantParameter(data=data, bits=bits, scale=scale, signs=signs, shape=param.shape,
+                                                   dtype=param.dtype, q_dtype=data.dtype, scale_2=scale_2)
+            q_params.size += data.nbytes
+        return q_params
+
+
+class QSGDChannel(_StochChannel):
+    """Bi-directional QSGD (quant.py:140-252) on the MI355X HIP codec."""
+
+    CODEC = "qsgd"
+
+
+class RQSGDChannel(_StochChannel):
+    """Bi-directional revised QSGD (quant.py:280-398): infinity norm, minimum factor for zero levels."""
+
+    CODEC = "rqsgd"
+    NORM_BYTES = 8
+
+
+class CNATChannel(_StochChannel):
+    """Bi-directional natural compression (quant.py:426-545): stochastic power-of-two exponents."""
+
+    CODEC = "cnat"
+
+
+class _Unidirectional:
+    """Only client -> server is compressed; server -> client and the client's receive use the identity
+    channel (quant.py:255-277,401-423,548-570)."""
+
+    def on_server_send(self, params: Parameters) -> Tuple[CompressedParameters, float]:
+        return IdentityChannel(no_compute_time=True).on_server_send(params)
+
+    def on_client_receive(self, c_params: CompressedParameters) -> Tuple[Parameters, float]:
+        return IdentityChannel(no_compute_time=True).on_client_receive(c_params)
+
+
+class UQSGDChannel(_Unidirectional, QSGDChannel):
+    """Uni-directional QSGD (quant.py:255-277)."""
+
+
+class URQSGDChannel(_Unidirectional, RQSGDChannel):
+    """Uni-directional RQSGD (quant.py:401-423)."""
+
+
+class UCNATChannel(_Unidirectional, CNATChannel):
+    """Uni-directional CNAT (quant.py:548-570)."""

@@ -17,7 +17,9 @@ from . import _lib
 
 _lib.load()
 
-from . import model, ops  # noqa: E402
-from .Channel import Channel, IdentityChannel, PackedSLQChannel, SLQChannel, USLQChannel  # noqa: E402
+from . import model, ops, stoch  # noqa: E402
+from .Channel import (Channel, CNATChannel, IdentityChannel, PackedSLQChannel, QSGDChannel,  # noqa: E402
+                      RQSGDChannel, SLQChannel, UCNATChannel, UQSGDChannel, URQSGDChannel, USLQChannel)
 
-__all__ = ["Channel", "IdentityChannel", "SLQChannel", "USLQChannel", "PackedSLQChannel", "model", "ops"]
+__all__ = ["Channel", "IdentityChannel", "SLQChannel", "USLQChannel", "PackedSLQChannel", "QSGDChannel",
+           "UQSGDChannel", "RQSGDChannel", "URQSGDChannel", "CNATChannel", "UCNATChannel", "model", "ops", "stoch"]

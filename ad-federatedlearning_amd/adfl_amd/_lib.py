@@ -1,4 +1,4 @@
-"""ctypes binding of libadfl_slq.so (the C ABI declared in include/adfl_slq.h).
+"""ctypes binding of libadfl_slq.so (the C ABI declared in include/adfl_slq.h and include/adfl_stoch.h).
 
 The product path has no CPU fallback: if the HIP library is missing this module raises at import
 time, and every op checks the status code the library returns.
@@ -17,6 +17,7 @@ from ._build import LIB_PATH
 P = ctypes.c_void_p
 I32 = ctypes.c_int32
 I64 = ctypes.c_int64
+U64 = ctypes.c_uint64
 INT = ctypes.c_int
 
 ALIGN_ELEMS = 64     # ADFL_SLQ_ALIGN_ELEMS
@@ -33,7 +34,7 @@ class Chunk(ctypes.Structure):
     _fields_ = [("start", I64), ("len", I32), ("tensor", I32), ("first_chunk", I32), ("nchunks", I32)]
 
 
-# name -> (restype, argtypes); the complete exported surface of include/adfl_slq.h
+# name -> (restype, argtypes); the complete exported surface of include/adfl_slq.h + adfl_stoch.h
 SIGNATURES = {
     "adfl_slq_abi_version": (INT, []),
     "adfl_slq_strerror": (ctypes.c_char_p, [INT]),
@@ -55,7 +56,20 @@ SIGNATURES = {
     "adfl_unpack_int4": (INT, [P, I64, P, P]),
     "adfl_slq_dequantize_mean": (INT, [P, I64, I32, I64, P, I64, P, P]),
     "adfl_slq_dequantize_mean_int4": (INT, [P, I64, I32, I64, P, I64, P, P]),
+    # adfl_stoch.h
+    "adfl_stoch_workspace_bytes": (I64, [I64]),
+    "adfl_stoch_norms_batched": (INT, [P, P, I64, INT, P, I64, P, P, P]),
+    "adfl_qsgd_quantize_batched": (INT, [P, P, I64, INT, P, P, U64, U64, P, P, P]),
+    "adfl_qsgd_encode_batched": (INT, [P, P, I64, INT, P, U64, U64, P, I64, P, P, P, P]),
+    "adfl_rqsgd_encode_batched": (INT, [P, P, I64, INT, P, U64, U64, P, I64, P, P, P, P, P]),
+    "adfl_qsgd_dequantize_batched": (INT, [P, P, P, I64, INT, P, P, P]),
+    "adfl_rqsgd_dequantize_batched": (INT, [P, P, P, I64, INT, P, P, P, P]),
+    "adfl_cnat_encode_batched": (INT, [P, P, I64, INT, P, U64, U64, P, I64, P, P, P, P]),
+    "adfl_cnat_dequantize_batched": (INT, [P, P, P, I64, P, P, P]),
+    "adfl_philox_uniforms": (INT, [P, I64, I64, U64, U64, P]),
 }
+
+NORM_L2, NORM_LINF = 0, 1  # ADFL_NORM_*
 
 _lib = None
 

@@ -1,0 +1,206 @@
+"""Device-resident stochastic codec ops (QSGD / RQSGD / CNAT) over the HIP C ABI (include/adfl_stoch.h).
+
+Every function takes and returns CUDA (HIP) tensors over a bucketed flat buffer described by an
+``ops.BucketLayout``, launches on the current stream and never synchronises:
+
+* ``qsgd_encode_batched`` / ``qsgd_decode_batched``   — QSGDChannel._quantize_tensor / _dequantize_tensor
+  (Src/ADFL/Channel/quant.py:223-252)
+* ``rqsgd_encode_batched`` / ``rqsgd_decode_batched`` — RQSGDChannel (quant.py:364-398)
+* ``cnat_encode_batched`` / ``cnat_decode_batched``   — CNATChannel (quant.py:509-545)
+* ``norms_batched`` — per-tensor ||x||_2 or (max|x|, min|x|); ``qsgd_quantize_batched`` — levels from
+  given norms (what the parity tests use to inject the reference's own norm)
+
+Randomness: pass ``uniforms`` (fp32 plane indexed like x, values in [0, 1)) to inject the reference's
+``torch.rand_like`` draws, or leave it None to draw from the Philox4x32-10 stream ``(seed, counter)``.
+``RngStream`` hands out (seed, counter) pairs seeded from torch's default CPU generator, so
+``torch.manual_seed`` makes a run reproducible the way it does for the reference.
+"""
+
+from typing import Optional, Tuple
+
+import torch
+
+from . import _lib
+from ._lib import NORM_L2, NORM_LINF, check
+from .ops import BucketLayout, _dev, _stream
+
+__all__ = ["RngStream", "norms_batched", "qsgd_quantize_batched", "qsgd_encode_batched", "rqsgd_encode_batched",
+           "qsgd_decode_batched", "rqsgd_decode_batched", "cnat_encode_batched", "cnat_decode_batched",
+           "philox_uniforms", "workspace", "NORM_L2", "NORM_LINF"]
+
+
+class RngStream:
+    """(seed, counter) pairs for successive encode calls. The seed is drawn from torch's default CPU
+    generator at construction (the generator the reference's torch.rand_like consumes); each call
+    advances the counter past the uniforms it used, so no two calls share a uniform."""
+
+    def __init__(self, seed: Optional[int] = None):
+        if seed is None:
+            seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+        self.seed = int(seed) & (2 ** 64 - 1)
+        self.counter = 0
+
+    def take(self, numel: int) -> Tuple[int, int]:
+        c = self.counter
+        self.counter += (int(numel) + 3) // 4
+        return self.seed, c
+
+
+def workspace(layout: BucketLayout, device) -> torch.Tensor:
+    return torch.empty(int(_lib.load().adfl_stoch_workspace_bytes(layout.nchunks)), dtype=torch.uint8, device=device)
+
+
+def _check_flat(flat: torch.Tensor, layout: BucketLayout) -> torch.Tensor:
+    if flat.dtype != torch.float32:
+        raise ValueError(f"adfl_amd.stoch: the HIP stochastic codecs take fp32 buckets, got {flat.dtype}")
+    flat = _dev(flat, "flat")
+    if flat.numel() < layout.total:
+        raise ValueError("adfl_amd.stoch: flat buffer smaller than the layout")
+    return flat
+
+
+def _uniforms(u: Optional[torch.Tensor], layout: BucketLayout) -> int:
+    if u is None:
+        return 0
+    if u.dtype != torch.float32 or u.numel() < layout.total:
+        raise ValueError("adfl_amd.stoch: uniforms must be an fp32 plane covering the layout")
+    if not u.is_cuda or not u.is_contiguous() or u.data_ptr() % 16:
+        raise ValueError("adfl_amd.stoch: uniforms must be a contiguous, 16-byte aligned device tensor")
+    return u.data_ptr()
+
+
+def _ws(ws: Optional[torch.Tensor], layout: BucketLayout, dev) -> torch.Tensor:
+    return workspace(layout, dev) if ws is None else ws
+
+
+def norms_batched(flat: torch.Tensor, layout: BucketLayout, mode: int = NORM_L2, *,
+                  norms: Optional[torch.Tensor] = None, mins: Optional[torch.Tensor] = None,
+                  ws: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """Per-tensor ||x||_2 (mode NORM_L2) or (max|x|, min|x|) (NORM_LINF)."""
+    flat = _check_flat(flat, layout)
+    dev = flat.device
+    norms = torch.empty(layout.ntensors, dtype=torch.float32, device=dev) if norms is None else norms
+    if mode == NORM_LINF and mins is None:
+        mins = torch.empty(layout.ntensors, dtype=torch.float32, device=dev)
+    ws = _ws(ws, layout, dev)
+    check(_lib.load().adfl_stoch_norms_batched(flat.data_ptr(), layout.device_chunks(dev).data_ptr(), layout.nchunks,
+                                               mode, ws.data_ptr(), ws.numel(), norms.data_ptr(),
+                                               mins.data_ptr() if mins is not None else None, _stream(dev)))
+    return norms, mins
+
+
+def _planes(layout, dev, levels, signs, ldtype):
+    levels = torch.empty(layout.total, dtype=ldtype, device=dev) if levels is None else levels
+    signs = torch.empty(layout.total, dtype=torch.int8, device=dev) if signs is None else signs
+    return levels, signs
+
+
+def qsgd_quantize_batched(flat: torch.Tensor, layout: BucketLayout, bits: int, norms: torch.Tensor, *,
+                          uniforms: Optional[torch.Tensor] = None, seed: int = 0, counter: int = 0,
+                          levels: Optional[torch.Tensor] = None,
+                          signs: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Levels + signs from given per-tensor norms (QSGD: L2 norms; RQSGD: max|x|)."""
+    flat = _check_flat(flat, layout)
+    dev = flat.device
+    levels, signs = _planes(layout, dev, levels, signs, torch.uint8)
+    check(_lib.load().adfl_qsgd_quantize_batched(flat.data_ptr(), layout.device_chunks(dev).data_ptr(),
+                                                 layout.nchunks, bits, _dev(norms, "norms").data_ptr(),
+                                                 _uniforms(uniforms, layout), seed, counter, levels.data_ptr(),
+                                                 signs.data_ptr(), _stream(dev)))
+    return levels, signs
+
+
+def qsgd_encode_batched(flat: torch.Tensor, layout: BucketLayout, bits: int, *,
+                        uniforms: Optional[torch.Tensor] = None, seed: int = 0, counter: int = 0,
+                        levels: Optional[torch.Tensor] = None, signs: Optional[torch.Tensor] = None,
+                        norms: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None):
+    """QSGD encode of every tensor of a bucket: (levels u8, signs i8, L2 norms f32)."""
+    flat = _check_flat(flat, layout)
+    dev = flat.device
+    levels, signs = _planes(layout, dev, levels, signs, torch.uint8)
+    norms = torch.empty(layout.ntensors, dtype=torch.float32, device=dev) if norms is None else norms
+    ws = _ws(ws, layout, dev)
+    check(_lib.load().adfl_qsgd_encode_batched(flat.data_ptr(), layout.device_chunks(dev).data_ptr(), layout.nchunks,
+                                               bits, _uniforms(uniforms, layout), seed, counter, ws.data_ptr(),
+                                               ws.numel(), levels.data_ptr(), signs.data_ptr(), norms.data_ptr(),
+                                               _stream(dev)))
+    return levels, signs, norms
+
+
+def rqsgd_encode_batched(flat: torch.Tensor, layout: BucketLayout, bits: int, *,
+                         uniforms: Optional[torch.Tensor] = None, seed: int = 0, counter: int = 0,
+                         levels: Optional[torch.Tensor] = None, signs: Optional[torch.Tensor] = None,
+                         norms: Optional[torch.Tensor] = None, mins: Optional[torch.Tensor] = None,
+                         ws: Optional[torch.Tensor] = None):
+    """RQSGD encode: (levels u8, signs i8, max|x| norms f32, min|x| factors f32)."""
+    flat = _check_flat(flat, layout)
+    dev = flat.device
+    levels, signs = _planes(layout, dev, levels, signs, torch.uint8)
+    norms = torch.empty(layout.ntensors, dtype=torch.float32, device=dev) if norms is None else norms
+    mins = torch.empty(layout.ntensors, dtype=torch.float32, device=dev) if mins is None else mins
+    ws = _ws(ws, layout, dev)
+    check(_lib.load().adfl_rqsgd_encode_batched(flat.data_ptr(), layout.device_chunks(dev).data_ptr(),
+                                                layout.nchunks, bits, _uniforms(uniforms, layout), seed, counter,
+                                                ws.data_ptr(), ws.numel(), levels.data_ptr(), signs.data_ptr(),
+                                                norms.data_ptr(), mins.data_ptr(), _stream(dev)))
+    return levels, signs, norms, mins
+
+
+def qsgd_decode_batched(levels: torch.Tensor, signs: torch.Tensor, norms: torch.Tensor, layout: BucketLayout,
+                        bits: int, *, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    levels, signs = _dev(levels, "levels"), _dev(signs, "signs")
+    dev = levels.device
+    out = torch.empty(layout.total, dtype=torch.float32, device=dev) if out is None else out
+    check(_lib.load().adfl_qsgd_dequantize_batched(levels.data_ptr(), signs.data_ptr(),
+                                                   layout.device_chunks(dev).data_ptr(), layout.nchunks, bits,
+                                                   _dev(norms, "norms").data_ptr(), out.data_ptr(), _stream(dev)))
+    return out
+
+
+def rqsgd_decode_batched(levels: torch.Tensor, signs: torch.Tensor, norms: torch.Tensor, mins: torch.Tensor,
+                         layout: BucketLayout, bits: int, *, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    levels, signs = _dev(levels, "levels"), _dev(signs, "signs")
+    dev = levels.device
+    out = torch.empty(layout.total, dtype=torch.float32, device=dev) if out is None else out
+    check(_lib.load().adfl_rqsgd_dequantize_batched(levels.data_ptr(), signs.data_ptr(),
+                                                    layout.device_chunks(dev).data_ptr(), layout.nchunks, bits,
+                                                    _dev(norms, "norms").data_ptr(), _dev(mins, "mins").data_ptr(),
+                                                    out.data_ptr(), _stream(dev)))
+    return out
+
+
+def cnat_encode_batched(flat: torch.Tensor, layout: BucketLayout, bits: int, *,
+                        uniforms: Optional[torch.Tensor] = None, seed: int = 0, counter: int = 0,
+                        exps: Optional[torch.Tensor] = None, signs: Optional[torch.Tensor] = None,
+                        norms: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None):
+    """CNAT encode (x read once): (exponents i8, signs i8, L2 norms f32). A tensor whose norm is 0 gets
+    the reference's zero-branch bytes (0 / 1)."""
+    flat = _check_flat(flat, layout)
+    dev = flat.device
+    exps, signs = _planes(layout, dev, exps, signs, torch.int8)
+    norms = torch.empty(layout.ntensors, dtype=torch.float32, device=dev) if norms is None else norms
+    ws = _ws(ws, layout, dev)
+    check(_lib.load().adfl_cnat_encode_batched(flat.data_ptr(), layout.device_chunks(dev).data_ptr(), layout.nchunks,
+                                               bits, _uniforms(uniforms, layout), seed, counter, ws.data_ptr(),
+                                               ws.numel(), exps.data_ptr(), signs.data_ptr(), norms.data_ptr(),
+                                               _stream(dev)))
+    return exps, signs, norms
+
+
+def cnat_decode_batched(exps: torch.Tensor, signs: torch.Tensor, norms: torch.Tensor, layout: BucketLayout, *,
+                        out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    exps, signs = _dev(exps, "exps"), _dev(signs, "signs")
+    dev = exps.device
+    out = torch.empty(layout.total, dtype=torch.float32, device=dev) if out is None else out
+    check(_lib.load().adfl_cnat_dequantize_batched(exps.data_ptr(), signs.data_ptr(),
+                                                   layout.device_chunks(dev).data_ptr(), layout.nchunks,
+                                                   _dev(norms, "norms").data_ptr(), out.data_ptr(), _stream(dev)))
+    return out
+
+
+def philox_uniforms(n: int, seed: int, counter: int, start: int = 0, *, device=None) -> torch.Tensor:
+    """The uniforms elements start .. start+n-1 of stream (seed, counter) draw."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    out = torch.empty(n, dtype=torch.float32, device=dev)
+    check(_lib.load().adfl_philox_uniforms(out.data_ptr(), n, start, seed & (2 ** 64 - 1), counter, _stream(dev)))
+    return out

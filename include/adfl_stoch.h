@@ -1,0 +1,100 @@
+/*
+ * adfl_stoch.h — C ABI of the MI355X (gfx950) stochastic gradient codecs in libadfl_slq.so:
+ * QSGD / RQSGD / CNAT (Src/ADFL/Channel/quant.py:140-570).
+ *
+ * Same conventions as adfl_slq.h (device pointers d_*, 16-byte aligned bases, int64 counts, void*
+ * hipStream_t, asynchronous, no allocation, graph-capturable, 0 / hipError_t / ADFL_E_* returns) and the
+ * same bucket description: an adfl_slq_chunk table from adfl_slq_build_chunks() over a flat buffer in
+ * which tensor t owns elements [offset_t, offset_t + size_t). A single tensor is a one-entry table.
+ *
+ * Payload planes (what the reference's QuantParameter holds, quant.py:209-217,349-358,495-503):
+ *   levels  uint8, one per element — QSGD/RQSGD quantization level l in [0, 2^bits - 1], or CNAT's
+ *           int8 exponent in [-2^(bits-1), 2^(bits-1) - 1] (stored as its byte)
+ *   signs   int8, one per element — torch.sign(x) in {-1, 0, 1} (NaN -> 0)
+ *   norms   fp32, one per tensor — QSGD/CNAT: ||x||_2; RQSGD: max|x| (+ mins = min|x|)
+ * Both planes are indexed like x (byte g of a plane belongs to element g of the bucket).
+ *
+ * Uniforms. Stochastic rounding compares u in [0, 1) with a per-element probability. d_uniforms == NULL
+ * draws u from the counter-based Philox4x32-10 stream keyed by `seed`: element g of the bucket uses word
+ * g % 4 of block (counter + g / 4), u = (word >> 8) * 2^-24. A caller that advances `counter` by
+ * ceil(total / 4) per call never reuses a uniform. d_uniforms != NULL injects one fp32 uniform per
+ * element (indexed like x) — with the reference's own uniforms the outputs are bit-identical to it.
+ *
+ * Norm: fp32 squares accumulated in fp64 per chunk and per tensor (fixed order: deterministic), rounded
+ * once to fp32, correctly rounded sqrt. torch's fp32 vector_norm differs from it only by torch's own
+ * accumulation error; every other output bit follows the reference exactly.
+ */
+#ifndef ADFL_STOCH_H
+#define ADFL_STOCH_H
+
+#include <stdint.h>
+
+#include "adfl_slq.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { ADFL_NORM_L2 = 0, ADFL_NORM_LINF = 1 };
+
+/* Device workspace bytes the encode / norm calls need for a table of nchunks chunks (16 B per chunk). */
+int64_t adfl_stoch_workspace_bytes(int64_t nchunks);
+
+/* Per-tensor norms of a bucket (two launches: chunk partials, per-tensor finalize).
+ *   ADFL_NORM_L2:   d_norms[t] = ||x_t||_2   (torch.linalg.vector_norm(x, ord=2), quant.py:226,512)
+ *   ADFL_NORM_LINF: d_norms[t] = max|x_t|, d_mins[t] = min|x_t| (ord=inf / -inf, quant.py:367,380);
+ *                   NaN anywhere in x_t makes both NaN. d_mins may be NULL for ADFL_NORM_L2. */
+int adfl_stoch_norms_batched(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, int mode,
+                             void* d_workspace, int64_t workspace_bytes, float* d_norms, float* d_mins,
+                             void* stream);
+
+/* QSGD / RQSGD level quantization given per-tensor norms (quant.py:230-238 and :371-379), levels =
+ * 2^bits - 1: scaled = fl(fl(levels*|x|) / norm); l = floor(scaled); q = u8(l + (u < scaled - l));
+ * norm == 0 gives levels 0 and signs 1 (quant.py:227-228). One launch. */
+int adfl_qsgd_quantize_batched(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, int bits,
+                               const float* d_norms, const float* d_uniforms, uint64_t seed, uint64_t counter,
+                               uint8_t* d_levels, int8_t* d_signs, void* stream);
+
+/* QSGDChannel._quantize_tensor over a bucket (quant.py:223-240): L2 norms + quantize (three launches). */
+int adfl_qsgd_encode_batched(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, int bits,
+                             const float* d_uniforms, uint64_t seed, uint64_t counter, void* d_workspace,
+                             int64_t workspace_bytes, uint8_t* d_levels, int8_t* d_signs, float* d_norms,
+                             void* stream);
+
+/* RQSGDChannel._quantize_tensor (quant.py:364-382): max|x| norms, min|x| factors + quantize. */
+int adfl_rqsgd_encode_batched(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, int bits,
+                              const float* d_uniforms, uint64_t seed, uint64_t counter, void* d_workspace,
+                              int64_t workspace_bytes, uint8_t* d_levels, int8_t* d_signs, float* d_norms,
+                              float* d_mins, void* stream);
+
+/* QSGDChannel._dequantize_tensor (quant.py:243-252): out = fl(fl(norm*l) / levels) * sign; 0 if norm == 0. */
+int adfl_qsgd_dequantize_batched(const uint8_t* d_levels, const int8_t* d_signs, const adfl_slq_chunk* d_chunks,
+                                 int64_t nchunks, int bits, const float* d_norms, float* d_out, void* stream);
+
+/* RQSGDChannel._dequantize_tensor (quant.py:385-398): out = fl(fl(norm*sign)*l) / levels, and
+ * min*sign where l == 0; 0 if norm == 0. */
+int adfl_rqsgd_dequantize_batched(const uint8_t* d_levels, const int8_t* d_signs, const adfl_slq_chunk* d_chunks,
+                                  int64_t nchunks, int bits, const float* d_norms, const float* d_mins,
+                                  float* d_out, void* stream);
+
+/* CNATChannel._quantize_tensor (quant.py:509-534) in one pass over x (exponents, signs and the L2 norm
+ * partials together), then a per-tensor finalize and the norm == 0 rewrite (levels 0, signs 1,
+ * quant.py:513-514): three launches, x read once. d_exps holds each exponent's int8 byte. */
+int adfl_cnat_encode_batched(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, int bits,
+                             const float* d_uniforms, uint64_t seed, uint64_t counter, void* d_workspace,
+                             int64_t workspace_bytes, int8_t* d_exps, int8_t* d_signs, float* d_norms,
+                             void* stream);
+
+/* CNATChannel._dequantize_tensor (quant.py:537-545): out = fl(fl(norm*sign) * 2^e); 0 if norm == 0. */
+int adfl_cnat_dequantize_batched(const int8_t* d_exps, const int8_t* d_signs, const adfl_slq_chunk* d_chunks,
+                                 int64_t nchunks, const float* d_norms, float* d_out, void* stream);
+
+/* The Philox uniforms the codecs draw: d_out[i] = u(start + i) of stream (seed, counter), i < n.
+ * (Exposed for tests and for callers that want the uniforms a call used.) */
+int adfl_philox_uniforms(float* d_out, int64_t n, int64_t start, uint64_t seed, uint64_t counter, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ADFL_STOCH_H */

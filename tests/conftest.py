@@ -8,6 +8,7 @@ import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(REPO, "tests", "golden")
 for p in (os.path.join(REPO, "ad-federatedlearning_amd"), os.path.join(REPO, "oracle"),
           os.path.join(REPO, "tests"), os.path.join(REPO, "tests", "golden"), REPO):
     if p not in sys.path:

@@ -1,4 +1,4 @@
-"""CPU: the C-ABI library loads and exports every symbol include/adfl_slq.h declares; argument checks
+"""CPU: the C-ABI library loads and exports every symbol include/*.h declares; argument checks
 and host-side chunk planning work without a GPU (no kernel is launched by any call here)."""
 
 import ctypes
@@ -11,13 +11,21 @@ import pytest
 from adfl_amd import _lib
 from adfl_amd._build import LIB_PATH
 
-HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "adfl_slq.h")
+INCLUDE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+HEADER = os.path.join(INCLUDE, "adfl_slq.h")
+HEADERS = sorted(os.path.join(INCLUDE, h) for h in os.listdir(INCLUDE) if h.endswith(".h"))
 
 
 def declared_functions():
-    text = open(HEADER).read()
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b(adfl_\w+)\s*\(", text, flags=re.M)))
+    names = set()
+    for h in HEADERS:
+        text = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        names |= set(re.findall(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b(adfl_\w+)\s*\(", text, flags=re.M))
+    return sorted(names)
+
+
+def test_headers_present():
+    assert [os.path.basename(h) for h in HEADERS] == ["adfl_slq.h", "adfl_stoch.h"]
 
 
 def test_header_declares_the_binding_table():
@@ -67,6 +75,29 @@ def test_argument_errors_return_codes_without_launching():
     assert lib.adfl_slq_encode_batched(16, 16, 0, 8, 16, 16, 16, None) == -1
     with pytest.raises(_lib.AdflError, match="bits"):
         _lib.check(-2)
+
+
+def test_stochastic_argument_errors_return_codes_without_launching():
+    lib = _lib.load()
+    assert lib.adfl_stoch_workspace_bytes(100) == 1600
+    # norms: bad mode, small workspace, misaligned x
+    assert lib.adfl_stoch_norms_batched(16, 16, 1, 7, 16, 1 << 20, 16, 16, None) == -1
+    assert lib.adfl_stoch_norms_batched(16, 16, 4, 0, 16, 63, 16, None, None) == -4
+    assert lib.adfl_stoch_norms_batched(20, 16, 1, 0, 16, 1 << 20, 16, None, None) == -3
+    assert lib.adfl_stoch_norms_batched(16, None, 1, 0, 16, 1 << 20, 16, None, None) == -1
+    # quantize / encode: bits, null planes, misaligned uniforms
+    assert lib.adfl_qsgd_quantize_batched(16, 16, 1, 0, 16, None, 0, 0, 16, 16, None) == -2
+    assert lib.adfl_qsgd_quantize_batched(16, 16, 1, 8, 16, None, 0, 0, None, 16, None) == -1
+    assert lib.adfl_qsgd_quantize_batched(16, 16, 1, 8, 16, 20, 0, 0, 16, 16, None) == -3
+    assert lib.adfl_qsgd_encode_batched(16, 16, 1, 17, None, 0, 0, 16, 1 << 20, 16, 16, 16, None) == -2
+    assert lib.adfl_rqsgd_encode_batched(16, 16, 1, 8, None, 0, 0, 16, 1 << 20, 16, 16, 16, None, None) == -1
+    assert lib.adfl_cnat_encode_batched(16, 16, 1, 8, None, 0, 0, 16, 8, 16, 16, 16, None) == -4
+    assert lib.adfl_cnat_encode_batched(16, 16, 0, 8, None, 0, 0, 16, 1 << 20, 16, 16, 16, None) == -1
+    # decoders
+    assert lib.adfl_qsgd_dequantize_batched(16, 16, 16, 1, 8, 16, 20, None) == -3
+    assert lib.adfl_rqsgd_dequantize_batched(16, 16, 16, 1, 8, 16, None, 16, None) == -1
+    assert lib.adfl_cnat_dequantize_batched(16, 16, 16, 1, None, 16, None) == -1
+    assert lib.adfl_philox_uniforms(16, 0, 0, 1, 0, None) == -1
 
 
 def test_build_chunks_host_planning():

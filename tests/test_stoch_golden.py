@@ -1,0 +1,153 @@
+"""CPU: the stochastic-codec oracle (oracle/stoch_oracle.py) against the reference's own outputs.
+
+tests/golden/stoch.npz was produced by executing the reference QSGD / RQSGD / CNAT channels
+(Src/ADFL/Channel/quant.py:140-570) with recorded uniforms in place of torch.rand_like
+(tests/golden/make_golden_stoch.py). Given the reference's norm and the same uniforms, every level /
+exponent byte, sign and decoded float must match bit for bit; the oracle's own L2 norm must agree with
+torch's within torch's fp32 accumulation error bound (n * 2^-24 relative), and max/min norms exactly.
+"""
+
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from golden_util import same_f32
+
+import stoch_oracle as so
+
+MANIFEST = json.load(open(os.path.join(GOLDEN, "stoch_manifest.json")))
+ARR = np.load(os.path.join(GOLDEN, "stoch.npz"))
+CASES = MANIFEST["cases"]
+
+
+def _scale(rec) -> np.float32:
+    if "int" in rec:
+        return np.float32(rec["int"])
+    return np.array([rec["bits"]], np.uint32).view(np.float32)[0]
+
+
+def load_case(c):
+    n = c["name"]
+    return (ARR[f"{n}__x"], ARR[f"{n}__u"], ARR[f"{n}__q"], ARR[f"{n}__signs"], ARR[f"{n}__deq"],
+            _scale(c["scale"]), _scale(c["scale_2"]))
+
+
+@pytest.mark.parametrize("c", CASES, ids=[c["name"] for c in CASES])
+def test_oracle_matches_reference(c):
+    x, u, q_ref, s_ref, d_ref, norm, scale2 = load_case(c)
+    bits = c["bits"]
+    levels = 2 ** bits - 1
+    if c["codec"] == "cnat":
+        q, s = so.cnat_quantize(x, bits, norm, u)
+        d = so.cnat_dequantize(q_ref.view(np.int8) if c["q_dtype"] == "int8" else q_ref, s_ref, norm)
+    else:
+        q, s = so.qsgd_quantize(x, levels, norm, u)
+        if c["codec"] == "qsgd":
+            d = so.qsgd_dequantize(q_ref, s_ref, levels, norm)
+        else:
+            d = so.rqsgd_dequantize(q_ref, s_ref, levels, norm, scale2)
+    assert str(q.dtype) == c["q_dtype"]
+    np.testing.assert_array_equal(q.view(np.uint8), q_ref)
+    np.testing.assert_array_equal(s, s_ref)
+    assert same_f32(d, d_ref)
+
+
+@pytest.mark.parametrize("c", CASES, ids=[c["name"] for c in CASES])
+def test_oracle_norms(c):
+    x, _, _, _, _, norm, scale2 = load_case(c)
+    zero_branch = c["scale"].get("tensor", False)
+    if c["codec"] == "rqsgd":
+        assert same_f32(np.float32(so.linf_norm(x)), np.float32(norm))
+        if not zero_branch:
+            assert same_f32(np.float32(so.lminf_norm(x)), scale2)
+        return
+    mine = so.l2_norm(x)
+    if np.isnan(norm) or np.isinf(norm) or norm == 0:
+        assert same_f32(np.float32(mine), np.float32(norm))  # NaN / overflow / underflow behave as torch's
+        return
+    bound = max(x.size * 2.0 ** -24, 2.0 ** -23)
+    assert abs(float(mine) - float(norm)) <= bound * float(norm), (mine, norm)
+
+
+def test_golden_covers_the_reference_branches():
+    kinds = {(c["codec"], c["q_dtype"], "tensor" in c["scale"]) for c in CASES}
+    for codec in ("qsgd", "rqsgd", "cnat"):
+        assert (codec, "uint8", True) in kinds  # norm == 0 branch (zeros_like u8, ones signs, tensor scale)
+    assert ("cnat", "int8", False) in kinds
+    assert {c["rand_calls"] for c in CASES if "tensor" not in c["scale"]} == {1}
+    assert any(c["bits"] == 9 for c in CASES)
+
+
+def test_levels_and_exponent_byte_rules():
+    # torch's fp32 -> u8 / i8: low byte of the truncated int32, NaN -> 0 (probed on this torch build)
+    v = np.array([np.nan, 300.0, 256.0, 255.5, -1.0, 1e9, -300.0], np.float32)
+    assert so.to_u8(v).tolist() == torch.from_numpy(v).to(torch.uint8).tolist()
+    assert so.to_i8(v).tolist() == torch.from_numpy(v).to(torch.int8).tolist()
+
+
+def test_cnat_log2_rule_against_torch_near_powers_of_two():
+    """The restated log2 (float64 log2 rounded once) makes torch's floor/ceil decision. Exhaustively
+    checked offline over all fp32 >= 2^-23 (tools/check_log2_exhaustive.py); here on +-4096 ulps around
+    every power of two CNAT can meet, plus 2^22 random values."""
+    vals = []
+    for k in range(-23, 128):
+        b = int(np.array([2.0 ** k], np.float32).view(np.uint32)[0])
+        lo = max(b - 4096, int(np.array([2.0 ** -23], np.float32).view(np.uint32)[0]))
+        vals.append(np.arange(lo, b + 4096, dtype=np.uint32))
+    rng = np.random.default_rng(5)
+    vals.append(rng.integers(0x34000000, 0x7F7FFFFF, size=1 << 22, dtype=np.uint32))
+    v = np.concatenate(vals).view(np.float32)
+    lt = torch.log2(torch.from_numpy(v)).numpy()
+    lc = so.log2_f32(v)
+    np.testing.assert_array_equal(np.floor(lt), np.floor(lc))
+    np.testing.assert_array_equal(np.ceil(lt), np.ceil(lc))
+
+
+def test_cnat_band_table_matches_restatement():
+    """ad-federatedlearning_amd/csrc/cnat_log2_table.h (the HIP kernel's exact rule) reproduces the
+    restated floor/ceil on the same near-power-of-two set."""
+    import re
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(GOLDEN)), "tools"))
+    import gen_cnat_table as g
+    text = open(g.OUT).read()
+    rows = [(int(a), int(b)) for a, b in re.findall(r"\{(\d+)u, (\d+)u\}", text)]
+    below, above = [r[0] for r in rows], [r[1] for r in rows]
+    assert len(rows) == g.K_MAX - g.K_MIN + 1
+    assert (below, above) == tuple(map(list, g.bands()))
+    vals = []
+    for k in range(-22, 128):
+        b = int(np.array([2.0 ** k], np.float32).view(np.uint32)[0])
+        vals.append(np.arange(b - 2048, min(b + 2048, 0x7F7FFFFF), dtype=np.uint32))
+    bits = np.concatenate(vals)
+    f, c = g.band_rule(bits, below, above)
+    lc = so.log2_f32(bits.view(np.float32))
+    np.testing.assert_array_equal(f, np.floor(lc))
+    np.testing.assert_array_equal(c, np.ceil(lc))
+
+
+def test_philox_known_answer():
+    """Philox4x32-10 known-answer vectors (Random123 kat_vectors, philox4x32 10 rounds): counter 0 / key 0,
+    counter all-ones / key all-ones, and the pi-digits counter / key."""
+    def words(c, k):
+        w = so.philox4x32(np.array([c[0]], np.uint64), np.array([c[1]], np.uint64), k[0] | (k[1] << 32), c[2], c[3])
+        return [int(a[0]) for a in w]
+    assert words((0, 0, 0, 0), (0, 0)) == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
+    ones = 0xFFFFFFFF
+    assert words((ones,) * 4, (ones, ones)) == [0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD]
+    assert words((0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344), (0xA4093822, 0x299F31D0)) == \
+        [0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1]
+
+
+def test_philox_uniform_range_and_layout():
+    u = so.philox_uniforms(4096, seed=123, counter=7)
+    assert u.dtype == np.float32 and (u >= 0).all() and (u < 1).all()
+    assert abs(float(u.mean()) - 0.5) < 0.02
+    # element e of a stream = element e - start of the same stream started at `start`
+    np.testing.assert_array_equal(so.philox_uniforms(100, 123, 7, start=13), u[13:113])
+    # counter advance by c blocks == skipping 4c elements
+    np.testing.assert_array_equal(so.philox_uniforms(64, 123, 9), u[8:72])

@@ -62,11 +62,14 @@ int main() {
     return 2;
   }
   CK(hipDeviceSynchronize());
+  printf("int8 round trip done\n");
+  fflush(stdout);
   float s;
   CK(hipMemcpy(&s, scale, 4, hipMemcpyDeviceToHost));
   const float s_ref = 7.5f / 127.f, inv = 1.f / s_ref;
   int bad = (s != s_ref);
-  const int64_t spans[3][2] = {{0, 8192}, {(1ll << 31) - 8192, (1ll << 31) + 8192}, {n - 8192, n}};
+  // the last span straddles element 2^31 and ends at n (the buffer end)
+  const int64_t spans[3][2] = {{0, 8192}, {1ll << 30, (1ll << 30) + 8192}, {n - 16384, n}};
   std::vector<int8_t> qh(16384);
   std::vector<float> oh(16384);
   for (auto& sp : spans) {
