@@ -10,6 +10,10 @@ bench.py measures the headline (C2). This tool measures the rest on the same cod
             (--packed --chunks 8 --elems 1073741824 for C5's int4 pipelined variant). torchrun N>1.
   pcie      the same 1 GiB round trip starting and ending in pinned host memory
             (H2D 4N, D2H N, H2D N, D2H 4N), the rate DESIGN.md reports next to the device-resident one
+  stoch     QSGD / RQSGD / CNAT (bits=8) device-resident encode + decode on the C2 tensor (2^28 fp32) and on
+            the C3 bucket, in-kernel Philox uniforms; algorithmic bytes: QSGD/RQSGD encode 10N (norm pass
+            4N + quantize 4N read, 2N levels+signs write), CNAT encode 6N (one pass), every decode 6N;
+            plus the reference's ATen op sequence timed on a 2^22-element host sample
 
     python tools/bench_configs.py --mode c3
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 tools/bench_configs.py --mode exchange
@@ -254,9 +258,102 @@ def mode_channel(args, world, rank, dev):
             "reference_threads": torch.get_num_threads(), "identical_output": same}
 
 
+def _ref_stoch_cpu(codec, x, bits=8):
+    """The reference's op sequence (quant.py:223-252 / 364-398 / 509-545) on a host tensor, in seconds."""
+    s = 2 ** bits - 1
+    t0 = time.perf_counter()
+    if codec == "cnat":
+        norm = torch.linalg.vector_norm(x, ord=2)
+        signs = torch.sign(x).to(torch.int8)
+        xa = torch.abs(x)
+        lg = torch.log2(xa + torch.finfo(x.dtype).eps)
+        f, c = torch.floor(lg), torch.ceil(lg)
+        prob = (2 ** c - xa) / 2 ** f
+        e = torch.where(torch.rand_like(prob) < prob, f, c).clamp_(-128, 127)
+        e[x == 0] = -128
+        e = e.to(torch.int8)
+        t1 = time.perf_counter()
+        _ = norm.item() * signs.float() * (2 ** e.float())
+    else:
+        norm = torch.linalg.vector_norm(x, ord=2 if codec == "qsgd" else float("inf"))
+        scaled = s * torch.abs(x) / norm
+        lo = torch.floor(scaled)
+        q = (lo + (torch.rand_like(scaled) < scaled - lo).float()).to(torch.uint8)
+        signs = torch.sign(x).to(torch.int8)
+        if codec == "rqsgd":
+            mf = torch.linalg.vector_norm(x, ord=-float("inf")).item()
+        t1 = time.perf_counter()
+        r = norm.item() * signs.float() * q.float() / s
+        if codec == "rqsgd":
+            z = q == 0
+            r[z] = mf * signs[z].float()
+    return t1 - t0, time.perf_counter() - t1
+
+
+def mode_stoch(args, world, rank, dev):
+    from adfl_amd import ops, stoch
+    n_flat = args.elems or (1 << 28)
+    base, rem = divmod(RESNET18, 256)
+    workloads = {"c2_flat": [n_flat], "c3_bucket": [base + (1 if i < rem else 0) for i in range(256)]}
+    res = {}
+    for wname, sizes in workloads.items():
+        lay = ops.BucketLayout(sizes, align=1)
+        g = torch.Generator(device=dev).manual_seed(rank)
+        x = torch.randn(lay.total, device=dev, generator=g) * 1e-3
+        lv = torch.empty(lay.total, dtype=torch.uint8, device=dev)
+        sg = torch.empty(lay.total, dtype=torch.int8, device=dev)
+        nr = torch.empty(lay.ntensors, device=dev)
+        mn = torch.empty(lay.ntensors, device=dev)
+        out = torch.empty(lay.total, device=dev)
+        ws = stoch.workspace(lay, dev)
+        n = lay.total
+        for codec in ("qsgd", "rqsgd", "cnat"):
+            def step(ev, codec=codec):
+                if ev is not None:
+                    ev[0].record()
+                if codec == "qsgd":
+                    stoch.qsgd_encode_batched(x, lay, 8, seed=7, counter=0, levels=lv, signs=sg, norms=nr, ws=ws)
+                elif codec == "rqsgd":
+                    stoch.rqsgd_encode_batched(x, lay, 8, seed=7, counter=0, levels=lv, signs=sg, norms=nr, mins=mn,
+                                               ws=ws)
+                else:
+                    stoch.cnat_encode_batched(x, lay, 8, seed=7, counter=0, exps=lv.view(torch.int8), signs=sg,
+                                              norms=nr, ws=ws)
+                if ev is not None:
+                    ev[1].record()
+                if codec == "qsgd":
+                    stoch.qsgd_decode_batched(lv, sg, nr, lay, 8, out=out)
+                elif codec == "rqsgd":
+                    stoch.rqsgd_decode_batched(lv, sg, nr, mn, lay, 8, out=out)
+                else:
+                    stoch.cnat_decode_batched(lv.view(torch.int8), sg, nr, lay, out=out)
+                if ev is not None:
+                    ev[2].record()
+            wall, evs = timed(step, args.steps, args.warmup, world, 3)
+            enc, dec = seg_ms(evs, 0, 1), seg_ms(evs, 1, 2)
+            enc_bytes = (6 if codec == "cnat" else 10) * n
+            res[f"{wname}_{codec}"] = {
+                "encode_ms": round(enc, 4), "decode_ms": round(dec, 4),
+                "encode_GBs": round(enc_bytes / enc / 1e6, 1), "decode_GBs": round(6 * n / dec / 1e6, 1),
+                "encode_frac": round(enc_bytes / enc / 1e6 / HBM_PEAK_GBS, 3),
+                "decode_frac": round(6 * n / dec / 1e6 / HBM_PEAK_GBS, 3),
+                "round_trip_GiBs": round(4 * n / GIB / ((enc + dec) / 1e3), 1),
+                "wall_ms_per_step": round(wall / args.steps * 1e3, 4)}
+    if rank == 0:
+        m = 1 << 22
+        xs = torch.randn(m) * 1e-3
+        torch.set_num_threads(os.cpu_count() if os.cpu_count() <= 16 else 16)
+        for codec in ("qsgd", "rqsgd", "cnat"):
+            best = min((_ref_stoch_cpu(codec, xs) for _ in range(3)), key=lambda t: t[0] + t[1])
+            res[f"cpu_reference_{codec}"] = {"sample_elems": m, "threads": torch.get_num_threads(),
+                                             "encode_ms": round(best[0] * 1e3, 2), "decode_ms": round(best[1] * 1e3, 2),
+                                             "round_trip_GiBs": round(4 * m / GIB / (best[0] + best[1]), 3)}
+    return {"mode": "stoch", "n_gpus": world, "steps": args.steps, **res}
+
+
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--mode", choices=["c3", "c5_int4", "exchange", "pcie", "channel"], required=True)
+    p.add_argument("--mode", choices=["c3", "c5_int4", "exchange", "pcie", "channel", "stoch"], required=True)
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
@@ -267,7 +364,7 @@ def main():
     world, rank, local = dist_setup(args)
     dev = torch.device("cuda", local)
     line = {"c3": mode_c3, "c5_int4": mode_c5_int4, "exchange": mode_exchange, "pcie": mode_pcie,
-            "channel": mode_channel}[args.mode](
+            "channel": mode_channel, "stoch": mode_stoch}[args.mode](
         args, world, rank, dev)
     if rank == 0:
         print(json.dumps(line), flush=True)
