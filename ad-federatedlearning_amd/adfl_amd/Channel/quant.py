@@ -199,6 +199,22 @@ def _decode_dict(items: List[Tuple[str, torch.Tensor]]) -> Dict[str, torch.Tenso
 
 
 @_serialized
+def _decode_add(c_params: QuantParameters, names: List[str], targets: List[Parameters]) -> None:
+    """Stage the qint8 payloads of `names` into an aligned bucket and accumulate them into every target."""
+    st = _staging()
+    dev = st.device
+    qs = [c_params.params[n].data for n in names]
+    for n, q in zip(names, qs):
+        if q.qscheme() != torch.per_tensor_affine or q.dtype != torch.qint8 or q.q_zero_point() != 0:
+            raise ValueError(f"SLQChannel: '{n}' is not a per-tensor qint8 payload with zero point 0")
+    lay = st.layout(tuple(int(q.numel()) for q in qs), align=ops.ALIGN_ELEMS)
+    q_dev = _stage_in([_int8_view(q) for q in qs], lay, st, "aq", torch.int8)
+    s_dev = torch.tensor([q.q_scale() for q in qs], dtype=torch.float32).to(dev, non_blocking=True)
+    with torch.no_grad():
+        ops.dequantize_add_batched(q_dev, s_dev, lay, [[t[n] for n in names] for t in targets])
+
+
+@_serialized
 def _encode_dict_packed(params: Parameters, names: List[str], bits: int):
     """Packed int4 variant of _encode_dict: {name: (int8 tensor of ceil(n/2) packed bytes, scale)}."""
     st = _staging()
@@ -302,6 +318,35 @@ class SLQChannel(Channel):
             else:
                 params[name] = p.data.data  # passthrough (quant.py:111-112)
         return params, time.perf_counter() - s_time
+
+    def receive_add_(self, c_params: CompressedParameters, targets: List[Parameters]) -> float:
+        """``on_client_receive(c_params)`` followed by ``add_parameters_inpace(t, decoded, 1, 1, False)`` for
+        every ``t`` in ``targets`` — the client pool's ``add_to_model`` / ``add_to_model_all``
+        (Src/ADFL/Client/pool.py:62-75) and QAFeL's hidden-state update (Src/ADFL/Server/qafel.py:176-179),
+        bit-identical to them. Returns the seconds spent.
+
+        Quantized tensors whose targets all live on the GPU are decoded once and accumulated into every
+        model by one launch (ops.dequantize_add_batched: the payload is read once, each model read and
+        written once, no decoded tensor is materialised). Everything else takes the reference's route:
+        decode, then ``mul_(1).add_(decoded, alpha=1)``."""
+        assert isinstance(c_params, QuantParameters)
+        for t in targets:
+            assert set(t.keys()) == set(c_params.params.keys())  # add_parameters_inpace, model.py:340
+        s_time = time.perf_counter()
+        fused = [n for n, p in c_params.params.items()
+                 if p.data.ndim > 1 and p.data.is_quantized and p.data.numel() > 0
+                 and all(t[n].is_cuda and t[n].dtype == torch.float32 and t[n].is_contiguous()
+                         and t[n].data_ptr() % 16 == 0 for t in targets)]
+        if fused:
+            _decode_add(c_params, fused, targets)
+        rest = QuantParameters({n: p for n, p in c_params.params.items() if n not in fused}, 0)
+        if rest.params:
+            decoded, _ = self.on_client_receive(rest)
+            with torch.no_grad():
+                for t in targets:
+                    for n, d in decoded.items():
+                        t[n].mul_(1).add_(d.to(t[n].device), alpha=1)
+        return time.perf_counter() - s_time
 
     def send_with_q_error(self, params: Parameters) -> Tuple[CompressedParameters, float, float, float]:
         """`on_client_send` fused with the worker's quantization-error metrics.

@@ -231,6 +231,34 @@ def qerror_batched(flat: torch.Tensor, q: torch.Tensor, scales: torch.Tensor,
     return tuple(partials.view(-1, 4).sum(0).tolist())
 
 
+def dequantize_add_batched(q: torch.Tensor, scales: torch.Tensor, layout: BucketLayout, targets) -> None:
+    """In place, for every model k and tensor t: targets[k][t] += fp32(scales[t] * q_t) (fp32 add) — decode
+    once, accumulate into K device-resident models (Src/ADFL/Client/pool.py:62-75, model.py:337-347).
+
+    targets: K sequences of T contiguous, 16-byte aligned fp32 device tensors, tensor t with
+    layout.sizes[t] elements. The layout's offsets must be multiples of 4 (an aligned bucket)."""
+    if (layout.offsets % 4).any():
+        raise ValueError("dequantize_add_batched: tensor offsets must be multiples of 4 (use an aligned layout)")
+    q = _dev(q, "q")
+    dev = q.device
+    ptrs = []
+    for k, model in enumerate(targets):
+        if len(model) != layout.ntensors:
+            raise ValueError(f"dequantize_add_batched: model {k} has {len(model)} tensors, layout {layout.ntensors}")
+        for t, (x, n) in enumerate(zip(model, layout.sizes.tolist())):
+            if (not x.is_cuda or x.device != dev or x.dtype != torch.float32 or not x.is_contiguous()
+                    or x.numel() != n or x.data_ptr() % 16):
+                raise ValueError(f"dequantize_add_batched: target {k}/{t} must be a contiguous, 16-byte aligned "
+                                 f"fp32 tensor of {n} elements on {dev}")
+            ptrs.append(x.data_ptr())
+    table = torch.tensor(ptrs, dtype=torch.int64).to(dev, non_blocking=True)
+    check(_lib.load().adfl_slq_dequantize_add_batched(q.data_ptr(), layout.device_chunks(dev).data_ptr(),
+                                                      layout.nchunks, _dev(scales, "scales").data_ptr(),
+                                                      table.data_ptr(), layout.ntensors, len(targets),
+                                                      _stream(dev)))
+    # `table` may be freed on return: the caching allocator only reuses it for later work on this stream
+
+
 def _require_even_offsets(layout: BucketLayout) -> None:
     if layout.align % 2 or (layout.offsets % 2).any():
         raise ValueError("int4 buckets need even tensor offsets (BucketLayout(align=2) or a multiple of 2)")

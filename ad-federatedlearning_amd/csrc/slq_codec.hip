@@ -560,6 +560,43 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_batched(const int8_t* __r
   for (int i = head + ntiles * kTile + threadIdx.x; i < c.len; i += kBlock) oc[i] = s * (float)qc[i];
 }
 
+// Decode + accumulate into K models (pool.py:62-75, qafel.py:176-179 via model.py:337-347): the chunk's
+// payload is decoded once into registers (8 float4 per thread), then every model's slice is read, added
+// (fp32(a + d), what mul_(1).add_(d, alpha=1) computes) and written back with 16-byte accesses. Tensor
+// offsets in the bucket are multiples of 4, so the payload dwords and the targets' float4s line up.
+__global__ __launch_bounds__(kBlock) void k_dequantize_add_batched(const int8_t* __restrict__ q,
+                                                                   const adfl_slq_chunk* __restrict__ chunks,
+                                                                   const float* __restrict__ scales,
+                                                                   float* const* __restrict__ targets,
+                                                                   int ntensors, int ntargets) {
+  constexpr int kPer = ADFL_SLQ_CHUNK_ELEMS / 4 / kBlock;
+  const adfl_slq_chunk c = chunks[blockIdx.x];
+  const float s = scales[c.tensor];
+  const int64_t in_tensor = (int64_t)(blockIdx.x - c.first_chunk) * ADFL_SLQ_CHUNK_ELEMS;
+  const int8_t* qc = q + c.start;
+  const uint32_t* q4 = reinterpret_cast<const uint32_t*>(qc);
+  const int n4 = c.len >> 2;
+  float4 dv[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int k = threadIdx.x + j * kBlock;
+    dv[j] = k < n4 ? dequant4(q4[k], s) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const int tail = n4 << 2;
+  const bool has_tail = (int)threadIdx.x < c.len - tail;
+  const float dt = has_tail ? s * (float)qc[tail + threadIdx.x] : 0.0f;
+  for (int m = 0; m < ntargets; ++m) {
+    float* tg = targets[(int64_t)m * ntensors + c.tensor] + in_tensor;
+    float4* t4 = reinterpret_cast<float4*>(tg);
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int k = threadIdx.x + j * kBlock;
+      if (k < n4) t4[k] = add4(t4[k], dv[j]);
+    }
+    if (has_tail) tg[tail + threadIdx.x] = tg[tail + threadIdx.x] + dt;
+  }
+}
+
 // Quantization-error statistics of a bucket against its own payload (worker.py:186-189 computes
 // parameter_relative_mse and parameter_cosine_similarity from a full decode; here they are four sums
 // per chunk, fp64): S0 = sum (x - s*q)^2, S1 = sum x^2, S2 = sum x*(s*q), S3 = sum (s*q)^2.
@@ -861,6 +898,18 @@ int adfl_slq_dequantize_mean(const int8_t* d_q, int64_t row_stride_bytes, int32_
   if (!aligned16(d_q) || !aligned16(d_out) || (row_stride_bytes & 15) != 0) return ADFL_E_ALIGN;
   hipLaunchKernelGGL(k_dequantize_mean, dim3(tile_grid(n / kTile)), dim3(kBlock), 0, (hipStream_t)stream, d_q,
                      row_stride_bytes, (int)k, n, d_scales, scale_stride, d_out);
+  return launch_status();
+}
+
+int adfl_slq_dequantize_add_batched(const int8_t* d_q, const adfl_slq_chunk* d_chunks, int64_t nchunks,
+                                    const float* d_scales, float* const* d_targets, int32_t ntensors,
+                                    int32_t ntargets, void* stream) {
+  if (!d_q || !d_chunks || !d_scales || !d_targets || nchunks < 1 || nchunks > INT32_MAX || ntensors < 1 ||
+      ntargets < 1)
+    return ADFL_E_ARG;
+  if (!aligned16(d_q)) return ADFL_E_ALIGN;
+  hipLaunchKernelGGL(k_dequantize_add_batched, dim3((unsigned)nchunks), dim3(kBlock), 0, (hipStream_t)stream, d_q,
+                     d_chunks, d_scales, d_targets, (int)ntensors, (int)ntargets);
   return launch_status();
 }
 

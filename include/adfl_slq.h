@@ -136,6 +136,20 @@ int adfl_slq_dequantize_mean(const int8_t* d_q, int64_t row_stride_bytes, int32_
 int adfl_slq_dequantize_mean_int4(const uint8_t* d_packed, int64_t row_stride_bytes, int32_t k, int64_t n,
                                   const float* d_scales, int64_t scale_stride, float* d_out, void* stream);
 
+/* Fused decode + in-place accumulate into K models: for every model k and tensor t,
+ *   model_k[t][i] = fp32(model_k[t][i] + fp32(scale_t * q[i]))
+ * which is the receiver's on_client_receive followed by add_parameters_inpace(model, decoded, 1, 1)
+ * (Src/ADFL/model.py:337-347) for each model: the client pool's add_to_model / add_to_model_all
+ * (Src/ADFL/Client/pool.py:62-75) and QAFeL's hidden-state update (Src/ADFL/Server/qafel.py:176-179).
+ * The payload is read once for all K models; each model is read and written once.
+ *   d_q, d_chunks  a bucketed payload whose tensor offsets are multiples of 4 elements (e.g. an
+ *                  ADFL_SLQ_ALIGN_ELEMS-aligned bucket); d_scales one fp32 per tensor
+ *   d_targets      DEVICE array of ntargets * ntensors device pointers, d_targets[k * ntensors + t] = the
+ *                  fp32 storage of tensor t of model k (contiguous, 16-byte aligned, sizes as the table) */
+int adfl_slq_dequantize_add_batched(const int8_t* d_q, const adfl_slq_chunk* d_chunks, int64_t nchunks,
+                                    const float* d_scales, float* const* d_targets, int32_t ntensors,
+                                    int32_t ntargets, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

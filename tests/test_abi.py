@@ -98,6 +98,10 @@ def test_stochastic_argument_errors_return_codes_without_launching():
     assert lib.adfl_rqsgd_dequantize_batched(16, 16, 16, 1, 8, 16, None, 16, None) == -1
     assert lib.adfl_cnat_dequantize_batched(16, 16, 16, 1, None, 16, None) == -1
     assert lib.adfl_philox_uniforms(16, 0, 0, 1, 0, None) == -1
+    # fused decode + accumulate
+    assert lib.adfl_slq_dequantize_add_batched(16, 16, 1, 16, 16, 1, 0, None) == -1
+    assert lib.adfl_slq_dequantize_add_batched(16, 16, 1, 16, None, 1, 1, None) == -1
+    assert lib.adfl_slq_dequantize_add_batched(20, 16, 1, 16, 16, 1, 1, None) == -3
 
 
 def test_build_chunks_host_planning():
