@@ -32,7 +32,6 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
-constexpr int kFinalizeGrid = 1024;
 constexpr int64_t kPartialBytes = 16;  // per chunk: fp64 sum of squares, or {max, min} |x| bits
 
 // ------------------------------------------------------------------------------------------------
@@ -91,26 +90,70 @@ __device__ __forceinline__ uint32_t pack4(uint32_t a, uint32_t b, uint32_t c, ui
   return a | (b << 8) | (c << 16) | (d << 24);
 }
 
-// QSGD / RQSGD level (quant.py:230-236): s * |x| / norm in fp32, floor, stochastic round up.
-__device__ __forceinline__ uint32_t qsgd_level(float x, float s, float norm, float u) {
+// Every element rule below comes in two forms:
+//  * an EXACT form — the reference's fp32 arithmetic, including every special case (NaN, inf, overflow,
+//    caller-supplied tiny norms), with correctly rounded __fdiv_rn divisions;
+//  * a FAST form — branch-free, the same result wherever it sets no `bad` flag. The kernels evaluate the
+//    fast form for a float4 group, and if any lane of the wave flagged its group (a wave-uniform ballot)
+//    that wave recomputes the flagged lanes with the exact form. Per-element exec-mask branching on rare
+//    cases made the kernels issue-bound (267 saveexec / 196 branches for 32 elements per lane).
+//
+// Division. The fast form uses a per-tensor reciprocal (Markstein): y = RN(1/b), q = RN(a*y),
+// r = RN(a - b*q) (exact), q' = RN(q + r*y) = RN(a/b) while every intermediate stays normal; it is valid
+// for b in [2^-60, 2^60] (block-uniform) and |a| in {0} U [2^-60, 2^60]. 4.4 vs 12.1 lane-cycles per
+// quotient, and 0 of 1.7e10 random operand pairs differ from __fdiv_rn (tools/microbench_stoch.hip,
+// profiles/r01/microbench_stoch.txt).
+struct Div {
+  float b, y;
+  bool fast;
+};
+
+__device__ __forceinline__ Div make_div(float b) {
+  Div d;
+  d.b = b;
+  d.y = __fdiv_rn(1.0f, b);
+  d.fast = b >= 0x1p-60f && b <= 0x1p60f;
+  return d;
+}
+
+__device__ __forceinline__ float div_fast(float a, const Div& d, bool& bad) {
+  const float aa = __builtin_fabsf(a);
+  bad |= !(aa <= 0x1p60f && (aa >= 0x1p-60f || aa == 0.0f));
+  const float q = a * d.y;
+  const float r = __builtin_fmaf(-d.b, q, a);
+  return __builtin_fmaf(r, d.y, q);  // +0 for a = +0 (a is never -0 on these paths)
+}
+
+// QSGD / RQSGD level (quant.py:230-236): s * |x| / norm in fp32, floor, stochastic round up, u8.
+__device__ __forceinline__ uint32_t qsgd_level_exact(float x, float s, float norm, float u) {
   const float scaled = __fdiv_rn(s * __builtin_fabsf(x), norm);
   const float l = __builtin_floorf(scaled);
-  const float prob = scaled - l;
-  return low_byte(l + (u < prob ? 1.0f : 0.0f));
+  return low_byte(l + (u < scaled - l ? 1.0f : 0.0f));
+}
+
+// Fast form: for 0 <= scaled < 2^24 (every level of bits <= 16 against its own norm) the floor is an
+// integer truncation and l + 1 is exact in fp32.
+__device__ __forceinline__ uint32_t qsgd_level_fast(float x, float s, const Div& d, float u, bool& bad) {
+  const float scaled = div_fast(s * __builtin_fabsf(x), d, bad);
+  bad |= !(scaled < 16777216.0f);                          // also catches NaN
+  const float sc = __builtin_fminf(scaled, 16777215.0f);   // keep the conversion defined when flagged
+  const int l = (int)sc;
+  return (uint32_t)(l + (u < sc - (float)l ? 1 : 0)) & 0xffu;
 }
 
 __device__ __forceinline__ float pow2i(int k) {  // 2^k for k in [-126, 128] (128 -> inf), exact
   return __uint_as_float((uint32_t)(k + 127) << 23);
 }
 
-// CNAT exponent (quant.py:516-532). v = fl(|x| + eps) >= 2^-23 is normal, so its binary exponent e and the
-// band table give floor / ceil of fl32(log2 v) exactly.
-__device__ __forceinline__ uint32_t cnat_exp(float x, float u, float min_e, float max_e) {
-  if (x == 0.0f) return low_byte(min_e);  // final_exponents[x == 0] = min_exp
+// CNAT exponent byte (quant.py:516-532). v = fl(|x| + eps) >= 2^-23 is normal, so its binary exponent e and
+// the band table give floor / ceil of fl32(log2 v) exactly. Integer clamp and low byte = torch's float
+// clamp_ then .to(int8) of an integral value.
+__device__ __forceinline__ uint32_t cnat_exp_exact(float x, float u, int min_e, int max_e) {
+  if (x == 0.0f) return (uint32_t)min_e & 0xffu;  // final_exponents[x == 0] = min_exp
   const float xa = __builtin_fabsf(x);
   const float v = xa + 0x1p-23f;
-  if (__builtin_isnan(v)) return 0u;                 // log2 NaN -> ceil NaN -> clamp keeps NaN -> int8 0
-  if (__builtin_isinf(v)) return low_byte(max_e);    // prob = NaN -> ceil = inf -> clamped to max_exp
+  if (__builtin_isnan(v)) return 0u;                        // ceil NaN, clamp keeps NaN, int8(NaN) = 0
+  if (__builtin_isinf(v)) return (uint32_t)max_e & 0xffu;   // prob = NaN -> ceil = inf -> max_exp
   const uint32_t bits = __float_as_uint(v);
   const int e = (int)(bits >> 23) - 127;
   const uint32_t m = bits & 0x7fffffu;
@@ -120,20 +163,50 @@ __device__ __forceinline__ uint32_t cnat_exp(float x, float u, float min_e, floa
   } else if (0x800000u - m <= kCnatBand[e + 1 - kCnatKMin].below) {
     f = e + 1;
   }
-  const float prob = __fdiv_rn(pow2i(c) - xa, pow2i(f));
-  float ef = (u < prob) ? (float)f : (float)c;
-  ef = __builtin_fminf(__builtin_fmaxf(ef, min_e), max_e);
-  return low_byte(ef);
+  // (2^c - |x|) / 2^f: dividing by a power of two is exact here (the quotient is 0, normal or inf), so an
+  // ldexp replaces the division; 2^128 = inf as a divisor (f = 128) makes the quotient NaN, as in torch.
+  const float a = pow2i(c) - xa;
+  const float prob = f < 128 ? __builtin_ldexpf(a, -f) : __builtin_nanf("");
+  const int r = (u < prob) ? f : c;
+  return (uint32_t)min(max(r, min_e), max_e) & 0xffu;
 }
 
-// decoders
-__device__ __forceinline__ float qsgd_value(uint32_t l, uint32_t sgn, float norm, float s) {
+// Fast form: finite non-zero x whose mantissa is outside every power of two's band (no band is wider
+// than kCnatMaxAbove / kCnatMaxBelow ulps): floor / ceil are e / e + 1. Zeros are handled inline.
+__device__ __forceinline__ uint32_t cnat_exp_fast(float x, float u, int min_e, int max_e, bool& bad) {
+  const float xa = __builtin_fabsf(x);
+  const float v = xa + 0x1p-23f;
+  const uint32_t bits = __float_as_uint(v);
+  const int e = (int)(bits >> 23) - 127;
+  const uint32_t m = bits & 0x7fffffu;
+  bad |= (x != 0.0f) & (!(v < 0x1p127f) | (m <= kCnatMaxAbove) | (0x800000u - m <= kCnatMaxBelow));
+  const float prob = __builtin_ldexpf(pow2i(e + 1) - xa, -e);
+  int r = (u < prob) ? e : e + 1;
+  r = min(max(r, min_e), max_e);
+  return (uint32_t)(x == 0.0f ? min_e : r) & 0xffu;
+}
+
+// decoders (d divides by levels)
+__device__ __forceinline__ float qsgd_value_exact(uint32_t l, uint32_t sgn, float norm, float s) {
   return __fdiv_rn(norm * (float)l, s) * (float)(int8_t)sgn;
 }
 
-__device__ __forceinline__ float rqsgd_value(uint32_t l, uint32_t sgn, float norm, float mn, float s) {
+__device__ __forceinline__ float qsgd_value_fast(uint32_t l, uint32_t sgn, float norm, const Div& d, bool& bad) {
+  return div_fast(norm * (float)l, d, bad) * (float)(int8_t)sgn;
+}
+
+__device__ __forceinline__ float rqsgd_value_exact(uint32_t l, uint32_t sgn, float norm, float mn, float s) {
   const float sf = (float)(int8_t)sgn;
   return l == 0u ? mn * sf : __fdiv_rn((norm * sf) * (float)l, s);
+}
+
+__device__ __forceinline__ float rqsgd_value_fast(uint32_t l, uint32_t sgn, float norm, float mn, const Div& d,
+                                                  bool& bad) {
+  const float sf = (float)(int8_t)sgn;
+  bool b2 = false;
+  const float v = div_fast((norm * sf) * (float)l, d, b2);
+  bad |= b2 & (l != 0u);
+  return l == 0u ? mn * sf : v;
 }
 
 __device__ __forceinline__ float cnat_value(uint32_t e, uint32_t sgn, float norm) {
@@ -179,6 +252,13 @@ __device__ __forceinline__ uint32_t abs_bits(float v) { return __float_as_uint(v
 
 __device__ __forceinline__ double sq(float v) { return (double)(v * v); }  // fp32 square, as torch
 
+// streaming (non-temporal) 16-byte load: x is read once per pass and must not evict the payload planes
+__device__ __forceinline__ float4 load4_nt(const float4* p) {
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+
 // elements [0, head) of a chunk are done one by one, up to the first 4-element boundary of the bucket
 __device__ __forceinline__ int chunk_head4(int64_t start, int len) {
   const int h = (int)((4 - (start & 3)) & 3);
@@ -188,77 +268,200 @@ __device__ __forceinline__ int chunk_head4(int64_t start, int len) {
 // ------------------------------------------------------------------------------------------------
 // kernels
 // ------------------------------------------------------------------------------------------------
-// Norm partials, one block per chunk: fp64 sum of fp32 squares (L2) or {max, min} of |x| bits (LINF).
+// Work layout: one block per chunk (<= 8192 elements; a 1 GiB tensor is 32768 blocks). Inside a chunk
+// every thread first issues all its loads (at most kPer = 8192 / 4 / 256 = 8 float4 or plane dwords),
+// then computes. Measured alternatives (profiles/r01/stoch_*): a loop that consumes each load before
+// issuing the next is latency-bound; blocks that walk a range of chunks serialise them and were slower
+// still (fresh blocks overlap one another's loads and compute).
+constexpr int kPer = ADFL_SLQ_CHUNK_ELEMS / 4 / kBlock;
+constexpr int64_t kKeepBytes = 192ll << 20;  // x tail the norm pass leaves in the Infinity Cache
+constexpr int64_t kKeepChunks = kKeepBytes / (4 * ADFL_SLQ_CHUNK_ELEMS);
+
+// Per-element head / tail of a chunk: the < 4 elements before the first 4-element boundary and after the
+// last; thread t < head takes head element t, the next threads the tail elements. Returns -1 if none.
+__device__ __forceinline__ int edge_elem(int head, int tail, int len) {
+  const int t = threadIdx.x;
+  if (t < head) return t;
+  return (t - head < len - tail) ? tail + t - head : -1;
+}
+
+template <int MODE>
+struct NormAcc {
+  double s = 0.0;
+  uint32_t mx = 0u, mn = 0xffffffffu;
+  __device__ __forceinline__ void add(float v) {
+    if (MODE == ADFL_NORM_L2) {
+      s += sq(v);
+    } else {
+      mx = max(mx, abs_bits(v));
+      mn = min(mn, abs_bits(v));
+    }
+  }
+  __device__ __forceinline__ void add4(float4 v) {
+    if (MODE == ADFL_NORM_L2) {
+      s += (sq(v.x) + sq(v.y)) + (sq(v.z) + sq(v.w));
+    } else {
+      const uint32_t a = abs_bits(v.x), b = abs_bits(v.y), d = abs_bits(v.z), e = abs_bits(v.w);
+      mx = max(mx, max(max(a, b), max(d, e)));
+      mn = min(mn, min(min(a, b), min(d, e)));
+    }
+  }
+  // block-reduce and write slot `ci` (every thread calls it: it synchronises)
+  __device__ __forceinline__ void flush(void* partials, int64_t ci) {
+    if (MODE == ADFL_NORM_L2) {
+      const double r = block_sum(s);
+      if (threadIdx.x == 0) reinterpret_cast<double*>(partials)[ci] = r;
+    } else {
+      const uint2 r = block_maxmin(mx, mn);
+      if (threadIdx.x == 0) reinterpret_cast<uint2*>(partials)[ci] = r;
+    }
+    *this = NormAcc();
+  }
+};
+
+// Norm partials, one block per chunk: the chunk's fp64 sum of fp32 squares (L2) or {max, min} |x| bits
+// (LINF) into its slot. Fixed assignment and order: deterministic.
+// Chunks from `keep_from` on are read with allocating loads, the rest non-temporally: the bucket's last
+// kKeepBytes stay in the 256 MiB Infinity Cache for the quantize pass, which walks the chunks in reverse.
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_norm_partials(const float* __restrict__ x,
                                                           const adfl_slq_chunk* __restrict__ chunks,
-                                                          void* __restrict__ partials) {
+                                                          int64_t keep_from, void* __restrict__ partials) {
   const adfl_slq_chunk c = chunks[blockIdx.x];
   const float* xc = x + c.start;
   const int head = chunk_head4(c.start, c.len);
   const float4* x4 = reinterpret_cast<const float4*>(xc + head);
   const int n4 = (c.len - head) >> 2;
-  const int tail = head + (n4 << 2);
+  const bool keep = (int64_t)blockIdx.x >= keep_from;
+  float4 v[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int k = threadIdx.x + j * kBlock;
+    if (k < n4) v[j] = keep ? x4[k] : load4_nt(x4 + k);
+  }
+  NormAcc<MODE> acc;
+  const int i = edge_elem(head, head + (n4 << 2), c.len);
+  if (i >= 0) acc.add(xc[i]);
+#pragma unroll
+  for (int j = 0; j < kPer; ++j)
+    if ((int)threadIdx.x + j * kBlock < n4) acc.add4(v[j]);
+  acc.flush(partials, blockIdx.x);
+}
+
+// Per-tensor finalize, two launches over the same table (every table entry is read by one thread, in
+// parallel). Small tensors (<= kSmallChunks chunks): the thread that meets the first chunk sums the slots
+// itself. Large tensors: a 1024-thread block sums them with 16 independent accumulators per thread,
+// combined in a fixed tree. Both write norm = fp32 sqrt of the sum rounded once to fp32 (L2), or the
+// max / min |x| with NaN propagated (LINF).
+constexpr int kSmallChunks = 16;
+constexpr int kBigBlock = 1024;
+
+template <int MODE>
+__device__ __forceinline__ void write_norm(const adfl_slq_chunk& c, double s, uint32_t mx, uint32_t mn,
+                                           float* __restrict__ norms, float* __restrict__ mins) {
   if (MODE == ADFL_NORM_L2) {
-    double s = 0.0;
-    if ((int)threadIdx.x < head) s = sq(xc[threadIdx.x]);
-    for (int i = threadIdx.x; i < n4; i += kBlock) {
-      const float4 v = x4[i];
-      s += (sq(v.x) + sq(v.y)) + (sq(v.z) + sq(v.w));
-    }
-    if ((int)threadIdx.x < c.len - tail) s += sq(xc[tail + threadIdx.x]);
-    s = block_sum(s);
-    if (threadIdx.x == 0) reinterpret_cast<double*>(partials)[blockIdx.x] = s;
+    norms[c.tensor] = (float)__builtin_sqrt((double)(float)s);
   } else {
-    uint32_t mx = 0u, mn = 0xffffffffu;
-    if ((int)threadIdx.x < head) mx = mn = abs_bits(xc[threadIdx.x]);
-    for (int i = threadIdx.x; i < n4; i += kBlock) {
-      const float4 v = x4[i];
-      const uint32_t a = abs_bits(v.x), b = abs_bits(v.y), d = abs_bits(v.z), e = abs_bits(v.w);
-      mx = max(mx, max(max(a, b), max(d, e)));
-      mn = min(mn, min(min(a, b), min(d, e)));
-    }
-    if ((int)threadIdx.x < c.len - tail) {
-      const uint32_t a = abs_bits(xc[tail + threadIdx.x]);
-      mx = max(mx, a);
-      mn = min(mn, a);
-    }
-    const uint2 r = block_maxmin(mx, mn);
-    if (threadIdx.x == 0) reinterpret_cast<uint2*>(partials)[blockIdx.x] = r;
+    const bool nan = mx > 0x7f800000u;  // NaN anywhere: torch's max and min both propagate it
+    norms[c.tensor] = nan ? __builtin_nanf("") : __uint_as_float(mx);
+    if (mins) mins[c.tensor] = nan ? __builtin_nanf("") : __uint_as_float(mn);
   }
 }
 
-// Per-tensor finalize: the block that meets a tensor's first chunk reduces its partials in a fixed
-// order and writes the norm (and min).
 template <int MODE>
-__global__ __launch_bounds__(kBlock) void k_norm_finalize(const adfl_slq_chunk* __restrict__ chunks, int64_t nchunks,
-                                                          const void* __restrict__ partials,
-                                                          float* __restrict__ norms, float* __restrict__ mins) {
-  for (int64_t ci = blockIdx.x; ci < nchunks; ci += gridDim.x) {
-    const adfl_slq_chunk c = chunks[ci];
-    if (c.first_chunk != ci) continue;  // uniform per block
+__global__ __launch_bounds__(kBlock) void k_norm_finalize_small(const adfl_slq_chunk* __restrict__ chunks,
+                                                                int64_t nchunks, const void* __restrict__ partials,
+                                                                float* __restrict__ norms, float* __restrict__ mins) {
+  const int64_t ci = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (ci >= nchunks) return;
+  const adfl_slq_chunk c = chunks[ci];
+  if (c.first_chunk != ci || c.nchunks > kSmallChunks) return;
+  double s = 0.0;
+  uint32_t mx = 0u, mn = 0xffffffffu;
+  for (int k = 0; k < c.nchunks; ++k) {
     if (MODE == ADFL_NORM_L2) {
-      const double* p = reinterpret_cast<const double*>(partials) + ci;
-      double s = 0.0;
-      for (int k = threadIdx.x; k < c.nchunks; k += kBlock) s += p[k];
-      s = block_sum(s);
-      // round the sum once to fp32 (as torch's fp32 sum ends), then the correctly rounded fp32 sqrt
-      if (threadIdx.x == 0) norms[c.tensor] = (float)__builtin_sqrt((double)(float)s);
+      s += reinterpret_cast<const double*>(partials)[ci + k];
     } else {
-      const uint2* p = reinterpret_cast<const uint2*>(partials) + ci;
-      uint32_t mx = 0u, mn = 0xffffffffu;
-      for (int k = threadIdx.x; k < c.nchunks; k += kBlock) {
-        const uint2 v = p[k];
-        mx = max(mx, v.x);
-        mn = min(mn, v.y);
-      }
-      const uint2 r = block_maxmin(mx, mn);
-      if (threadIdx.x == 0) {
-        const bool nan = r.x > 0x7f800000u;  // NaN anywhere: torch's max and min both propagate it
-        norms[c.tensor] = nan ? __builtin_nanf("") : __uint_as_float(r.x);
-        if (mins) mins[c.tensor] = nan ? __builtin_nanf("") : __uint_as_float(r.y);
+      const uint2 v = reinterpret_cast<const uint2*>(partials)[ci + k];
+      mx = max(mx, v.x);
+      mn = min(mn, v.y);
+    }
+  }
+  write_norm<MODE>(c, s, mx, mn, norms, mins);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kBigBlock) void k_norm_finalize_big(const adfl_slq_chunk* __restrict__ chunks,
+                                                                 int64_t nchunks, const void* __restrict__ partials,
+                                                                 float* __restrict__ norms, float* __restrict__ mins) {
+  constexpr int U = 16, W = kBigBlock / 64;
+  __shared__ int64_t firsts[kBigBlock];
+  __shared__ int nfirst;
+  __shared__ double red_s[W];
+  __shared__ uint32_t red_mx[W], red_mn[W];
+  if (threadIdx.x == 0) nfirst = 0;
+  __syncthreads();
+  const int64_t me = (int64_t)blockIdx.x * kBigBlock + threadIdx.x;
+  if (me < nchunks) {
+    const adfl_slq_chunk c = chunks[me];
+    if (c.first_chunk == me && c.nchunks > kSmallChunks) firsts[atomicAdd(&nfirst, 1)] = me;
+  }
+  __syncthreads();
+  for (int f = 0; f < nfirst; ++f) {  // block-uniform loop; tensors are independent, so order is free
+    const int64_t ci = firsts[f];
+    const adfl_slq_chunk c = chunks[ci];
+    double a[U];
+    uint32_t mx = 0u, mn = 0xffffffffu;
+#pragma unroll
+    for (int u = 0; u < U; ++u) a[u] = 0.0;
+    for (int k0 = threadIdx.x; k0 < c.nchunks; k0 += U * kBigBlock) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = k0 + u * kBigBlock;
+        if (k < c.nchunks) {
+          if (MODE == ADFL_NORM_L2) {
+            a[u] += reinterpret_cast<const double*>(partials)[ci + k];
+          } else {
+            const uint2 v = reinterpret_cast<const uint2*>(partials)[ci + k];
+            mx = max(mx, v.x);
+            mn = min(mn, v.y);
+          }
+        }
       }
     }
+    double s = 0.0;
+    if (MODE == ADFL_NORM_L2) {
+#pragma unroll
+      for (int w = U / 2; w > 0; w >>= 1)
+#pragma unroll
+        for (int u = 0; u < w; ++u) a[u] += a[u + w];
+      s = a[0];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    } else {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+        mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
+      }
+    }
+    if ((threadIdx.x & 63) == 0) {
+      red_s[threadIdx.x >> 6] = s;
+      red_mx[threadIdx.x >> 6] = mx;
+      red_mn[threadIdx.x >> 6] = mn;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double t = 0.0;
+      uint32_t tx = 0u, tn = 0xffffffffu;
+      for (int w = 0; w < W; ++w) {
+        t += red_s[w];
+        tx = max(tx, red_mx[w]);
+        tn = min(tn, red_mn[w]);
+      }
+      write_norm<MODE>(c, t, tx, tn, norms, mins);
+    }
+    __syncthreads();
   }
 }
 
@@ -269,11 +472,53 @@ __device__ __forceinline__ void fill_zero_norm(uint8_t* __restrict__ lv, int8_t*
   }
 }
 
+__device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0ull; }
+
+// The vector part of a quantize chunk: x (and injected uniforms) loaded up front, then per float4 group
+// the level / exponent bytes (fast form; exact form for the wave if any lane flagged its group) and the
+// sign bytes, stored as one dword each (contiguous across the wave). `all_exact` is block-uniform.
+template <class F, class E, class A>
+__device__ __forceinline__ void quantize_chunk_vec(const float4* __restrict__ x4, int n4, int64_t g0, const Uniforms& U,
+                                                   uint32_t* __restrict__ l4, uint32_t* __restrict__ s4, F fast,
+                                                   E exact, bool all_exact, A* acc) {
+  float4 v[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int k = threadIdx.x + j * kBlock;
+    if (k < n4) v[j] = load4_nt(x4 + k);
+  }
+  float4 u[kPer];
+  if (U.inj) {
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int k = threadIdx.x + j * kBlock;
+      if (k < n4) u[j] = U.group(g0 + 4 * (int64_t)k);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int k = threadIdx.x + j * kBlock;
+    if (j * kBlock >= n4) break;  // block-uniform: no thread has group j
+    const bool live = k < n4;
+    const float4 uj = U.inj ? u[j] : U.group(g0 + 4 * (int64_t)k);
+    bool bad = all_exact;
+    uint32_t w = pack4(fast(v[j].x, uj.x, bad), fast(v[j].y, uj.y, bad), fast(v[j].z, uj.z, bad),
+                       fast(v[j].w, uj.w, bad));
+    if (wave_any(bad && live) && bad)
+      w = pack4(exact(v[j].x, uj.x), exact(v[j].y, uj.y), exact(v[j].z, uj.z), exact(v[j].w, uj.w));
+    if (live) {
+      l4[k] = w;
+      s4[k] = pack4(sign_byte(v[j].x), sign_byte(v[j].y), sign_byte(v[j].z), sign_byte(v[j].w));
+      if (acc) acc->add4(v[j]);
+    }
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_qsgd_quantize(const float* __restrict__ x,
                                                           const adfl_slq_chunk* __restrict__ chunks, float s,
                                                           const float* __restrict__ norms, Uniforms U,
                                                           uint8_t* __restrict__ levels, int8_t* __restrict__ signs) {
-  const adfl_slq_chunk c = chunks[blockIdx.x];
+  const adfl_slq_chunk c = chunks[gridDim.x - 1 - blockIdx.x];  // reverse: start on the cached tail of x
   const float norm = norms[c.tensor];
   uint8_t* lv = levels + c.start;
   int8_t* sg = signs + c.start;
@@ -281,72 +526,47 @@ __global__ __launch_bounds__(kBlock) void k_qsgd_quantize(const float* __restric
     fill_zero_norm(lv, sg, c.len);
     return;
   }
+  const Div d = make_div(norm);
   const float* xc = x + c.start;
   const int head = chunk_head4(c.start, c.len);
-  if ((int)threadIdx.x < head) {
-    const int i = threadIdx.x;
-    lv[i] = (uint8_t)qsgd_level(xc[i], s, norm, U.one(c.start + i));
-    sg[i] = (int8_t)sign_byte(xc[i]);
-  }
   const int n4 = (c.len - head) >> 2;
-  const float4* x4 = reinterpret_cast<const float4*>(xc + head);
-  uint32_t* l4 = reinterpret_cast<uint32_t*>(lv + head);
-  uint32_t* s4 = reinterpret_cast<uint32_t*>(sg + head);
-  for (int k = threadIdx.x; k < n4; k += kBlock) {
-    const float4 v = x4[k];
-    const float4 u = U.group(c.start + head + 4 * (int64_t)k);
-    l4[k] = pack4(qsgd_level(v.x, s, norm, u.x), qsgd_level(v.y, s, norm, u.y), qsgd_level(v.z, s, norm, u.z),
-                  qsgd_level(v.w, s, norm, u.w));
-    s4[k] = pack4(sign_byte(v.x), sign_byte(v.y), sign_byte(v.z), sign_byte(v.w));
-  }
-  const int tail = head + (n4 << 2);
-  if ((int)threadIdx.x < c.len - tail) {
-    const int i = tail + threadIdx.x;
-    lv[i] = (uint8_t)qsgd_level(xc[i], s, norm, U.one(c.start + i));
+  const auto fast = [&](float xv, float uv, bool& bad) { return qsgd_level_fast(xv, s, d, uv, bad); };
+  const auto exact = [&](float xv, float uv) { return qsgd_level_exact(xv, s, norm, uv); };
+  quantize_chunk_vec(reinterpret_cast<const float4*>(xc + head), n4, c.start + head, U,
+                     reinterpret_cast<uint32_t*>(lv + head), reinterpret_cast<uint32_t*>(sg + head), fast, exact,
+                     !d.fast, (NormAcc<ADFL_NORM_L2>*)nullptr);
+  const int i = edge_elem(head, head + (n4 << 2), c.len);
+  if (i >= 0) {
+    lv[i] = (uint8_t)exact(xc[i], U.one(c.start + i));
     sg[i] = (int8_t)sign_byte(xc[i]);
   }
 }
 
-// CNAT: exponents + signs + L2 partials in one read of x.
+// CNAT: exponents + signs + the chunk's L2 partial in one read of x.
 __global__ __launch_bounds__(kBlock) void k_cnat_quantize(const float* __restrict__ x,
-                                                          const adfl_slq_chunk* __restrict__ chunks, float min_e,
-                                                          float max_e, Uniforms U, int8_t* __restrict__ exps,
+                                                          const adfl_slq_chunk* __restrict__ chunks, int min_e,
+                                                          int max_e, Uniforms U, int8_t* __restrict__ exps,
                                                           int8_t* __restrict__ signs, double* __restrict__ partials) {
   const adfl_slq_chunk c = chunks[blockIdx.x];
   const float* xc = x + c.start;
   int8_t* ex = exps + c.start;
   int8_t* sg = signs + c.start;
   const int head = chunk_head4(c.start, c.len);
-  double ss = 0.0;
-  if ((int)threadIdx.x < head) {
-    const int i = threadIdx.x;
-    const float v = xc[i];
-    ex[i] = (int8_t)cnat_exp(v, U.one(c.start + i), min_e, max_e);
-    sg[i] = (int8_t)sign_byte(v);
-    ss = sq(v);
-  }
   const int n4 = (c.len - head) >> 2;
-  const float4* x4 = reinterpret_cast<const float4*>(xc + head);
-  uint32_t* e4 = reinterpret_cast<uint32_t*>(ex + head);
-  uint32_t* s4 = reinterpret_cast<uint32_t*>(sg + head);
-  for (int k = threadIdx.x; k < n4; k += kBlock) {
-    const float4 v = x4[k];
-    const float4 u = U.group(c.start + head + 4 * (int64_t)k);
-    e4[k] = pack4(cnat_exp(v.x, u.x, min_e, max_e), cnat_exp(v.y, u.y, min_e, max_e),
-                  cnat_exp(v.z, u.z, min_e, max_e), cnat_exp(v.w, u.w, min_e, max_e));
-    s4[k] = pack4(sign_byte(v.x), sign_byte(v.y), sign_byte(v.z), sign_byte(v.w));
-    ss += (sq(v.x) + sq(v.y)) + (sq(v.z) + sq(v.w));
-  }
-  const int tail = head + (n4 << 2);
-  if ((int)threadIdx.x < c.len - tail) {
-    const int i = tail + threadIdx.x;
+  const auto fast = [=](float xv, float uv, bool& bad) { return cnat_exp_fast(xv, uv, min_e, max_e, bad); };
+  const auto exact = [=](float xv, float uv) { return cnat_exp_exact(xv, uv, min_e, max_e); };
+  NormAcc<ADFL_NORM_L2> acc;
+  quantize_chunk_vec(reinterpret_cast<const float4*>(xc + head), n4, c.start + head, U,
+                     reinterpret_cast<uint32_t*>(ex + head), reinterpret_cast<uint32_t*>(sg + head), fast, exact,
+                     false, &acc);
+  const int i = edge_elem(head, head + (n4 << 2), c.len);
+  if (i >= 0) {
     const float v = xc[i];
-    ex[i] = (int8_t)cnat_exp(v, U.one(c.start + i), min_e, max_e);
+    ex[i] = (int8_t)exact(v, U.one(c.start + i));
     sg[i] = (int8_t)sign_byte(v);
-    ss += sq(v);
+    acc.add(v);
   }
-  ss = block_sum(ss);
-  if (threadIdx.x == 0) partials[blockIdx.x] = ss;
+  acc.flush(partials, blockIdx.x);
 }
 
 // CNAT norm == 0 (an all-zero tensor): the reference returns u8 zeros and int8 ones (quant.py:513-514).
@@ -366,9 +586,16 @@ __device__ __forceinline__ void store4_nt(float4* p, float4 d) {
 
 // Decoders. KIND 0 = QSGD, 1 = RQSGD, 2 = CNAT.
 template <int KIND>
-__device__ __forceinline__ float decode1(uint32_t l, uint32_t sgn, float norm, float mn, float s) {
-  if (KIND == 0) return qsgd_value(l, sgn, norm, s);
-  if (KIND == 1) return rqsgd_value(l, sgn, norm, mn, s);
+__device__ __forceinline__ float decode_exact(uint32_t l, uint32_t sgn, float norm, float mn, float s) {
+  if (KIND == 0) return qsgd_value_exact(l, sgn, norm, s);
+  if (KIND == 1) return rqsgd_value_exact(l, sgn, norm, mn, s);
+  return cnat_value(l, sgn, norm);
+}
+
+template <int KIND>
+__device__ __forceinline__ float decode_fast(uint32_t l, uint32_t sgn, float norm, float mn, const Div& d, bool& bad) {
+  if (KIND == 0) return qsgd_value_fast(l, sgn, norm, d, bad);
+  if (KIND == 1) return rqsgd_value_fast(l, sgn, norm, mn, d, bad);
   return cnat_value(l, sgn, norm);
 }
 
@@ -387,28 +614,45 @@ __global__ __launch_bounds__(kBlock) void k_stoch_dequantize(const uint8_t* __re
     for (int i = threadIdx.x; i < c.len; i += kBlock) oc[i] = 0.0f;
     return;
   }
+  const Div d = make_div(s);
   const uint8_t* lv = levels + c.start;
   const uint8_t* sg = reinterpret_cast<const uint8_t*>(signs) + c.start;
   const int head = chunk_head4(c.start, c.len);
-  if ((int)threadIdx.x < head) oc[threadIdx.x] = decode1<KIND>(lv[threadIdx.x], sg[threadIdx.x], norm, mn, s);
   const int n4 = (c.len - head) >> 2;
   const uint32_t* l4 = reinterpret_cast<const uint32_t*>(lv + head);
   const uint32_t* s4 = reinterpret_cast<const uint32_t*>(sg + head);
   float4* o4 = reinterpret_cast<float4*>(oc + head);
-  for (int k = threadIdx.x; k < n4; k += kBlock) {
-    const uint32_t l = l4[k], g = s4[k];
+  uint32_t lw[kPer], gw[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int k = threadIdx.x + j * kBlock;
+    if (k < n4) {
+      lw[j] = l4[k];
+      gw[j] = s4[k];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int k = threadIdx.x + j * kBlock;
+    if (j * kBlock >= n4) break;  // block-uniform
+    const bool live = k < n4;
+    const uint32_t l = lw[j], g = gw[j];
+    bool bad = KIND != 2 && !d.fast;
     float4 r;
-    r.x = decode1<KIND>(l & 0xffu, g & 0xffu, norm, mn, s);
-    r.y = decode1<KIND>((l >> 8) & 0xffu, (g >> 8) & 0xffu, norm, mn, s);
-    r.z = decode1<KIND>((l >> 16) & 0xffu, (g >> 16) & 0xffu, norm, mn, s);
-    r.w = decode1<KIND>(l >> 24, g >> 24, norm, mn, s);
-    store4_nt(o4 + k, r);
+    r.x = decode_fast<KIND>(l & 0xffu, g & 0xffu, norm, mn, d, bad);
+    r.y = decode_fast<KIND>((l >> 8) & 0xffu, (g >> 8) & 0xffu, norm, mn, d, bad);
+    r.z = decode_fast<KIND>((l >> 16) & 0xffu, (g >> 16) & 0xffu, norm, mn, d, bad);
+    r.w = decode_fast<KIND>(l >> 24, g >> 24, norm, mn, d, bad);
+    if (KIND != 2 && wave_any(bad && live) && bad) {
+      r.x = decode_exact<KIND>(l & 0xffu, g & 0xffu, norm, mn, s);
+      r.y = decode_exact<KIND>((l >> 8) & 0xffu, (g >> 8) & 0xffu, norm, mn, s);
+      r.z = decode_exact<KIND>((l >> 16) & 0xffu, (g >> 16) & 0xffu, norm, mn, s);
+      r.w = decode_exact<KIND>(l >> 24, g >> 24, norm, mn, s);
+    }
+    if (live) store4_nt(o4 + k, r);
   }
-  const int tail = head + (n4 << 2);
-  if ((int)threadIdx.x < c.len - tail) {
-    const int i = tail + threadIdx.x;
-    oc[i] = decode1<KIND>(lv[i], sg[i], norm, mn, s);
-  }
+  const int i = edge_elem(head, head + (n4 << 2), c.len);
+  if (i >= 0) oc[i] = decode_exact<KIND>(lv[i], sg[i], norm, mn, s);
 }
 
 __global__ __launch_bounds__(kBlock) void k_philox_uniforms(float* __restrict__ out, int64_t n, int64_t start,
@@ -441,7 +685,17 @@ inline int check_ws(const void* d_ws, int64_t bytes, int64_t nchunks) {
   return bytes < nchunks * kPartialBytes ? ADFL_E_WORKSPACE : ADFL_OK;
 }
 
-inline int finalize_grid(int64_t nchunks) { return (int)(nchunks < kFinalizeGrid ? nchunks : kFinalizeGrid); }
+
+template <int MODE>
+inline int launch_finalize(const adfl_slq_chunk* d_chunks, int64_t nchunks, const void* d_ws, float* d_norms,
+                           float* d_mins, hipStream_t st) {
+  hipLaunchKernelGGL(k_norm_finalize_small<MODE>, dim3((unsigned)((nchunks + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                     st, d_chunks, nchunks, d_ws, d_norms, d_mins);
+  if (int s = launch_status()) return s;
+  hipLaunchKernelGGL(k_norm_finalize_big<MODE>, dim3((unsigned)((nchunks + kBigBlock - 1) / kBigBlock)),
+                     dim3(kBigBlock), 0, st, d_chunks, nchunks, d_ws, d_norms, d_mins);
+  return launch_status();
+}
 
 }  // namespace
 
@@ -462,18 +716,14 @@ int adfl_stoch_norms_batched(const float* d_x, const adfl_slq_chunk* d_chunks, i
   hipStream_t st = (hipStream_t)stream;
   if (mode == ADFL_NORM_L2) {
     hipLaunchKernelGGL(k_norm_partials<ADFL_NORM_L2>, dim3((unsigned)nchunks), dim3(kBlock), 0, st, d_x, d_chunks,
-                       d_workspace);
+                       nchunks - kKeepChunks, d_workspace);
     if (int s = launch_status()) return s;
-    hipLaunchKernelGGL(k_norm_finalize<ADFL_NORM_L2>, dim3(finalize_grid(nchunks)), dim3(kBlock), 0, st, d_chunks,
-                       nchunks, (const void*)d_workspace, d_norms, d_mins);
-  } else {
-    hipLaunchKernelGGL(k_norm_partials<ADFL_NORM_LINF>, dim3((unsigned)nchunks), dim3(kBlock), 0, st, d_x,
-                       d_chunks, d_workspace);
-    if (int s = launch_status()) return s;
-    hipLaunchKernelGGL(k_norm_finalize<ADFL_NORM_LINF>, dim3(finalize_grid(nchunks)), dim3(kBlock), 0, st,
-                       d_chunks, nchunks, (const void*)d_workspace, d_norms, d_mins);
+    return launch_finalize<ADFL_NORM_L2>(d_chunks, nchunks, d_workspace, d_norms, d_mins, st);
   }
-  return launch_status();
+  hipLaunchKernelGGL(k_norm_partials<ADFL_NORM_LINF>, dim3((unsigned)nchunks), dim3(kBlock), 0, st, d_x, d_chunks,
+                     nchunks - kKeepChunks, d_workspace);
+  if (int s = launch_status()) return s;
+  return launch_finalize<ADFL_NORM_LINF>(d_chunks, nchunks, d_workspace, d_norms, d_mins, st);
 }
 
 int adfl_qsgd_quantize_batched(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, int bits,
@@ -546,13 +796,11 @@ int adfl_cnat_encode_batched(const float* d_x, const adfl_slq_chunk* d_chunks, i
     return ADFL_E_ALIGN;
   hipStream_t st = (hipStream_t)stream;
   const Uniforms U{d_uniforms, seed, counter};
-  const float min_e = -(float)(1LL << (bits - 1)), max_e = (float)((1LL << (bits - 1)) - 1);  // quant.py:519-520
+  const int min_e = -(1 << (bits - 1)), max_e = (1 << (bits - 1)) - 1;  // quant.py:519-520
   hipLaunchKernelGGL(k_cnat_quantize, dim3((unsigned)nchunks), dim3(kBlock), 0, st, d_x, d_chunks, min_e, max_e, U,
                      d_exps, d_signs, (double*)d_workspace);
   if (int s = launch_status()) return s;
-  hipLaunchKernelGGL(k_norm_finalize<ADFL_NORM_L2>, dim3(finalize_grid(nchunks)), dim3(kBlock), 0, st, d_chunks,
-                     nchunks, (const void*)d_workspace, d_norms, (float*)nullptr);
-  if (int s = launch_status()) return s;
+  if (int s = launch_finalize<ADFL_NORM_L2>(d_chunks, nchunks, d_workspace, d_norms, nullptr, st)) return s;
   hipLaunchKernelGGL(k_cnat_zero_fixup, dim3((unsigned)nchunks), dim3(kBlock), 0, st, d_chunks,
                      (const float*)d_norms, d_exps, d_signs);
   return launch_status();

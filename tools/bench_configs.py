@@ -339,7 +339,29 @@ def mode_stoch(args, world, rank, dev):
                 "decode_frac": round(6 * n / dec / 1e6 / HBM_PEAK_GBS, 3),
                 "round_trip_GiBs": round(4 * n / GIB / ((enc + dec) / 1e3), 1),
                 "wall_ms_per_step": round(wall / args.steps * 1e3, 4)}
-    if rank == 0:
+    # calibration on the same box: the SLQ flat round trip of bench.py's headline kernels
+    from adfl_amd import _lib
+    lib = _lib.load()
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    x = torch.randn(n_flat, device=dev) * 1e-3
+    q = torch.empty(n_flat, dtype=torch.int8, device=dev)
+    sc = torch.empty(1, device=dev)
+    wsl = ops.new_workspace(dev)
+    outf = torch.empty(n_flat, device=dev)
+
+    def slq_step(ev):
+        if ev is not None:
+            ev[0].record()
+        lib.adfl_slq_encode(x.data_ptr(), n_flat, 8, q.data_ptr(), sc.data_ptr(), wsl.data_ptr(), wsl.numel(), sh)
+        if ev is not None:
+            ev[1].record()
+        lib.adfl_slq_dequantize(q.data_ptr(), n_flat, sc.data_ptr(), outf.data_ptr(), sh)
+        if ev is not None:
+            ev[2].record()
+    _, evs = timed(slq_step, args.steps, args.warmup, world, 3)
+    res["c2_flat_slq_calibration"] = {"encode_ms": round(seg_ms(evs, 0, 1), 4), "decode_ms": round(seg_ms(evs, 1, 2), 4)}
+    del x, q, outf
+    if rank == 0 and not args.no_cpu:
         m = 1 << 22
         xs = torch.randn(m) * 1e-3
         torch.set_num_threads(os.cpu_count() if os.cpu_count() <= 16 else 16)
@@ -360,6 +382,7 @@ def main():
     p.add_argument("--elems", type=int, default=0)
     p.add_argument("--packed", action="store_true")
     p.add_argument("--chunks", type=int, default=1)
+    p.add_argument("--no-cpu", action="store_true", help="stoch: skip the host reference timing")
     args = p.parse_args()
     world, rank, local = dist_setup(args)
     dev = torch.device("cuda", local)
