@@ -30,7 +30,7 @@ from typing import Dict, List, Optional, Tuple
 
 import torch
 
-from .. import ops
+from .. import hostcopy, ops
 from ..model import (CompressedParameters, Parameters, QuantParameter, QuantParameters, get_parameter_info)
 from .channel import Channel, IdentityChannel
 
@@ -119,7 +119,11 @@ def _stage_in(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _DeviceSta
     kinds = {t.is_cuda for t in tensors}
     if kinds == {False}:
         host = st.buf(key + "_host", lay.total, dtype, pinned=True)
-        _gather(tensors, lay, host)
+        if all(t.is_contiguous() for t in tensors):
+            # native parallel gather (csrc/host_copy.cpp): pads of an aligned layout are never read
+            hostcopy.gather(tensors, host, lay.offsets)
+        else:
+            _gather(tensors, lay, host)
         dev_buf.copy_(host, non_blocking=True)
     elif kinds == {True}:
         _gather([t.to(st.device) for t in tensors], lay, dev_buf)
@@ -180,7 +184,10 @@ def _decode_dict(items: List[Tuple[str, torch.Tensor]]) -> Dict[str, torch.Tenso
         if q.qscheme() != torch.per_tensor_affine or q.dtype != torch.qint8 or q.q_zero_point() != 0:
             raise ValueError(f"SLQChannel: '{name}' is not a per-tensor qint8 payload with zero point 0")
     lay = st.layout(tuple(int(q.numel()) for _, q in items))
-    q_dev = _stage_in([_int8_view(q) for _, q in items], lay, st, "dq", torch.int8)
+    # CPU qint8 payloads are gathered byte-wise straight from their storage; device ones through int8 views
+    all_host = all(not q.is_cuda and q.is_contiguous() for _, q in items)
+    qs = [q if all_host else _int8_view(q) for _, q in items]
+    q_dev = _stage_in(qs, lay, st, "dq", torch.int8)
     # q_scale() is a double; fbgemm's dequantize uses it as fp32 (quant.py:110), so round it the same way
     s_dev = torch.tensor([q.q_scale() for _, q in items], dtype=torch.float32).to(dev, non_blocking=True)
     on_cpu = [not q.is_cuda for _, q in items]
@@ -376,13 +383,14 @@ class SLQChannel(Channel):
             ops.require_quantizable(params[name])
         encoded = _encode_dict(params, names, bits, stats) if names else {}
         q_params = QuantParameters({}, 0)
+        signs = torch.zeros(1, dtype=torch.uint8)  # the unused field (quant.py:91), one object per call
         for name, param in params.items():
             if name in encoded:
                 q_param, scale = encoded[name]
             else:
                 q_param, scale = param, 1
             q_params.params[name] = QuantParameter(
-                data=q_param, bits=bits, scale=scale, signs=torch.zeros(1, dtype=torch.uint8),
+                data=q_param, bits=bits, scale=scale, signs=signs,
                 shape=param.shape, dtype=param.dtype, q_dtype=q_param.dtype)
             q_params.size += q_param.nbytes
         return q_params

@@ -30,6 +30,7 @@ from typing import Dict, List, Tuple
 
 import torch
 
+from .. import hostcopy
 from .. import stoch as sops
 from ..model import CompressedParameters, Parameters, QuantParameter, QuantParameters, get_parameter_info
 from .channel import Channel, IdentityChannel
@@ -47,6 +48,13 @@ def _owned(parts: List[torch.Tensor], shapes: List[torch.Size]) -> List[torch.Te
     """Per-tensor copies: each payload tensor owns its bytes (it is pickled on its own; the staging
     buffers are reused by the next call)."""
     return [p.view(s).clone() for p, s in zip(parts, shapes)]
+
+
+def _owned_host(buf: torch.Tensor, offsets, shapes: List[torch.Size]) -> List[torch.Tensor]:
+    """_owned for a host bucket: fresh tensors filled by one native parallel scatter."""
+    outs = [torch.empty(s, dtype=buf.dtype) for s in shapes]
+    hostcopy.scatter(buf, outs, offsets)
+    return outs
 
 
 @_serialized
@@ -93,8 +101,8 @@ def _encode_stoch(params: Parameters, names: List[str], codec: str, bits: int, u
     nm = nm_host.tolist()
     sizes, shapes = lay.sizes.tolist(), [t.shape for t in tensors]
     split = lambda buf: [p[:n] for p, n in zip(torch.split(buf, lay.padded.tolist()), sizes)]  # noqa: E731
-    lv_parts = _owned(split(lv_h), shapes) if any(on_cpu) else None
-    sg_parts = _owned(split(sg_h), shapes) if any(on_cpu) else None
+    lv_parts = _owned_host(lv_h, lay.offsets, shapes) if any(on_cpu) else None
+    sg_parts = _owned_host(sg_h, lay.offsets, shapes) if any(on_cpu) else None
     lv_dev = _owned(split(lv), shapes) if not all(on_cpu) else None
     sg_dev = _owned(split(sg), shapes) if not all(on_cpu) else None
     out = {}
@@ -206,6 +214,7 @@ class _StochChannel(Channel):
             _require_fp32(name, params[name], self.__class__.__name__)
         encoded = _encode_stoch(params, names, self.CODEC, bits, uniforms, seed) if names else {}
         q_params = QuantParameters({}, 0)
+        pass_signs = torch.zeros(1, dtype=torch.uint8)  # passthrough entries' unused signs, one per call
         for name, param in params.items():
             if name in encoded:
                 data, signs, scale, scale_2 = encoded[name]
@@ -213,7 +222,7 @@ class _StochChannel(Channel):
                 data = torch.zeros_like(param, dtype=torch.uint8)
                 signs, scale, scale_2 = torch.ones_like(param, dtype=torch.int8), torch.tensor(0.0), 0
             else:
-                data, signs, scale, scale_2 = param, torch.zeros(1, dtype=torch.uint8), 0, 0
+                data, signs, scale, scale_2 = param, pass_signs, 0, 0
             q_params.params[name] = QuantParameter(data=data, bits=bits, scale=scale, signs=signs, shape=param.shape,
                                                    dtype=param.dtype, q_dtype=data.dtype, scale_2=scale_2)
             q_params.size += data.nbytes

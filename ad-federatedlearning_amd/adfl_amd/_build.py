@@ -7,7 +7,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 SRC_ROOT = os.path.dirname(PKG_DIR)                      # ad-federatedlearning_amd/
 REPO_ROOT = os.path.dirname(SRC_ROOT)
 CSRC = os.path.join(SRC_ROOT, "csrc", "slq_codec.hip")
-SOURCES = [CSRC, os.path.join(SRC_ROOT, "csrc", "stoch_codec.hip")]
+SOURCES = [CSRC, os.path.join(SRC_ROOT, "csrc", "stoch_codec.hip"), os.path.join(SRC_ROOT, "csrc", "host_copy.cpp")]
 DEPENDS = SOURCES + [os.path.join(SRC_ROOT, "csrc", "cnat_log2_table.h")]
 INCLUDE = os.path.join(REPO_ROOT, "include")
 LIB_DIR = os.path.join(PKG_DIR, "lib")
@@ -20,7 +20,7 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp
 
 def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(LIB_DIR, exist_ok=True)
-    deps = DEPENDS + [os.path.join(INCLUDE, h) for h in ("adfl_slq.h", "adfl_stoch.h")]
+    deps = DEPENDS + [os.path.join(INCLUDE, h) for h in ("adfl_slq.h", "adfl_stoch.h", "adfl_host.h")]
     if (not force and os.path.exists(LIB_PATH)
             and os.path.getmtime(LIB_PATH) >= max(os.path.getmtime(d) for d in deps)):
         return LIB_PATH

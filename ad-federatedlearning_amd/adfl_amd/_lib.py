@@ -1,4 +1,4 @@
-"""ctypes binding of libadfl_slq.so (the C ABI declared in include/adfl_slq.h and include/adfl_stoch.h).
+"""ctypes binding of libadfl_slq.so (the C ABI declared in include/adfl_slq.h, adfl_stoch.h and adfl_host.h).
 
 The product path has no CPU fallback: if the HIP library is missing this module raises at import
 time, and every op checks the status code the library returns.
@@ -34,7 +34,7 @@ class Chunk(ctypes.Structure):
     _fields_ = [("start", I64), ("len", I32), ("tensor", I32), ("first_chunk", I32), ("nchunks", I32)]
 
 
-# name -> (restype, argtypes); the complete exported surface of include/adfl_slq.h + adfl_stoch.h
+# name -> (restype, argtypes); the complete exported surface of include/adfl_slq.h + adfl_stoch.h + adfl_host.h
 SIGNATURES = {
     "adfl_slq_abi_version": (INT, []),
     "adfl_slq_strerror": (ctypes.c_char_p, [INT]),
@@ -68,6 +68,9 @@ SIGNATURES = {
     "adfl_cnat_encode_batched": (INT, [P, P, I64, INT, P, U64, U64, P, I64, P, P, P, P]),
     "adfl_cnat_dequantize_batched": (INT, [P, P, P, I64, P, P, P]),
     "adfl_philox_uniforms": (INT, [P, I64, I64, U64, U64, P]),
+    # adfl_host.h
+    "adfl_host_copy": (INT, [P, P, P, I64, I32]),
+    "adfl_host_threads": (I32, []),
 }
 
 NORM_L2, NORM_LINF = 0, 1  # ADFL_NORM_*

@@ -1,0 +1,47 @@
+"""Parallel host staging copies over the native pool (include/adfl_host.h, csrc/host_copy.cpp).
+
+gather(): pieces of a CPU state dict -> one (pinned) host bucket; scatter(): a host bucket -> per-tensor
+storages. ctypes releases the GIL for the call, so the copy runs on the pool's threads plus the caller's.
+"""
+
+from typing import Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check
+
+
+def copy_pieces(dst_ptrs: Sequence[int], src_ptrs: Sequence[int], nbytes: Sequence[int], threads: int = 0) -> None:
+    d = np.asarray(dst_ptrs, dtype=np.uint64)
+    s = np.asarray(src_ptrs, dtype=np.uint64)
+    b = np.asarray(nbytes, dtype=np.int64)
+    if not (len(d) == len(s) == len(b)):
+        raise ValueError("copy_pieces: pointer and size lists differ in length")
+    check(_lib.load().adfl_host_copy(d.ctypes.data, s.ctypes.data, b.ctypes.data, len(b), threads))
+
+
+def gather(srcs: Sequence[torch.Tensor], dst: torch.Tensor, offsets: Sequence[int]) -> None:
+    """dst.view(-1)[offsets[k] : offsets[k] + srcs[k].numel()] = srcs[k] for contiguous CPU tensors of
+    dst's element size (byte copies; dtypes of equal size are reinterpreted)."""
+    es = dst.element_size()
+    base = dst.data_ptr()
+    for t in srcs:
+        if t.is_cuda or not t.is_contiguous() or t.element_size() != es:
+            raise ValueError("hostcopy.gather: sources must be contiguous CPU tensors of the bucket's element size")
+    copy_pieces([base + int(o) * es for o in offsets], [t.data_ptr() for t in srcs], [t.numel() * es for t in srcs])
+
+
+def scatter(src: torch.Tensor, dsts: Sequence[torch.Tensor], offsets: Sequence[int]) -> None:
+    """dsts[k] = src.view(-1)[offsets[k] : offsets[k] + dsts[k].numel()] (byte copies)."""
+    es = src.element_size()
+    base = src.data_ptr()
+    for t in dsts:
+        if t.is_cuda or not t.is_contiguous() or t.element_size() != es:
+            raise ValueError("hostcopy.scatter: destinations must be contiguous CPU tensors of the bucket's element size")
+    copy_pieces([t.data_ptr() for t in dsts], [base + int(o) * es for o in offsets], [t.numel() * es for t in dsts])
+
+
+def threads() -> int:
+    return int(_lib.load().adfl_host_threads())
