@@ -112,6 +112,23 @@ def _gather(tensors: List[torch.Tensor], lay: ops.BucketLayout, out: torch.Tenso
     torch.cat(pieces, out=out)
 
 
+_PIECE_BYTES = 8 << 20  # staging pieces of at least this size: one gather + one H2D each
+
+
+def _pieces(lay: ops.BucketLayout, elem_bytes: int) -> List[Tuple[int, int]]:
+    """Split the tensors of `lay` into consecutive runs [a, b) of about max(_PIECE_BYTES, total / 4) bytes."""
+    target = max(_PIECE_BYTES, lay.total * elem_bytes // 4)
+    out, a, acc = [], 0, 0
+    for i, n in enumerate(lay.padded.tolist()):
+        acc += n * elem_bytes
+        if acc >= target:
+            out.append((a, i + 1))
+            a, acc = i + 1, 0
+    if a < lay.ntensors:
+        out.append((a, lay.ntensors))
+    return out
+
+
 def _stage_in(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _DeviceStaging, key: str,
               dtype: torch.dtype) -> torch.Tensor:
     """The bucket on the device: one gather + one H2D for CPU tensors, one device gather otherwise."""
@@ -120,11 +137,18 @@ def _stage_in(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _DeviceSta
     if kinds == {False}:
         host = st.buf(key + "_host", lay.total, dtype, pinned=True)
         if all(t.is_contiguous() for t in tensors):
-            # native parallel gather (csrc/host_copy.cpp): pads of an aligned layout are never read
-            hostcopy.gather(tensors, host, lay.offsets)
+            # Native parallel gather (csrc/host_copy.cpp) in tensor-aligned pieces, each piece's H2D
+            # enqueued as soon as it is staged so the copy engine overlaps the next piece's host copy.
+            # Pads of an aligned layout are never read.
+            offs = lay.offsets.tolist()
+            for a, b in _pieces(lay, host.element_size()):
+                hostcopy.gather(tensors[a:b], host, offs[a:b])
+                lo = offs[a]
+                hi = offs[b] if b < len(offs) else lay.total
+                dev_buf[lo:hi].copy_(host[lo:hi], non_blocking=True)
         else:
             _gather(tensors, lay, host)
-        dev_buf.copy_(host, non_blocking=True)
+            dev_buf.copy_(host, non_blocking=True)
     elif kinds == {True}:
         _gather([t.to(st.device) for t in tensors], lay, dev_buf)
     else:  # mixed host / device dict: per-tensor copies (rare)
