@@ -111,10 +111,12 @@ class PeerExchange:
         return works
 
     def mean(self, works: List, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """Wait for each chunk's all-gather and decode the K payloads into their fp32 mean."""
+        """Wait for each chunk's all-gather and decode the K payloads into their fp32 mean (a `None` work
+        is a chunk whose collective the caller has already waited on)."""
         out = torch.empty(self.numel, dtype=torch.float32, device=self.device) if out is None else out
         for (c0, c1), rows, pb, w in zip(self.bounds, self.gathered, self.payload, works):
-            w.wait()
+            if w is not None:
+                w.wait()
             self.codec.mean(rows, c1 - c0, self.packed, pb, out[c0:c1])
         return out
 

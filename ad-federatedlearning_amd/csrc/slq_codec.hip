@@ -500,8 +500,64 @@ __device__ __forceinline__ int chunk_head(int64_t start, int len, int align) {
   return h < len ? h : len;
 }
 
-// Pass 1 keeps default (allocating) loads: a bucketed update (e.g. 46.8 MB for ResNet-18) fits the
-// Infinity Cache whole, so pass 2 re-reads it on-die.
+// A chunk (<= 8192 elements) is at most 2 wave tiles per wave + < 1024 tail elements + < 16 head
+// elements: small enough to hold in VGPRs, so each pass issues ALL of a chunk's loads before the first
+// use (8 x 16 B per lane in flight; a one-tile-at-a-time loop leaves a 32 KiB chunk latency-bound).
+constexpr int kChunkTilesPerWave = ADFL_SLQ_CHUNK_ELEMS / kTile / kWaves;  // 2
+constexpr int kChunkTailPerThread = kTile / kBlock;                        // < 1024 tail elements -> 4
+static_assert(ADFL_SLQ_CHUNK_ELEMS % (kTile * kWaves) == 0, "chunk = whole tiles per wave");
+
+struct ChunkRegs {
+  float4 v[kChunkTilesPerWave][4];
+  float tail[kChunkTailPerThread];
+  float head;
+};
+
+// Load chunk c (x non-temporal: dead after this pass) into registers in the quantize tile layout.
+__device__ __forceinline__ void chunk_load(const float* __restrict__ x, const adfl_slq_chunk& c, ChunkRegs& r,
+                                           int lane, int wave) {
+  const float* xc = x + c.start;
+  const int head = chunk_head(c.start, c.len, 16);  // 16 elements: 64-B x and 16-B payload alignment
+  const int ntiles = (c.len - head) / kTile;
+  const float4* x4 = reinterpret_cast<const float4*>(xc + head);
+#pragma unroll
+  for (int k = 0; k < kChunkTilesPerWave; ++k) {
+    const int t = wave + k * kWaves;
+    if (t < ntiles) load_tile(x4 + t * (kTile / 4), r.v[k], lane);
+  }
+  r.head = (int)threadIdx.x < head ? xc[threadIdx.x] : 0.0f;
+  const int t0 = head + ntiles * kTile;
+#pragma unroll
+  for (int k = 0; k < kChunkTailPerThread; ++k) {
+    const int i = t0 + k * kBlock + (int)threadIdx.x;
+    r.tail[k] = i < c.len ? __builtin_nontemporal_load(xc + i) : 0.0f;
+  }
+}
+
+// Quantize the registers of chunk c into the payload (tiles through the wave's LDS transpose).
+__device__ __forceinline__ void chunk_store(const adfl_slq_chunk& c, const ChunkRegs& r, float inv,
+                                            int8_t* __restrict__ q, uint32_t* __restrict__ lds, int lane, int wave) {
+  int8_t* qc = q + c.start;
+  const int head = chunk_head(c.start, c.len, 16);
+  const int ntiles = (c.len - head) / kTile;
+  uint4* q16 = reinterpret_cast<uint4*>(qc + head);
+#pragma unroll
+  for (int k = 0; k < kChunkTilesPerWave; ++k) {
+    const int t = wave + k * kWaves;
+    if (t < ntiles) quantize_tile_regs(r.v[k], q16 + t * (kTile / 16), inv, lds, lane);
+  }
+  if ((int)threadIdx.x < head) qc[threadIdx.x] = (int8_t)quant1(r.head, inv);
+  const int t0 = head + ntiles * kTile;
+#pragma unroll
+  for (int k = 0; k < kChunkTailPerThread; ++k) {
+    const int i = t0 + k * kBlock + (int)threadIdx.x;
+    if (i < c.len) qc[i] = (int8_t)quant1(r.tail[k], inv);
+  }
+}
+
+// Pass 1: one partial per chunk. Non-temporal loads, all in flight: on a C3-sized bucket this is
+// 1.5x faster than allocating loads that leave x in the Infinity Cache for pass 2
+// (profiles/r01/microbench_bucket.txt).
 __global__ __launch_bounds__(kBlock) void k_absmax_batched(const float* __restrict__ x,
                                                            const adfl_slq_chunk* __restrict__ chunks,
                                                            uint32_t* __restrict__ partials) {
@@ -510,35 +566,37 @@ __global__ __launch_bounds__(kBlock) void k_absmax_batched(const float* __restri
   const int head = chunk_head(c.start, c.len, 4);
   const float4* x4 = reinterpret_cast<const float4*>(xc + head);
   const int n4 = (c.len - head) >> 2;
+  constexpr int U = ADFL_SLQ_CHUNK_ELEMS / 4 / kBlock;  // 8 float4 per thread
+  float4 v[U];
+#pragma unroll
+  for (int k = 0; k < U; ++k) {
+    const int i = (int)threadIdx.x + k * kBlock;
+    v[k] = i < n4 ? load4<true>(x4 + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   uint32_t m = 0;
   if (threadIdx.x < head) m = abs_bits(xc[threadIdx.x]);
-  for (int i = threadIdx.x; i < n4; i += kBlock) m = max(m, abs_bits4(x4[i]));
   const int tail = head + (n4 << 2);
   if (threadIdx.x < c.len - tail) m = max(m, abs_bits(xc[tail + threadIdx.x]));
+#pragma unroll
+  for (int k = 0; k < U; ++k) m = max(m, abs_bits4(v[k]));
   m = block_max(m);
   if (threadIdx.x == 0) partials[blockIdx.x] = m;
 }
 
+// Pass 2: the chunk's loads are issued before the partial reduction, whose latency they hide.
 __global__ __launch_bounds__(kBlock) void k_quantize_batched(const float* __restrict__ x,
                                                              const adfl_slq_chunk* __restrict__ chunks,
-                                                             int64_t nchunks, float qmax,
-                                                             const uint32_t* __restrict__ partials,
+                                                             float qmax, const uint32_t* __restrict__ partials,
                                                              int8_t* __restrict__ q, float* __restrict__ scales) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kWaves][kTile / 4];
-  const int64_t ci = nchunks - 1 - (int64_t)blockIdx.x;  // reverse of pass 1
+  const int64_t ci = blockIdx.x;
   const adfl_slq_chunk c = chunks[ci];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  ChunkRegs r;
+  chunk_load(x, c, r, lane, wave);
   const ScaleInv si = make_scale(reduce_partials(partials + c.first_chunk, c.nchunks), qmax);
   if (ci == c.first_chunk && threadIdx.x == 0) scales[c.tensor] = si.scale;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const float* xc = x + c.start;
-  int8_t* qc = q + c.start;
-  const int head = chunk_head(c.start, c.len, 16);  // 16 elements: 64-B x and 16-B payload alignment
-  if (threadIdx.x < head) qc[threadIdx.x] = (int8_t)quant1(xc[threadIdx.x], si.inv);
-  const int ntiles = (c.len - head) / kTile;
-  for (int t = wave; t < ntiles; t += kWaves)
-    quantize_tile(reinterpret_cast<const float4*>(xc + head) + t * (kTile / 4),
-                  reinterpret_cast<uint4*>(qc + head) + t * (kTile / 16), si.inv, lds[wave], lane);
-  for (int i = head + ntiles * kTile + threadIdx.x; i < c.len; i += kBlock) qc[i] = (int8_t)quant1(xc[i], si.inv);
+  chunk_store(c, r, si.inv, q, lds[wave], lane, wave);
 }
 
 __global__ __launch_bounds__(kBlock) void k_dequantize_batched(const int8_t* __restrict__ q,
@@ -808,8 +866,8 @@ int adfl_slq_encode_batched(const float* d_x, const adfl_slq_chunk* d_chunks, in
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(k_absmax_batched, dim3((unsigned)nchunks), dim3(kBlock), 0, st, d_x, d_chunks, d_partials);
   if (int s = launch_status()) return s;
-  hipLaunchKernelGGL(k_quantize_batched, dim3((unsigned)nchunks), dim3(kBlock), 0, st, d_x, d_chunks, nchunks,
-                     qmax_f(bits), (const uint32_t*)d_partials, d_q, d_scales);
+  hipLaunchKernelGGL(k_quantize_batched, dim3((unsigned)nchunks), dim3(kBlock), 0, st, d_x, d_chunks, qmax_f(bits),
+                     (const uint32_t*)d_partials, d_q, d_scales);
   return launch_status();
 }
 

@@ -12,7 +12,10 @@ Also reported on the same line:
   events on the launch stream inside the timed region, against the 8.0 TB/s HBM3E peak; `traffic` is
   the PMC-measured HBM bytes per launch from profiles/ when a summary for that kernel exists;
 * cpu_baseline — the reference's ATen op sequence (quant.py:100-103,110) timed on this host's cores
-  (rank 0, N=1), over a bounded sample of the same workload.
+  (rank 0, N=1), over a bounded sample of the same workload;
+* exchange (N > 1, or --exchange on) — BASELINE configs[3] (C4) on the same buffers after the timed
+  headline: encode + RCCL all-gather of the int8 payloads over xGMI + fused decode-mean, with the
+  all-gather's bus bandwidth. Never part of `value`.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 """
@@ -45,6 +48,8 @@ def parse():
     p.add_argument("--bits", type=int, default=8)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget for the CPU baseline sample")
+    p.add_argument("--exchange", choices=("auto", "on", "off"), default="auto",
+                   help="C4 peer-exchange leg (encode + RCCL all-gather + decode-mean); auto = only when N > 1")
     return p.parse_args()
 
 
@@ -119,6 +124,57 @@ def cpu_baseline(x_dev: torch.Tensor, bits: int, budget_s: float, q_dev: torch.T
     return cpu, parity
 
 
+def exchange_leg(x: torch.Tensor, out: torch.Tensor, bits: int, world: int, steps: int, warmup: int):
+    """BASELINE configs[3] (C4) on the same buffers: every rank is one simulated client that encodes its
+    1 GiB update, all-gathers the int8 payloads (+ scale trailers) over RCCL and decodes the K payloads
+    into their fp32 mean in one fused launch (adfl_amd.exchange; Examples/ray_ad.py:164-190). Reported
+    beside the headline, never as `value`. Segments are HIP events on the compute stream: the stream
+    waits on the all-gather, so [encode end, wait] is the collective as the codec sees it."""
+    import torch.distributed as dist
+    from adfl_amd.exchange import PeerExchange
+
+    n = x.numel()
+    ex = PeerExchange(n, bits=bits, device=x.device)
+    flat, flat_out = x.reshape(-1), out.reshape(-1)
+    stream = torch.cuda.current_stream(x.device)
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        works = ex.encode_and_gather(flat)
+        if ev is not None:
+            ev[1].record(stream)
+        for w in works:
+            w.wait()
+        if ev is not None:
+            ev[2].record(stream)
+        ex.mean([None] * len(works), flat_out)
+        if ev is not None:
+            ev[3].record(stream)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(steps)]
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    barrier(world)
+    t = max_over_ranks(time.perf_counter() - t0, world) / steps
+    seg = [max_over_ranks(sum(e[i].elapsed_time(e[i + 1]) for e in evs) / steps, world) for i in range(3)]
+    recv = ex.bytes_per_rank * (world - 1)          # bytes each rank receives (rccl-tests: busbw)
+    return {"workload": f"C4: {world} simulated clients x 1 GiB fp32, SLQ bits={bits} encode + RCCL "
+                        f"all_gather_into_tensor + fused decode-mean", "steps": steps,
+            "ms_per_step": round(t * 1e3, 4), "GiB_per_s": round(world * n * 4 / GIB / t, 2),
+            "encode_ms": round(seg[0], 4), "allgather_wait_ms": round(seg[1], 4), "mean_ms": round(seg[2], 4),
+            "bytes_per_rank_on_wire": ex.bytes_per_rank,
+            "allgather_busbw_GBs": round(recv / (seg[1] * 1e-3) / 1e9, 1) if world > 1 and seg[1] > 0 else None,
+            "backend": dist.get_backend()}
+
+
 def main():
     args = parse()
     world, rank, local = dist_setup(args)
@@ -166,6 +222,14 @@ def main():
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(elapsed, world)
 
+    exchange = None
+    if args.exchange == "on" or (args.exchange == "auto" and world > 1):
+        if world == 1:
+            import torch.distributed as dist
+            dist.init_process_group("nccl", init_method="tcp://127.0.0.1:29577", rank=0, world_size=1,
+                                    device_id=dev)
+        exchange = exchange_leg(x, out, args.bits, world, min(args.steps, 20), min(args.warmup, 3))
+
     per_kernel = {name: sum(e[i].elapsed_time(e[i + 1]) for e in events) / args.steps
                   for i, name in enumerate(("absmax", "quantize", "dequantize"))}
     ms_per_step = elapsed / args.steps * 1e3
@@ -173,7 +237,7 @@ def main():
     value = world * gib_per_rank / (elapsed / args.steps)
 
     if rank != 0:
-        if world > 1:
+        if torch.distributed.is_initialized():
             torch.distributed.destroy_process_group()
         return
     dominant = max(per_kernel, key=per_kernel.get)
@@ -198,12 +262,14 @@ def main():
                                 "wall_frac": round(14 * n / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
         "cpu_baseline": None,
     }
+    if exchange is not None:
+        line["exchange"] = exchange
     if world == 1 and not args.no_cpu_baseline:
         cpu, parity = cpu_baseline(x, args.bits, args.cpu_seconds, q, scale)
         line["cpu_baseline"] = cpu
         line["parity_vs_reference_ops"] = parity
     print(json.dumps(line), flush=True)
-    if world > 1:
+    if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
 
 

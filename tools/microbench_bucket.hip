@@ -1,0 +1,260 @@
+// microbench_bucket.hip — the bucketed (state-dict) codec on the C3 bucket (11,689,512 fp32 in 256
+// tensors, 1536 chunks), Infinity Cache warm and flushed: the product encode (non-temporal absmax with
+// all loads in flight, register-staged quantize) against the previous product pair and against a
+// one-launch register-resident encode (x read once, inter-block hand-off), and two decode shapes.
+// Not part of the product; it #includes the product source to reach its helpers.
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -Iinclude -o tools/microbench_bucket tools/microbench_bucket.hip
+#include "../ad-federatedlearning_amd/csrc/slq_codec.hip"
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#define CK(x)                                                                                \
+  do {                                                                                       \
+    hipError_t e_ = (hipError_t)(x);                                                                 \
+    if (e_ != hipSuccess) {                                                                  \
+      fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+      exit(1);                                                                               \
+    }                                                                                        \
+  } while (0)
+
+namespace {
+// ---- the previous product pair: allocating one-float4-per-iteration absmax, per-tile reverse quantize
+__global__ __launch_bounds__(kBlock) void k_absmax_old(const float* __restrict__ x, const adfl_slq_chunk* __restrict__ chunks,
+                                                       uint32_t* __restrict__ partials) {
+  const adfl_slq_chunk c = chunks[blockIdx.x];
+  const float* xc = x + c.start;
+  const int head = chunk_head(c.start, c.len, 4);
+  const float4* x4 = reinterpret_cast<const float4*>(xc + head);
+  const int n4 = (c.len - head) >> 2;
+  uint32_t m = 0;
+  if (threadIdx.x < head) m = abs_bits(xc[threadIdx.x]);
+  for (int i = threadIdx.x; i < n4; i += kBlock) m = max(m, abs_bits4(x4[i]));
+  const int tail = head + (n4 << 2);
+  if (threadIdx.x < c.len - tail) m = max(m, abs_bits(xc[tail + threadIdx.x]));
+  m = block_max(m);
+  if (threadIdx.x == 0) partials[blockIdx.x] = m;
+}
+
+__global__ __launch_bounds__(kBlock) void k_quantize_old(const float* __restrict__ x, const adfl_slq_chunk* __restrict__ chunks,
+                                                         int64_t nchunks, float qmax, const uint32_t* __restrict__ partials,
+                                                         int8_t* __restrict__ q, float* __restrict__ scales) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kWaves][kTile / 4];
+  const int64_t ci = nchunks - 1 - (int64_t)blockIdx.x;
+  const adfl_slq_chunk c = chunks[ci];
+  const ScaleInv si = make_scale(reduce_partials(partials + c.first_chunk, c.nchunks), qmax);
+  if (ci == c.first_chunk && threadIdx.x == 0) scales[c.tensor] = si.scale;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const float* xc = x + c.start;
+  int8_t* qc = q + c.start;
+  const int head = chunk_head(c.start, c.len, 16);
+  if (threadIdx.x < head) qc[threadIdx.x] = (int8_t)quant1(xc[threadIdx.x], si.inv);
+  const int ntiles = (c.len - head) / kTile;
+  for (int t = wave; t < ntiles; t += kWaves)
+    quantize_tile(reinterpret_cast<const float4*>(xc + head) + t * (kTile / 4),
+                  reinterpret_cast<uint4*>(qc + head) + t * (kTile / 16), si.inv, lds[wave], lane);
+  for (int i = head + ntiles * kTile + threadIdx.x; i < c.len; i += kBlock) qc[i] = (int8_t)quant1(xc[i], si.inv);
+}
+
+// ---- one-launch register-resident encode (measured dead end, kept as the record) -----------------
+// Every block holds its chunk in VGPRs, publishes the chunk partial, waits until its tensor's chunks
+// have all arrived, quantizes from registers: x read once (5 B/elem), one launch. WAIT 0 skips the
+// hand-off (own partial as the scale: timing floor only). Hand-off through agent-scope atomics only
+// (coherent, sc1); an agent release/acquire (buffer_wbl2 / buffer_inv per block) measured 3x slower.
+// DONE 1: one global done counter re-arms the arrival counters (every block hits one word).
+template <int WAIT, int DONE>
+__global__ __launch_bounds__(kBlock) void k_resident(const float* __restrict__ x, const adfl_slq_chunk* __restrict__ chunks,
+                                                     int64_t nchunks, int32_t ntensors, float qmax,
+                                                     uint32_t* __restrict__ partials, uint32_t* __restrict__ sync,
+                                                     int8_t* __restrict__ q, float* __restrict__ scales) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kWaves][kTile / 4];
+  __shared__ uint32_t red[kWaves];
+  __shared__ uint32_t bc;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  ChunkRegs r;
+  const adfl_slq_chunk c = chunks[blockIdx.x];
+  chunk_load(x, c, r, lane, wave);
+  uint32_t m = abs_bits(r.head);
+  const int ntiles = (c.len - chunk_head(c.start, c.len, 16)) / kTile;
+  for (int k = 0; k < kChunkTilesPerWave; ++k)
+    if (wave + k * kWaves < ntiles)
+      for (int j = 0; j < 4; ++j) m = max(m, abs_bits4(r.v[k][j]));
+  for (int k = 0; k < kChunkTailPerThread; ++k) m = max(m, abs_bits(r.tail[k]));
+  m = wave_max(m);
+  if (lane == 0) red[wave] = m;
+  __syncthreads();
+  m = max(max(red[0], red[1]), max(red[2], red[3]));
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(partials + blockIdx.x, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __hip_atomic_fetch_add(sync + c.tensor, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (WAIT) {
+      const uint64_t t0 = wall_clock64();
+      while (__hip_atomic_load(sync + c.tensor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)c.nchunks) {
+        if (wall_clock64() - t0 > 20000) break;  // 200 us: never hangs (timing tool; no fallback)
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+  }
+  __syncthreads();
+  uint32_t am = m;
+  if (WAIT) {
+    am = 0;
+    for (int k = threadIdx.x; k < c.nchunks; k += kBlock)
+      am = max(am, __hip_atomic_load(partials + c.first_chunk + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    am = wave_max(am);
+    __syncthreads();
+    if (lane == 0) red[wave] = am;
+    __syncthreads();
+    am = max(max(red[0], red[1]), max(red[2], red[3]));
+  }
+  const ScaleInv si = make_scale(am, qmax);
+  if (blockIdx.x == c.first_chunk && threadIdx.x == 0) scales[c.tensor] = si.scale;
+  chunk_store(c, r, si.inv, q, lds[wave], lane, wave);
+  if (!DONE) return;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    bc = __hip_atomic_fetch_add(sync + ntensors, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (bc)
+    for (int t = threadIdx.x; t <= ntensors; t += kBlock) __hip_atomic_store(sync + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// decode with both of a wave's tiles loaded before either is processed
+__global__ __launch_bounds__(kBlock) void k_dequantize_v2(const int8_t* __restrict__ q, const adfl_slq_chunk* __restrict__ chunks,
+                                                          const float* __restrict__ scales, float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kWaves][kTile / 4];
+  const adfl_slq_chunk c = chunks[blockIdx.x];
+  const float s = scales[c.tensor];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int8_t* qc = q + c.start;
+  float* oc = out + c.start;
+  const int head = chunk_head(c.start, c.len, 16);
+  const int ntiles = (c.len - head) / kTile;
+  const uint4* q16 = reinterpret_cast<const uint4*>(qc + head);
+  uint4 w[kChunkTilesPerWave];
+#pragma unroll
+  for (int k = 0; k < kChunkTilesPerWave; ++k) {
+    const int t = wave + k * kWaves;
+    if (t < ntiles) w[k] = q16[t * (kTile / 16) + lane];
+  }
+  if (threadIdx.x < head) oc[threadIdx.x] = s * (float)qc[threadIdx.x];
+  for (int i = head + ntiles * kTile + threadIdx.x; i < c.len; i += kBlock) oc[i] = s * (float)qc[i];
+#pragma unroll
+  for (int k = 0; k < kChunkTilesPerWave; ++k) {
+    const int t = wave + k * kWaves;
+    if (t < ntiles) {
+      reinterpret_cast<uint4*>(lds[wave])[lane] = w[k];
+      __builtin_amdgcn_wave_barrier();
+      uint32_t d[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) d[j] = lds[wave][j * 64 + lane];
+      __builtin_amdgcn_wave_barrier();
+      float4* o4 = reinterpret_cast<float4*>(oc + head) + t * (kTile / 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) store4_nt(o4 + j * 64 + lane, dequant4(d[j], s));
+    }
+  }
+}
+
+__global__ void k_flush(uint4* p, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = make_uint4(1, 2, 3, 4);
+}
+}  // namespace
+
+int main() {
+  const int64_t total_params = 11689512;
+  std::vector<int64_t> sizes(256), offs(256);
+  int64_t o = 0;
+  for (int i = 0; i < 256; ++i) {
+    sizes[i] = total_params / 256 + (i < total_params % 256 ? 1 : 0);
+    offs[i] = o;
+    o += (sizes[i] + 63) / 64 * 64;
+  }
+  const int64_t total = o;
+  const int64_t nch = adfl_slq_build_chunks(offs.data(), sizes.data(), 256, nullptr, 0);
+  std::vector<adfl_slq_chunk> ch(nch);
+  adfl_slq_build_chunks(offs.data(), sizes.data(), 256, ch.data(), nch);
+  float* x;
+  int8_t *q, *q_ref;
+  float *sc, *sc_ref;
+  uint32_t *part, *sync;
+  adfl_slq_chunk* dch;
+  uint4* junk;
+  CK(hipMalloc(&x, total * 4));
+  CK(hipMalloc(&q, total));
+  CK(hipMalloc(&q_ref, total));
+  CK(hipMalloc(&sc, 256 * 4));
+  CK(hipMalloc(&sc_ref, 256 * 4));
+  CK(hipMalloc(&part, nch * 4));
+  CK(hipMalloc(&sync, 258 * 4));
+  CK(hipMalloc(&dch, nch * sizeof(adfl_slq_chunk)));
+  CK(hipMalloc(&junk, 512ll << 20));
+  CK(hipMemset(sync, 0, 258 * 4));
+  CK(hipMemcpy(dch, ch.data(), nch * sizeof(adfl_slq_chunk), hipMemcpyHostToDevice));
+  std::vector<float> hx(total);
+  uint32_t s = 12345;
+  for (auto& v : hx) {
+    s = s * 1664525u + 1013904223u;
+    v = ((int32_t)s) * 1e-12f;
+  }
+  CK(hipMemcpy(x, hx.data(), total * 4, hipMemcpyHostToDevice));
+  CK(adfl_slq_encode_batched(x, dch, nch, 8, q_ref, sc_ref, part, nullptr));
+  CK(hipDeviceSynchronize());
+  uint32_t* sync_floor;  // the no-hand-off floor never re-arms: keep its counters away from the real ones
+  CK(hipMalloc(&sync_floor, 258 * 4));
+  auto launch_res = [&](auto kern, uint32_t* sy) {
+    hipLaunchKernelGGL(kern, dim3(nch), dim3(kBlock), 0, 0, x, dch, nch, 256, 127.f, part, sy, q, sc);
+  };
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  float *out, *out_ref;
+  CK(hipMalloc(&out, total * 4));
+  CK(hipMalloc(&out_ref, total * 4));
+  CK(adfl_slq_dequantize_batched(q_ref, dch, nch, sc_ref, out_ref, nullptr));
+  const char* names[] = {"enc product", "enc previous product", "enc one-launch resident", "enc floor (no hand-off)",
+                         "dec product", "dec loads-first"};
+  const int nv = 6;
+  std::vector<double> tot(nv, 0), totf(nv, 0);
+  std::vector<int> ok(nv, 1);
+  for (int rep = 0; rep < 52; ++rep)
+    for (int v = 0; v < nv; ++v)
+      for (int flush = 0; flush < 2; ++flush) {
+        if (flush) hipLaunchKernelGGL(k_flush, dim3(4096), dim3(256), 0, 0, junk, (512ll << 20) / 16);
+        CK(hipEventRecord(e0, 0));
+        switch (v) {
+          case 0: CK(adfl_slq_encode_batched(x, dch, nch, 8, q, sc, part, nullptr)); break;
+          case 1:
+            hipLaunchKernelGGL(k_absmax_old, dim3(nch), dim3(kBlock), 0, 0, x, dch, part);
+            hipLaunchKernelGGL(k_quantize_old, dim3(nch), dim3(kBlock), 0, 0, x, dch, nch, 127.f, part, q, sc);
+            break;
+          case 2: launch_res(k_resident<1, 1>, sync); break;
+          case 3: launch_res(k_resident<0, 0>, sync_floor); break;
+          case 4: CK(adfl_slq_dequantize_batched(q_ref, dch, nch, sc_ref, out, nullptr)); break;
+          case 5: hipLaunchKernelGGL(k_dequantize_v2, dim3(nch), dim3(kBlock), 0, 0, q_ref, dch, sc_ref, out); break;
+        }
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (rep >= 2) (flush ? totf : tot)[v] += ms;
+        if (rep == 1 && v != 3) {
+          const bool enc = v < 4;
+          std::vector<uint8_t> a(total * (enc ? 1 : 4)), b(total * (enc ? 1 : 4));
+          CK(hipMemcpy(a.data(), enc ? (void*)q : (void*)out, a.size(), hipMemcpyDeviceToHost));
+          CK(hipMemcpy(b.data(), enc ? (void*)q_ref : (void*)out_ref, b.size(), hipMemcpyDeviceToHost));
+          const int w = enc ? 1 : 4;
+          for (int t = 0; t < 256 && ok[v]; ++t)
+            if (memcmp(a.data() + offs[t] * w, b.data() + offs[t] * w, sizes[t] * w)) ok[v] = 0;
+        }
+      }
+  for (int v = 0; v < nv; ++v)
+    printf("%-26s cached %.4f ms  flushed %.4f ms  %s\n", names[v], tot[v] / 50, totf[v] / 50,
+           v != 3 ? (ok[v] ? "bit-exact" : "MISMATCH") : "(timing only)");
+  return 0;
+}
