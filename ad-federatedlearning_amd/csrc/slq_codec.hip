@@ -555,9 +555,9 @@ __device__ __forceinline__ void chunk_store(const adfl_slq_chunk& c, const Chunk
   }
 }
 
-// Pass 1: one partial per chunk. Non-temporal loads, all in flight: on a C3-sized bucket this is
-// 1.5x faster than allocating loads that leave x in the Infinity Cache for pass 2
-// (profiles/r01/microbench_bucket.txt).
+// Pass 1: one partial per chunk, all of the chunk's loads in flight. Non-temporal: in the C3 config
+// bench, allocating loads (x left in the Infinity Cache for pass 2) measured the same (A/B in
+// profiles/r01/c3_absmax_policy.txt), and NT leaves the cache to the payload.
 __global__ __launch_bounds__(kBlock) void k_absmax_batched(const float* __restrict__ x,
                                                            const adfl_slq_chunk* __restrict__ chunks,
                                                            uint32_t* __restrict__ partials) {

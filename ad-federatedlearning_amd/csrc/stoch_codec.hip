@@ -323,6 +323,8 @@ struct NormAcc {
 // (LINF) into its slot. Fixed assignment and order: deterministic.
 // Chunks from `keep_from` on are read with allocating loads, the rest non-temporally: the bucket's last
 // kKeepBytes stay in the 256 MiB Infinity Cache for the quantize pass, which walks the chunks in reverse.
+// A/B in the config bench (profiles/r01/stoch/keep_policy_ab.txt): 5% faster C3 encode than all
+// non-temporal, 1% at C2.
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_norm_partials(const float* __restrict__ x,
                                                           const adfl_slq_chunk* __restrict__ chunks,
@@ -348,7 +350,7 @@ __global__ __launch_bounds__(kBlock) void k_norm_partials(const float* __restric
   acc.flush(partials, blockIdx.x);
 }
 
-// Per-tensor finalize, two launches over the same table (every table entry is read by one thread, in
+// Per-tensor finalize, one launch in two roles over the same table (every table entry is read by one thread, in
 // parallel). Small tensors (<= kSmallChunks chunks): the thread that meets the first chunk sums the slots
 // itself. Large tensors: a 1024-thread block sums them with 16 independent accumulators per thread,
 // combined in a fixed tree. Both write norm = fp32 sqrt of the sum rounded once to fp32 (L2), or the
@@ -369,10 +371,9 @@ __device__ __forceinline__ void write_norm(const adfl_slq_chunk& c, double s, ui
 }
 
 template <int MODE>
-__global__ __launch_bounds__(kBlock) void k_norm_finalize_small(const adfl_slq_chunk* __restrict__ chunks,
-                                                                int64_t nchunks, const void* __restrict__ partials,
-                                                                float* __restrict__ norms, float* __restrict__ mins) {
-  const int64_t ci = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+__device__ __forceinline__ void finalize_small(const adfl_slq_chunk* __restrict__ chunks, int64_t nchunks,
+                                               const void* __restrict__ partials, float* __restrict__ norms,
+                                               float* __restrict__ mins, int64_t ci) {
   if (ci >= nchunks) return;
   const adfl_slq_chunk c = chunks[ci];
   if (c.first_chunk != ci || c.nchunks > kSmallChunks) return;
@@ -390,10 +391,17 @@ __global__ __launch_bounds__(kBlock) void k_norm_finalize_small(const adfl_slq_c
   write_norm<MODE>(c, s, mx, mn, norms, mins);
 }
 
+// One launch for both: blocks [0, nsmall) take the small tensors (one table entry per thread), blocks
+// [nsmall, ...) the large ones (a launch saved per encode; the empty role costs one table read).
 template <int MODE>
-__global__ __launch_bounds__(kBigBlock) void k_norm_finalize_big(const adfl_slq_chunk* __restrict__ chunks,
-                                                                 int64_t nchunks, const void* __restrict__ partials,
-                                                                 float* __restrict__ norms, float* __restrict__ mins) {
+__global__ __launch_bounds__(kBigBlock) void k_norm_finalize(const adfl_slq_chunk* __restrict__ chunks,
+                                                             int64_t nchunks, int64_t nsmall,
+                                                             const void* __restrict__ partials,
+                                                             float* __restrict__ norms, float* __restrict__ mins) {
+  if ((int64_t)blockIdx.x < nsmall) {
+    finalize_small<MODE>(chunks, nchunks, partials, norms, mins, (int64_t)blockIdx.x * kBigBlock + threadIdx.x);
+    return;
+  }
   constexpr int U = 16, W = kBigBlock / 64;
   __shared__ int64_t firsts[kBigBlock];
   __shared__ int nfirst;
@@ -401,7 +409,7 @@ __global__ __launch_bounds__(kBigBlock) void k_norm_finalize_big(const adfl_slq_
   __shared__ uint32_t red_mx[W], red_mn[W];
   if (threadIdx.x == 0) nfirst = 0;
   __syncthreads();
-  const int64_t me = (int64_t)blockIdx.x * kBigBlock + threadIdx.x;
+  const int64_t me = ((int64_t)blockIdx.x - nsmall) * kBigBlock + threadIdx.x;
   if (me < nchunks) {
     const adfl_slq_chunk c = chunks[me];
     if (c.first_chunk == me && c.nchunks > kSmallChunks) firsts[atomicAdd(&nfirst, 1)] = me;
@@ -689,11 +697,9 @@ inline int check_ws(const void* d_ws, int64_t bytes, int64_t nchunks) {
 template <int MODE>
 inline int launch_finalize(const adfl_slq_chunk* d_chunks, int64_t nchunks, const void* d_ws, float* d_norms,
                            float* d_mins, hipStream_t st) {
-  hipLaunchKernelGGL(k_norm_finalize_small<MODE>, dim3((unsigned)((nchunks + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                     st, d_chunks, nchunks, d_ws, d_norms, d_mins);
-  if (int s = launch_status()) return s;
-  hipLaunchKernelGGL(k_norm_finalize_big<MODE>, dim3((unsigned)((nchunks + kBigBlock - 1) / kBigBlock)),
-                     dim3(kBigBlock), 0, st, d_chunks, nchunks, d_ws, d_norms, d_mins);
+  const int64_t blocks = (nchunks + kBigBlock - 1) / kBigBlock;  // per role
+  hipLaunchKernelGGL(k_norm_finalize<MODE>, dim3((unsigned)(2 * blocks)), dim3(kBigBlock), 0, st, d_chunks, nchunks,
+                     blocks, d_ws, d_norms, d_mins);
   return launch_status();
 }
 

@@ -160,9 +160,13 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_v2(const int8_t* __restri
   }
 }
 
-__global__ void k_flush(uint4* p, int64_t n) {
+// Infinity-Cache flush by READING 512 MiB (clean junk lines; a write-based flush leaves dirty lines that
+// drain during the next measurement)
+__global__ void k_flush(const uint4* p, int64_t n) {
+  uint32_t a = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    p[i] = make_uint4(1, 2, 3, 4);
+    a ^= p[i].x;
+  if (a == 0x9e3779b9u) const_cast<uint4*>(p)[0].y = a;
 }
 }  // namespace
 
