@@ -80,6 +80,10 @@ def main():
             x = recipes.randn((31, 67), seed, mult)
             add_raw(f"randn_31x67_s{seed}_m{mult:g}_b{bits}", x, bits)
     add_raw("heavy_64x257_b8", recipes.heavy_tail((64, 257), 7, 1e-3), 8)
+    # every other bit width SLQChannel accepts (q_max = 2**(bits-1)-1: bits=1 -> q_max 0, scale inf;
+    # bits >= 9 -> q_max > 127, the int8 container clamps)
+    for bits in (1, 3, 5, 6, 7, 9, 12, 16):
+        add_raw(f"randn_33x31_s9_b{bits}", recipes.randn((33, 31), 9, 1e-3), bits)
     # C1: CPU 2-client small model, Examples/ray_async.py:63-70 ([10,3072] weight + [10] bias)
     add_raw("c1_fc_weight_b8", recipes.randn((10, 3072), 11, 0.02), 8)
 
@@ -112,6 +116,9 @@ def main():
     for name, x in edge.items():
         for bits in (8, 4, 2):
             add_raw(f"edge_{name}_b{bits}", x, bits, group="edge")
+    for name in ("ties", "zeros", "nan", "pinf", "ninf", "denormal_all", "tiny", "near_max"):
+        for bits in (1, 16):
+            add_raw(f"edge_{name}_b{bits}", edge[name], bits, group="edge")
 
     # ---- C. recipe-defined larger cases, stored as SHA-256 ---------------------------------------
     recipe_cases = [
