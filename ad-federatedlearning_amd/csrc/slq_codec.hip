@@ -320,11 +320,13 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_flat(const int8_t* __rest
 
 // int4 wave tile: 2048 elements = 8 coalesced 16-byte loads per lane -> 16 packed bytes per lane,
 // transposed through 1 KiB of LDS (lane l, load j packs float4 j*64+l into halfword j*64+l).
-__device__ __forceinline__ void quantize_tile_int4(const float4* __restrict__ xs, uint4* __restrict__ p16, float inv,
-                                                   uint16_t* __restrict__ lds, int lane) {
-  float4 v[8];
+__device__ __forceinline__ void load_tile_int4(const float4* __restrict__ xs, float4 (&v)[8], int lane) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) v[j] = load4<true>(xs + j * 64 + lane);
+}
+
+__device__ __forceinline__ void quantize_tile_int4_regs(const float4 (&v)[8], uint4* __restrict__ p16, float inv,
+                                                        uint16_t* __restrict__ lds, int lane) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) lds[j * 64 + lane] = (uint16_t)quant4_int4(v[j], inv);
   __builtin_amdgcn_wave_barrier();
@@ -352,16 +354,21 @@ __global__ __launch_bounds__(kBlock) void k_quantize_int4_flat(const float* __re
                                                                uint8_t* __restrict__ packed,
                                                                float* __restrict__ scale_out) {
   __shared__ __attribute__((aligned(16))) uint16_t lds[kWaves][kTile4 / 4];
-  const ScaleInv si = make_scale(reduce_partials(partials, (int)partials[kCountSlot]), qmax);
-  if (blockIdx.x == 0 && threadIdx.x == 0) *scale_out = si.scale;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const float4* x4 = reinterpret_cast<const float4*>(x);
   uint4* p16 = reinterpret_cast<uint4*>(packed);
   const int64_t ntiles = n / kTile4;
   const int64_t wstride = (int64_t)gridDim.x * kWaves;
-  for (int64_t t0 = (int64_t)blockIdx.x * kWaves + wave; t0 < ntiles; t0 += wstride) {
+  const int64_t first = (int64_t)blockIdx.x * kWaves + wave;
+  // the first tile's loads do not need the scale: issued before the partial reduction they hide
+  float4 v[8];
+  if (first < ntiles) load_tile_int4(x4 + (ntiles - 1 - first) * (kTile4 / 4), v, lane);
+  const ScaleInv si = make_scale(reduce_partials(partials, (int)partials[kCountSlot]), qmax);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *scale_out = si.scale;
+  for (int64_t t0 = first; t0 < ntiles; t0 += wstride) {
     const int64_t t = ntiles - 1 - t0;
-    quantize_tile_int4(x4 + t * (kTile4 / 4), p16 + t * 64, si.inv, lds[wave], lane);
+    if (t0 != first) load_tile_int4(x4 + t * (kTile4 / 4), v, lane);
+    quantize_tile_int4_regs(v, p16 + t * 64, si.inv, lds[wave], lane);
   }
   if (blockIdx.x == gridDim.x - 1) {
     const int64_t np = (n + 1) >> 1;
@@ -719,20 +726,23 @@ __global__ __launch_bounds__(kBlock) void k_quantize_batched_int4(const float* _
                                                                   const uint32_t* __restrict__ partials,
                                                                   uint8_t* __restrict__ packed,
                                                                   float* __restrict__ scales) {
+  static_assert(ADFL_SLQ_CHUNK_ELEMS == kTile4 * kWaves, "one int4 tile per wave per chunk");
   __shared__ __attribute__((aligned(16))) uint16_t lds[kWaves][kTile4 / 4];
   const int64_t ci = nchunks - 1 - (int64_t)blockIdx.x;
   const adfl_slq_chunk c = chunks[ci];
-  const ScaleInv si = make_scale(reduce_partials(partials + c.first_chunk, c.nchunks), qmax);
-  if (ci == c.first_chunk && threadIdx.x == 0) scales[c.tensor] = si.scale;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const float* xc = x + c.start;
   uint8_t* pc = packed + (c.start >> 1);
   const int head = chunk_head(c.start, c.len, 32);
-  quantize_pairs_int4(xc, pc, 0, head, c.len, si.inv);
   const int ntiles = (c.len - head) / kTile4;
-  for (int t = wave; t < ntiles; t += kWaves)
-    quantize_tile_int4(reinterpret_cast<const float4*>(xc + head) + t * (kTile4 / 4),
-                       reinterpret_cast<uint4*>(pc + (head >> 1)) + t * 64, si.inv, lds[wave], lane);
+  // the wave's tile is loaded before the partial reduction, whose latency it hides
+  float4 v[8];
+  if (wave < ntiles) load_tile_int4(reinterpret_cast<const float4*>(xc + head) + wave * (kTile4 / 4), v, lane);
+  const ScaleInv si = make_scale(reduce_partials(partials + c.first_chunk, c.nchunks), qmax);
+  if (ci == c.first_chunk && threadIdx.x == 0) scales[c.tensor] = si.scale;
+  quantize_pairs_int4(xc, pc, 0, head, c.len, si.inv);
+  if (wave < ntiles)
+    quantize_tile_int4_regs(v, reinterpret_cast<uint4*>(pc + (head >> 1)) + wave * 64, si.inv, lds[wave], lane);
   quantize_pairs_int4(xc, pc, head + ntiles * kTile4, c.len, c.len, si.inv);
 }
 

@@ -61,21 +61,21 @@ def seg_ms(evs, i, j):
     return sum(e[i].elapsed_time(e[j]) for e in evs) / len(evs)
 
 
-def mode_c3(args, world, rank, dev):
-    from adfl_amd import _lib, ops
-    lib = _lib.load()
-    sh = torch.cuda.current_stream(dev).cuda_stream
-    base, rem = divmod(RESNET18, 256)
-    sizes = [base + (1 if i < rem else 0) for i in range(256)]
-    lay = ops.BucketLayout(sizes)
+def c3_round_trip(lay, packed, args, world, rank, dev, lib, sh, junk):
+    """Device-resident encode + decode of one bucket (per-tensor scales), Infinity Cache warm and
+    flushed. packed: the int4 nibble layout (PackedSLQChannel's kernels, 13 B/element)."""
+    from adfl_amd import _lib
     g = torch.Generator(device=dev).manual_seed(rank)
     x = torch.randn(lay.total, device=dev, generator=g) * 1e-3
-    q = torch.empty(lay.total, dtype=torch.int8, device=dev)
+    q = torch.empty(lay.total // 2 if packed else lay.total, dtype=torch.int8, device=dev)
     scales = torch.empty(lay.ntensors, device=dev)
     partials = torch.empty(lay.nchunks, dtype=torch.int32, device=dev)
     out = torch.empty(lay.total, device=dev)
     chunks = lay.device_chunks(dev)
-    junk = torch.zeros(128 << 20, dtype=torch.float32, device=dev)
+    enc = lib.adfl_slq_encode_batched_int4 if packed else lib.adfl_slq_encode_batched
+    dec = lib.adfl_slq_dequantize_batched_int4 if packed else lib.adfl_slq_dequantize_batched
+    bits = 4 if packed else 8
+    n = int(lay.sizes.sum())
     res = {}
     for flush in (False, True):
         def step(ev):
@@ -84,23 +84,40 @@ def mode_c3(args, world, rank, dev):
                              # the codec's buffers, and no dirty lines drain during the timed region
             if ev is not None:
                 ev[0].record()
-            _lib.check(lib.adfl_slq_encode_batched(x.data_ptr(), chunks.data_ptr(), lay.nchunks, 8, q.data_ptr(),
-                                                   scales.data_ptr(), partials.data_ptr(), sh))
+            _lib.check(enc(x.data_ptr(), chunks.data_ptr(), lay.nchunks, bits, q.data_ptr(), scales.data_ptr(),
+                           partials.data_ptr(), sh))
             if ev is not None:
                 ev[1].record()
-            _lib.check(lib.adfl_slq_dequantize_batched(q.data_ptr(), chunks.data_ptr(), lay.nchunks,
-                                                       scales.data_ptr(), out.data_ptr(), sh))
+            _lib.check(dec(q.data_ptr(), chunks.data_ptr(), lay.nchunks, scales.data_ptr(), out.data_ptr(), sh))
             if ev is not None:
                 ev[2].record()
         _, evs = timed(step, args.steps, args.warmup, world, 3)
-        enc, dec = seg_ms(evs, 0, 1), seg_ms(evs, 1, 2)
-        gib = RESNET18 * 4 / GIB
+        e, d = seg_ms(evs, 0, 1), seg_ms(evs, 1, 2)
         res["flushed" if flush else "cache_resident"] = {
-            "encode_ms": round(enc, 4), "decode_ms": round(dec, 4), "round_trip_ms": round(enc + dec, 4),
-            "GiB_per_s": round(gib / ((enc + dec) * 1e-3), 1),
-            "hbm_frac": round(14 * RESNET18 / ((enc + dec) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+            "encode_ms": round(e, 4), "decode_ms": round(d, 4), "round_trip_ms": round(e + d, 4),
+            "GiB_per_s": round(n * 4 / GIB / ((e + d) * 1e-3), 1),
+            "hbm_frac": round((13 if packed else 14) * n / ((e + d) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    return res
+
+
+def mode_c3(args, world, rank, dev):
+    """C3: ResNet-18's 11,689,512 parameters in 256 tensors. The headline layout is equal sizes; the
+    log-uniform layout (64 .. 2.4 M elements, tests/golden/recipes.py) and the packed int4 variant are
+    reported beside it."""
+    sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
+    import recipes
+    from adfl_amd import _lib, ops
+    lib = _lib.load()
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    junk = torch.zeros(128 << 20, dtype=torch.float32, device=dev)
+    lay = ops.BucketLayout(recipes.bucket_sizes("equal"))
+    res = c3_round_trip(lay, False, args, world, rank, dev, lib, sh, junk)
+    lay_log = ops.BucketLayout(recipes.bucket_sizes("loguniform", 0))
     return {"metric": "C3 bucketed round trip, 11,689,512 fp32 in 256 tensors (per-tensor scales)", "unit": "GiB/s",
-            "value": res["flushed"]["GiB_per_s"], "launches_per_round_trip": 3, "chunks": lay.nchunks, **res}
+            "value": res["flushed"]["GiB_per_s"], "launches_per_round_trip": 3, "chunks": lay.nchunks, **res,
+            "loguniform_layout": {"chunks": lay_log.nchunks,
+                                  **c3_round_trip(lay_log, False, args, world, rank, dev, lib, sh, junk)},
+            "int4_packed": c3_round_trip(lay, True, args, world, rank, dev, lib, sh, junk)}
 
 
 def mode_c5_int4(args, world, rank, dev):
