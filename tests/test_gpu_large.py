@@ -16,7 +16,8 @@ BIN = os.path.join(REPO, "tools", "bigtest")
 
 
 def test_beyond_int32_element_count():
-    if not os.path.exists(BIN) or os.path.getmtime(BIN) < os.path.getmtime(BIN + ".hip"):
+    srcs = [BIN + ".hip", os.path.join(REPO, "ad-federatedlearning_amd", "csrc", "slq_codec.hip")]
+    if not os.path.exists(BIN) or os.path.getmtime(BIN) < max(os.path.getmtime(p) for p in srcs):
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
                         "-I", os.path.join(REPO, "include"), "-o", BIN, BIN + ".hip"], check=True, timeout=600)
     r = subprocess.run([BIN], capture_output=True, text=True, timeout=300)
