@@ -157,6 +157,58 @@ def _stage_in(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _DeviceSta
     return dev_buf
 
 
+def _piece_bounds(lay: ops.BucketLayout, a: int, b: int, offs: List[int]) -> Tuple[int, int]:
+    return offs[a], (offs[b] if b < len(offs) else lay.total)
+
+
+def _stage_out(dev_buf: torch.Tensor, lay: ops.BucketLayout, st: _DeviceStaging, key: str,
+               outs: List[torch.Tensor]) -> None:
+    """Copy the bucket `dev_buf` (on the device) into the per-tensor CPU storages `outs` (contiguous, owned
+    by the caller; tensor k at lay.offsets[k]): tensor-aligned pieces go D2H into a reused pinned staging
+    buffer, and each piece is scattered into its tensors by the native pool as soon as its copy lands,
+    while the copy engine moves the next piece."""
+    host = st.buf(key + "_host", lay.total, dev_buf.dtype, pinned=True)
+    stream = torch.cuda.current_stream(st.device)
+    offs = lay.offsets.tolist()
+    pieces = _pieces(lay, host.element_size())
+    events = []
+    for a, b in pieces:
+        lo, hi = _piece_bounds(lay, a, b, offs)
+        host[lo:hi].copy_(dev_buf[lo:hi], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        events.append(ev)
+    for (a, b), ev in zip(pieces, events):
+        ev.synchronize()
+        hostcopy.scatter(host, outs[a:b], offs[a:b])
+
+
+def _hand_out(out_dev: torch.Tensor, lay: ops.BucketLayout, shapes: List[torch.Size], on_cpu: List[bool],
+              st: _DeviceStaging, key: str) -> List[torch.Tensor]:
+    """Decoded tensors as the reference returns them (quant.py:107-112): one new, owned, writable tensor
+    per entry — pageable CPU tensors for CPU payloads, device tensors for device payloads — never views
+    of a shared bucket (a strategy keeps single updates alive, Src/ADFL/Strategy/fed_buff.py:75,90, and
+    pickling one must not ship the whole bucket)."""
+    outs: List[Optional[torch.Tensor]] = [None] * len(shapes)
+    if any(on_cpu):
+        host_outs = [torch.empty(s, dtype=out_dev.dtype) for s in shapes]
+        if all(on_cpu):
+            _stage_out(out_dev, lay, st, key, host_outs)
+        else:  # mixed host / device dict (rare): per-tensor copies
+            for i, (off, n) in enumerate(zip(lay.offsets.tolist(), lay.sizes.tolist())):
+                if on_cpu[i]:
+                    host_outs[i].view(-1).copy_(out_dev[off:off + n])
+        for i, cpu in enumerate(on_cpu):
+            if cpu:
+                outs[i] = host_outs[i]
+    if not all(on_cpu):
+        for i, (off, n, s) in enumerate(zip(lay.offsets.tolist(), lay.sizes.tolist(), shapes)):
+            if not on_cpu[i]:
+                outs[i] = out_dev[off:off + n].view(s).clone()
+        torch.cuda.current_stream(st.device).synchronize()
+    return outs
+
+
 @_serialized
 def _encode_dict(params: Parameters, names: List[str], bits: int, stats: Optional[list] = None):
     """Encode the ndim>1 tensors `names` of `params` in one bucketed pass.
@@ -175,20 +227,23 @@ def _encode_dict(params: Parameters, names: List[str], bits: int, stats: Optiona
         stats.extend(ops.qerror_batched(x_dev, q_dev, s_dev, lay))
     scales_host = st.buf("scales_host", lay.ntensors, torch.float32, pinned=True)
     scales_host.copy_(s_dev, non_blocking=True)
-    on_cpu = [not t.is_cuda for t in tensors]
-    if any(on_cpu):
-        q_host = st.buf("q_host", lay.total, torch.int8, pinned=True)
-        q_host.copy_(q_dev, non_blocking=True)
     torch.cuda.current_stream(dev).synchronize()
     scales = scales_host.tolist()
-    padded = lay.padded.tolist()
-    parts_host = torch.split(q_host, padded) if any(on_cpu) else None
-    parts_dev = torch.split(q_dev, padded) if not all(on_cpu) else None
+    on_cpu = [not t.is_cuda for t in tensors]
+    if all(on_cpu):
+        # every payload tensor owns its bytes (compact pickles; the staging buffer is reused by the next
+        # call): empty qint8 tensors filled by the pipelined D2H + native scatter
+        qs = [torch._empty_affine_quantized(t.shape, scale=sc, zero_point=0, dtype=torch.qint8)
+              for t, sc in zip(tensors, scales)]
+        _stage_out(q_dev, lay, st, "q", qs)
+        return {name: (qt, sc) for name, qt, sc in zip(names, qs, scales)}
     out = {}
-    for i, (name, t, n, cpu) in enumerate(zip(names, tensors, lay.sizes.tolist(), on_cpu)):
-        src = (parts_host if cpu else parts_dev)[i][:n].view(t.shape)
-        # _make_per_tensor_quantized_tensor copies into a fresh qint8 storage: every payload tensor owns
-        # its bytes (compact pickles; the staging buffer is reused by the next call).
+    offs, sizes = lay.offsets.tolist(), lay.sizes.tolist()
+    for i, (name, t) in enumerate(zip(names, tensors)):
+        src = q_dev[offs[i]:offs[i] + sizes[i]].view(t.shape)
+        if on_cpu[i]:
+            src = src.cpu()
+        # _make_per_tensor_quantized_tensor copies into a fresh qint8 storage of the source's device
         out[name] = (torch._make_per_tensor_quantized_tensor(src, scales[i], 0), scales[i])
     return out
 
@@ -215,18 +270,9 @@ def _decode_dict(items: List[Tuple[str, torch.Tensor]]) -> Dict[str, torch.Tenso
     # q_scale() is a double; fbgemm's dequantize uses it as fp32 (quant.py:110), so round it the same way
     s_dev = torch.tensor([q.q_scale() for _, q in items], dtype=torch.float32).to(dev, non_blocking=True)
     on_cpu = [not q.is_cuda for _, q in items]
-    # fresh outputs (the caching allocators make this cheap): decoded tensors are handed to the caller,
-    # owned and writable; strategies mutate them in place (Src/ADFL/Strategy/fed_buff.py:75,90)
-    out_dev = ops.decode_batched(q_dev, s_dev, lay, out=torch.empty(lay.total, dtype=torch.float32, device=dev))
-    if any(on_cpu):
-        out_host = torch.empty(lay.total, dtype=torch.float32, pin_memory=True)
-        out_host.copy_(out_dev, non_blocking=True)
-    torch.cuda.current_stream(dev).synchronize()
-    padded = lay.padded.tolist()
-    parts_host = torch.split(out_host, padded) if any(on_cpu) else None
-    parts_dev = torch.split(out_dev, padded) if not all(on_cpu) else None
-    return {name: (parts_host if cpu else parts_dev)[i][:n].view(q.shape)
-            for i, ((name, q), n, cpu) in enumerate(zip(items, lay.sizes.tolist(), on_cpu))}
+    out_dev = ops.decode_batched(q_dev, s_dev, lay, out=st.buf("d_out", lay.total, torch.float32))
+    decoded = _hand_out(out_dev, lay, [q.shape for _, q in items], on_cpu, st, "d_out")
+    return {name: t for (name, _), t in zip(items, decoded)}
 
 
 @_serialized
@@ -243,11 +289,14 @@ def _decode_add(c_params: QuantParameters, names: List[str], targets: List[Param
     s_dev = torch.tensor([q.q_scale() for q in qs], dtype=torch.float32).to(dev, non_blocking=True)
     with torch.no_grad():
         ops.dequantize_add_batched(q_dev, s_dev, lay, [[t[n] for n in names] for t in targets])
+    # the next call's host gather rewrites the pinned staging this call's H2D reads from
+    torch.cuda.current_stream(dev).synchronize()
 
 
 @_serialized
-def _encode_dict_packed(params: Parameters, names: List[str], bits: int):
-    """Packed int4 variant of _encode_dict: {name: (int8 tensor of ceil(n/2) packed bytes, scale)}."""
+def _encode_dict_packed(params: Parameters, names: List[str], bits: int, stats: Optional[list] = None):
+    """Packed int4 variant of _encode_dict: {name: (int8 tensor of ceil(n/2) packed bytes, scale)}; with
+    `stats`, the bucket's four q-error sums against its packed payload are appended."""
     st = _staging()
     dev = st.device
     tensors = [params[n] for n in names]
@@ -256,20 +305,19 @@ def _encode_dict_packed(params: Parameters, names: List[str], bits: int):
     p_dev, s_dev = ops.encode_batched_int4(x_dev, lay, bits, packed=st.buf("p", lay.total // 2, torch.uint8),
                                            scales=st.buf("scales", lay.ntensors, torch.float32),
                                            partials=st.buf("partials", lay.nchunks, torch.int32))
+    if stats is not None:
+        stats.extend(ops.qerror_batched_int4(x_dev, p_dev, s_dev, lay))
     scales_host = st.buf("scales_host", lay.ntensors, torch.float32, pinned=True)
     scales_host.copy_(s_dev, non_blocking=True)
-    on_cpu = [not t.is_cuda for t in tensors]
-    if any(on_cpu):
-        p_host = st.buf("p_host", lay.total // 2, torch.uint8, pinned=True)
-        p_host.copy_(p_dev, non_blocking=True)
     torch.cuda.current_stream(dev).synchronize()
     scales = scales_host.tolist()
-    half = (lay.padded // 2).tolist()
-    parts_host = torch.split(p_host, half) if any(on_cpu) else None
-    parts_dev = torch.split(p_dev, half) if not all(on_cpu) else None
+    on_cpu = [not t.is_cuda for t in tensors]
+    # packed-byte layout: with align=2 tensor k's ceil(n/2) bytes sit at offsets[k] / 2
+    p_lay = st.layout(tuple(int(n) // 2 for n in lay.padded.tolist()), align=1)
+    shapes = [torch.Size([(int(t.numel()) + 1) // 2]) for t in tensors]
     # int8, as compression.py:pack_4bit returns; each tensor owns its bytes (the staging is reused)
-    return {name: ((parts_host if cpu else parts_dev)[i].clone().view(torch.int8), scales[i])
-            for i, (name, cpu) in enumerate(zip(names, on_cpu))}
+    parts = _hand_out(p_dev.view(torch.int8), p_lay, shapes, on_cpu, st, "p")
+    return {name: (pt, sc) for name, pt, sc in zip(names, parts, scales)}
 
 
 @_serialized
@@ -287,16 +335,9 @@ def _decode_dict_packed(items: List[Tuple[str, torch.Tensor, torch.Size, float]]
     p_dev = _stage_in([p.view(torch.uint8) for _, p, _, _ in items], p_lay, st, "dp", torch.uint8)
     s_dev = torch.tensor([s for _, _, _, s in items], dtype=torch.float32).to(dev, non_blocking=True)
     on_cpu = [not p.is_cuda for _, p, _, _ in items]
-    out_dev = ops.decode_batched_int4(p_dev, s_dev, lay, out=torch.empty(lay.total, dtype=torch.float32, device=dev))
-    if any(on_cpu):
-        out_host = torch.empty(lay.total, dtype=torch.float32, pin_memory=True)
-        out_host.copy_(out_dev, non_blocking=True)
-    torch.cuda.current_stream(dev).synchronize()
-    padded = lay.padded.tolist()
-    parts_host = torch.split(out_host, padded) if any(on_cpu) else None
-    parts_dev = torch.split(out_dev, padded) if not all(on_cpu) else None
-    return {name: (parts_host if cpu else parts_dev)[i][:n].view(shape)
-            for i, ((name, _, shape, _), n, cpu) in enumerate(zip(items, sizes, on_cpu))}
+    out_dev = ops.decode_batched_int4(p_dev, s_dev, lay, out=st.buf("d_out", lay.total, torch.float32))
+    decoded = _hand_out(out_dev, lay, [torch.Size(shape) for _, _, shape, _ in items], on_cpu, st, "d_out")
+    return {name: t for (name, _, _, _), t in zip(items, decoded)}
 
 
 class SLQChannel(Channel):
@@ -462,11 +503,11 @@ class PackedSLQChannel(SLQChannel):
         params = {name: decoded[name] if name in decoded else p.data.data for name, p in c_params.params.items()}
         return params, time.perf_counter() - s_time
 
-    def _quantize_params(self, params: Parameters, bits: int) -> QuantParameters:
+    def _quantize_params(self, params: Parameters, bits: int, stats: Optional[list] = None) -> QuantParameters:
         names = [name for name, p in params.items() if p.ndim > 1]
         for name in names:
             ops.require_quantizable(params[name])
-        encoded = _encode_dict_packed(params, names, bits) if names else {}
+        encoded = _encode_dict_packed(params, names, bits, stats) if names else {}
         q_params = QuantParameters({}, 0)
         for name, param in params.items():
             q_param, scale = encoded[name] if name in encoded else (param, 1)

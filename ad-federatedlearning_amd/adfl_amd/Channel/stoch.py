@@ -34,7 +34,7 @@ from .. import hostcopy
 from .. import stoch as sops
 from ..model import CompressedParameters, Parameters, QuantParameter, QuantParameters, get_parameter_info
 from .channel import Channel, IdentityChannel
-from .quant import _serialized, _stage_in, _staging
+from .quant import _hand_out, _serialized, _stage_in, _staging
 
 _CODECS = ("qsgd", "rqsgd", "cnat")
 
@@ -133,7 +133,7 @@ def _decode_stoch(items: List[Tuple[str, QuantParameter]], codec: str, bits: int
     ntens = len(items)
     sc = torch.tensor(scales + ([float(p.scale_2) for _, p in items] if codec == "rqsgd" else []),
                       dtype=torch.float32).to(dev, non_blocking=True)
-    out_dev = torch.empty(lay.total, dtype=torch.float32, device=dev)
+    out_dev = st.buf("d_out", lay.total, torch.float32)
     if codec == "qsgd":
         sops.qsgd_decode_batched(lv_dev, sg_dev, sc[:ntens], lay, bits, out=out_dev)
     elif codec == "rqsgd":
@@ -141,15 +141,8 @@ def _decode_stoch(items: List[Tuple[str, QuantParameter]], codec: str, bits: int
     else:
         sops.cnat_decode_batched(lv_dev.view(torch.int8), sg_dev, sc[:ntens], lay, out=out_dev)
     on_cpu = [not p.data.is_cuda for _, p in items]
-    if any(on_cpu):
-        out_host = torch.empty(lay.total, dtype=torch.float32, pin_memory=True)
-        out_host.copy_(out_dev, non_blocking=True)
-    torch.cuda.current_stream(dev).synchronize()
-    padded = lay.padded.tolist()
-    parts_host = torch.split(out_host, padded) if any(on_cpu) else None
-    parts_dev = torch.split(out_dev, padded) if not all(on_cpu) else None
-    return {name: (parts_host if cpu else parts_dev)[i][:p.data.numel()].view(p.data.shape)
-            for i, ((name, p), cpu) in enumerate(zip(items, on_cpu))}
+    decoded = _hand_out(out_dev, lay, [p.data.shape for _, p in items], on_cpu, st, "d_out")
+    return {name: t for (name, _), t in zip(items, decoded)}
 
 
 class _StochChannel(Channel):

@@ -47,6 +47,7 @@ SIGNATURES = {
     "adfl_slq_encode_batched": (INT, [P, P, I64, INT, P, P, P, P]),
     "adfl_slq_dequantize_batched": (INT, [P, P, I64, P, P, P]),
     "adfl_slq_qerror_batched": (INT, [P, P, P, I64, P, P, P]),
+    "adfl_slq_qerror_batched_int4": (INT, [P, P, P, I64, P, P, P]),
     "adfl_slq_encode_batched_int4": (INT, [P, P, I64, INT, P, P, P, P]),
     "adfl_slq_dequantize_batched_int4": (INT, [P, P, I64, P, P, P]),
     "adfl_slq_quantize_int4": (INT, [P, I64, INT, P, P, P, P]),
@@ -56,6 +57,8 @@ SIGNATURES = {
     "adfl_unpack_int4": (INT, [P, I64, P, P]),
     "adfl_slq_dequantize_mean": (INT, [P, I64, I32, I64, P, I64, P, P]),
     "adfl_slq_dequantize_mean_int4": (INT, [P, I64, I32, I64, P, I64, P, P]),
+    "adfl_slq_dequantize_mean_self": (INT, [P, I64, I32, I64, P, I64, I32, P, P, P]),
+    "adfl_slq_dequantize_mean_self_int4": (INT, [P, I64, I32, I64, P, I64, I32, P, P, P]),
     "adfl_slq_dequantize_add_batched": (INT, [P, P, I64, P, P, I32, I32, P]),
     # adfl_stoch.h
     "adfl_stoch_workspace_bytes": (I64, [I64]),

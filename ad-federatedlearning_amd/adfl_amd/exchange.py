@@ -9,8 +9,18 @@ fp32 tensors pickled through Ray's object store. Here each rank is one client on
                                       ->  fused decode + mean of the K payloads (one HIP launch)
 
 Message layout (one row per chunk per rank, 16-byte aligned): ``payload | pad to 16 | fp32 scale | pad``.
-The scale rides in the row, so one all-gather moves payloads and scales together. The mean sums the K
-decoded payloads in rank order, fp32, then divides by K (the oracle's ``dequantize_mean``).
+The scale rides in the row, so one all-gather moves payloads and scales together.
+
+The mean (``exact_self=True``, the default) is the reference's: the peers' decoded updates in rank order,
+then the rank's OWN update exactly as it is (fp32, not quantized: async_peer.py:170-174 and
+ray_ad.py:183-188 append the local parameters after the received ones), fp32 sum, then / K (the oracle's
+``dequantize_mean_self``). ``exact_self=False`` averages the K decoded payloads, own row included, in rank
+order (``dequantize_mean``), so every rank ends with the bit-identical mean.
+
+Transport: RCCL (``nccl`` backend) all-gathers device rows directly over xGMI. With any other backend
+(gloo) on a GPU — e.g. two simulated clients sharing one GPU, the reference's ``NUM_GPUS = 0.5`` packing
+(``Examples/ray_ad.py:29``), which RCCL cannot form because it needs distinct devices per rank — each row
+is staged through pinned host memory: D2H, gloo all-gather, H2D.
 
 With ``chunks > 1`` (the C5 4 GiB/client int4 variant) the absmax pass runs over the whole update first
 (the scale needs the global max), then chunk c is quantized while chunk c-1's all-gather is in flight:
@@ -54,11 +64,27 @@ class HipCodec:
         fn = self.lib.adfl_slq_quantize_int4 if packed else self.lib.adfl_slq_quantize
         check(fn(x.data_ptr(), x.numel(), bits, self.ws.data_ptr(), row.data_ptr(), scale_ptr, self._stream()))
 
-    def mean(self, rows: torch.Tensor, n: int, packed: bool, payload_bytes: int, out: torch.Tensor) -> None:
+    def mean(self, rows: torch.Tensor, n: int, packed: bool, payload_bytes: int, out: torch.Tensor,
+             self_row: int = -1, self_x: Optional[torch.Tensor] = None) -> None:
         k, row_bytes = rows.shape
         scales = rows.data_ptr() + _pad16(payload_bytes)
-        fn = self.lib.adfl_slq_dequantize_mean_int4 if packed else self.lib.adfl_slq_dequantize_mean
-        check(fn(rows.data_ptr(), row_bytes, k, n, scales, row_bytes // 4, out.data_ptr(), self._stream()))
+        fn = self.lib.adfl_slq_dequantize_mean_self_int4 if packed else self.lib.adfl_slq_dequantize_mean_self
+        xp = self_x.data_ptr() if self_row >= 0 else None
+        check(fn(rows.data_ptr(), row_bytes, k, n, scales, row_bytes // 4, self_row, xp, out.data_ptr(),
+                 self._stream()))
+
+
+class _StagedGather:
+    """A pending host-staged all-gather: wait() finishes the gloo collective, then copies the gathered
+    rows to the device on the current stream (ordered before the mean kernel)."""
+
+    def __init__(self, work, host: torch.Tensor, dev: torch.Tensor):
+        self.work, self.host, self.dev = work, host, dev
+
+    def wait(self):
+        self.work.wait()
+        self.dev.copy_(self.host)
+        return True
 
 
 class PeerExchange:
@@ -70,10 +96,13 @@ class PeerExchange:
     """
 
     def __init__(self, numel: int, bits: int = 8, packed: bool = False, chunks: int = 1,
-                 group: Optional[dist.ProcessGroup] = None, device: Optional[torch.device] = None, codec=None):
+                 group: Optional[dist.ProcessGroup] = None, device: Optional[torch.device] = None, codec=None,
+                 exact_self: bool = True):
         if numel < 1 or chunks < 1:
             raise ValueError("PeerExchange: numel and chunks must be >= 1")
         self.numel, self.bits, self.packed, self.group = numel, bits, packed, group
+        self.exact_self = exact_self
+        self._x: Optional[torch.Tensor] = None
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         if device is None:
@@ -88,6 +117,12 @@ class PeerExchange:
         self.row_bytes = [_pad16(p) + 16 for p in self.payload]
         self.local = [torch.empty(rb, dtype=torch.uint8, device=device) for rb in self.row_bytes]
         self.gathered = [torch.empty(self.world, rb, dtype=torch.uint8, device=device) for rb in self.row_bytes]
+        # device rows over a host-only backend (gloo): stage each row through pinned host memory
+        self.host_staged = device.type == "cuda" and dist.get_backend(group) != "nccl"
+        if self.host_staged:
+            self.local_host = [torch.empty(rb, dtype=torch.uint8, pin_memory=True) for rb in self.row_bytes]
+            self.gathered_host = [torch.empty(self.world, rb, dtype=torch.uint8, pin_memory=True)
+                                  for rb in self.row_bytes]
 
     def _payload_bytes(self, n: int) -> int:
         return (n + 1) // 2 if self.packed else n
@@ -103,21 +138,30 @@ class PeerExchange:
         if x.numel() != self.numel or x.dtype != torch.float32:
             raise ValueError(f"PeerExchange: expected {self.numel} fp32 elements, got {x.numel()} {x.dtype}")
         x = x.reshape(-1)
+        self._x = x
         self.codec.absmax(x)
         works = []
-        for (c0, c1), row, out, pb in zip(self.bounds, self.local, self.gathered, self.payload):
+        for c, ((c0, c1), row, out, pb) in enumerate(zip(self.bounds, self.local, self.gathered, self.payload)):
             self.codec.quantize(x[c0:c1], self.bits, self.packed, row, pb)
-            works.append(dist.all_gather_into_tensor(out.view(-1), row, group=self.group, async_op=True))
+            if self.host_staged:
+                lh, gh = self.local_host[c], self.gathered_host[c]
+                lh.copy_(row)  # blocking D2H: also orders after the previous step's H2D from gh
+                w = dist.all_gather_into_tensor(gh.view(-1), lh, group=self.group, async_op=True)
+                works.append(_StagedGather(w, gh, out))
+            else:
+                works.append(dist.all_gather_into_tensor(out.view(-1), row, group=self.group, async_op=True))
         return works
 
     def mean(self, works: List, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Wait for each chunk's all-gather and decode the K payloads into their fp32 mean (a `None` work
         is a chunk whose collective the caller has already waited on)."""
         out = torch.empty(self.numel, dtype=torch.float32, device=self.device) if out is None else out
+        self_row = self.rank if self.exact_self else -1
         for (c0, c1), rows, pb, w in zip(self.bounds, self.gathered, self.payload, works):
             if w is not None:
                 w.wait()
-            self.codec.mean(rows, c1 - c0, self.packed, pb, out[c0:c1])
+            self.codec.mean(rows, c1 - c0, self.packed, pb, out[c0:c1], self_row,
+                            self._x[c0:c1] if self_row >= 0 else None)
         return out
 
     def exchange_mean(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -129,16 +129,24 @@ def unpack_int4(packed: torch.Tensor, shape: Sequence[int]) -> torch.Tensor:
 
 
 def dequantize_mean(q_rows: torch.Tensor, scales: torch.Tensor, n: int, *,
-                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                    out: Optional[torch.Tensor] = None, self_row: int = -1,
+                    self_x: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Mean over K int8 payload rows (Examples/ray_ad.py:188): q_rows is [K, row_bytes] int8 (row_bytes >= n,
-    16-byte multiple), scales is [K] or [K, stride] fp32 (column 0 used)."""
+    16-byte multiple), scales is [K] or [K, stride] fp32 (column 0 used). With self_row >= 0 that row is
+    replaced by the receiver's own fp32 update self_x, added last and exactly (async_peer.py:170-174)."""
     if q_rows.dim() != 2 or q_rows.dtype != torch.int8 or not q_rows.is_contiguous():
         raise ValueError("dequantize_mean: q_rows must be a contiguous [K, row_bytes] int8 tensor")
     k, row = q_rows.shape
     sc = scales.reshape(k, -1)
+    xp = None
+    if self_row >= 0:
+        self_x = _dev(self_x, "self_x")
+        if self_x.dtype != torch.float32 or self_x.numel() != n or not self_x.is_contiguous():
+            raise ValueError("dequantize_mean: self_x must be a contiguous fp32 tensor of n elements")
+        xp = self_x.data_ptr()
     out = torch.empty(n, dtype=torch.float32, device=q_rows.device) if out is None else out
-    check(_lib.load().adfl_slq_dequantize_mean(q_rows.data_ptr(), row, k, n, sc.data_ptr(), sc.stride(0),
-                                               out.data_ptr(), _stream(q_rows.device)))
+    check(_lib.load().adfl_slq_dequantize_mean_self(q_rows.data_ptr(), row, k, n, sc.data_ptr(), sc.stride(0),
+                                                    self_row, xp, out.data_ptr(), _stream(q_rows.device)))
     return out
 
 
@@ -228,6 +236,20 @@ def qerror_batched(flat: torch.Tensor, q: torch.Tensor, scales: torch.Tensor,
     check(_lib.load().adfl_slq_qerror_batched(flat.data_ptr(), q.data_ptr(), layout.device_chunks(dev).data_ptr(),
                                               layout.nchunks, scales.data_ptr(), partials.data_ptr(),
                                               _stream(dev)))
+    return tuple(partials.view(-1, 4).sum(0).tolist())
+
+
+def qerror_batched_int4(flat: torch.Tensor, packed: torch.Tensor, scales: torch.Tensor,
+                        layout: BucketLayout) -> Tuple[float, float, float, float]:
+    """qerror_batched against an int4-packed bucket (layout offsets even; encode_batched_int4's payload)."""
+    flat, packed = _dev(flat, "flat"), _dev(packed, "packed")
+    if (layout.offsets % 2).any():
+        raise ValueError("qerror_batched_int4: tensor offsets must be even (an int4 bucket layout)")
+    dev = flat.device
+    partials = torch.empty(layout.nchunks * 4, dtype=torch.float64, device=dev)
+    check(_lib.load().adfl_slq_qerror_batched_int4(flat.data_ptr(), packed.data_ptr(),
+                                                   layout.device_chunks(dev).data_ptr(), layout.nchunks,
+                                                   scales.data_ptr(), partials.data_ptr(), _stream(dev)))
     return tuple(partials.view(-1, 4).sum(0).tolist())
 
 

@@ -424,9 +424,13 @@ __global__ __launch_bounds__(kBlock) void k_unpack_int4(const uint8_t* __restric
 
 // Peer-exchange epilogue: mean of K dequantized int8 rows, rows summed in order (fp32), then / K.
 // Per row: one coalesced 16-byte load per lane + LDS transpose; output: coalesced NT float4 stores.
+// self_row >= 0: that row is skipped and the rank's own fp32 update self_x is added LAST instead, exactly
+// (async_peer.py:170-174 / ray_ad.py:183-188 append the local parameters after the received updates).
 __global__ __launch_bounds__(kBlock) void k_dequantize_mean(const int8_t* __restrict__ q, int64_t row_stride, int k,
                                                             int64_t n, const float* __restrict__ scales,
-                                                            int64_t scale_stride, float* __restrict__ out) {
+                                                            int64_t scale_stride, int self_row,
+                                                            const float* __restrict__ self_x,
+                                                            float* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kWaves][kTile / 4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t ntiles = n / kTile;
@@ -434,7 +438,9 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_mean(const int8_t* __rest
   const double dk = (double)k;
   for (int64_t t = (int64_t)blockIdx.x * kWaves + wave; t < ntiles; t += wstride) {
     float4 acc[4];
+    bool first = true;
     for (int r = 0; r < k; ++r) {
+      if (r == self_row) continue;
       const uint4* q16 = reinterpret_cast<const uint4*>(q + r * row_stride) + t * (kTile / 16);
       const float s = scales[r * scale_stride];
       reinterpret_cast<uint4*>(lds[wave])[lane] = q16[lane];
@@ -442,9 +448,18 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_mean(const int8_t* __rest
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float4 v = dequant4(lds[wave][j * 64 + lane], s);
-        acc[j] = (r == 0) ? v : add4(acc[j], v);
+        acc[j] = first ? v : add4(acc[j], v);
       }
       __builtin_amdgcn_wave_barrier();
+      first = false;
+    }
+    if (self_row >= 0) {
+      const float4* xs = reinterpret_cast<const float4*>(self_x) + t * (kTile / 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float4 v = xs[j * 64 + lane];
+        acc[j] = first ? v : add4(acc[j], v);
+      }
     }
     float4* o4 = reinterpret_cast<float4*>(out) + t * (kTile / 4);
 #pragma unroll
@@ -452,8 +467,15 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_mean(const int8_t* __rest
   }
   if (blockIdx.x == gridDim.x - 1)
     for (int64_t i = ntiles * kTile + threadIdx.x; i < n; i += kBlock) {
-      float acc = scales[0] * (float)q[i];
-      for (int r = 1; r < k; ++r) acc += scales[r * scale_stride] * (float)q[r * row_stride + i];
+      float acc = 0.0f;
+      bool first = true;
+      for (int r = 0; r < k; ++r) {
+        if (r == self_row) continue;
+        const float d = scales[r * scale_stride] * (float)q[r * row_stride + i];
+        acc = first ? d : acc + d;
+        first = false;
+      }
+      if (self_row >= 0) acc = first ? self_x[i] : acc + self_x[i];
       out[i] = (float)((double)acc / dk);
     }
 }
@@ -461,7 +483,9 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_mean(const int8_t* __rest
 // Same over K int4-packed rows (2048-element wave tiles, 1 KiB of packed bytes per row per tile).
 __global__ __launch_bounds__(kBlock) void k_dequantize_mean_int4(const uint8_t* __restrict__ p, int64_t row_stride,
                                                                  int k, int64_t n, const float* __restrict__ scales,
-                                                                 int64_t scale_stride, float* __restrict__ out) {
+                                                                 int64_t scale_stride, int self_row,
+                                                                 const float* __restrict__ self_x,
+                                                                 float* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint16_t lds[kWaves][kTile4 / 4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t ntiles = n / kTile4;
@@ -469,7 +493,9 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_mean_int4(const uint8_t* 
   const double dk = (double)k;
   for (int64_t t = (int64_t)blockIdx.x * kWaves + wave; t < ntiles; t += wstride) {
     float4 acc[8];
+    bool first = true;
     for (int r = 0; r < k; ++r) {
+      if (r == self_row) continue;
       const uint4* p16 = reinterpret_cast<const uint4*>(p + r * row_stride) + t * 64;
       const float s = scales[r * scale_stride];
       reinterpret_cast<uint4*>(lds[wave])[lane] = p16[lane];
@@ -477,9 +503,18 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_mean_int4(const uint8_t* 
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float4 v = dequant2_int4(lds[wave][j * 64 + lane], s);
-        acc[j] = (r == 0) ? v : add4(acc[j], v);
+        acc[j] = first ? v : add4(acc[j], v);
       }
       __builtin_amdgcn_wave_barrier();
+      first = false;
+    }
+    if (self_row >= 0) {
+      const float4* xs = reinterpret_cast<const float4*>(self_x) + t * (kTile4 / 4);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float4 v = xs[j * 64 + lane];
+        acc[j] = first ? v : add4(acc[j], v);
+      }
     }
     float4* o4 = reinterpret_cast<float4*>(out) + t * (kTile4 / 4);
 #pragma unroll
@@ -488,11 +523,16 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_mean_int4(const uint8_t* 
   if (blockIdx.x == gridDim.x - 1)
     for (int64_t i = ntiles * kTile4 + threadIdx.x; i < n; i += kBlock) {
       float acc = 0.0f;
+      bool first = true;
       for (int r = 0; r < k; ++r) {
+        if (r == self_row) continue;
         float e0, e1;
         dequant_byte_int4(p[r * row_stride + (i >> 1)], scales[r * scale_stride], e0, e1);
-        acc = (r == 0) ? ((i & 1) ? e1 : e0) : acc + ((i & 1) ? e1 : e0);
+        const float d = (i & 1) ? e1 : e0;
+        acc = first ? d : acc + d;
+        first = false;
       }
+      if (self_row >= 0) acc = first ? self_x[i] : acc + self_x[i];
       out[i] = (float)((double)acc / dk);
     }
 }
@@ -665,6 +705,9 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_add_batched(const int8_t*
 // Quantization-error statistics of a bucket against its own payload (worker.py:186-189 computes
 // parameter_relative_mse and parameter_cosine_similarity from a full decode; here they are four sums
 // per chunk, fp64): S0 = sum (x - s*q)^2, S1 = sum x^2, S2 = sum x*(s*q), S3 = sum (s*q)^2.
+// PACKED: q is an int4 bucket (pack_4bit layout, even tensor offsets): element e's code is the high
+// (even e) or low (odd e) nibble of byte e/2, minus 8 — what unpack_4bit hands the dequantize.
+template <bool PACKED>
 __global__ __launch_bounds__(kBlock) void k_qerror_batched(const float* __restrict__ x, const int8_t* __restrict__ q,
                                                            const adfl_slq_chunk* __restrict__ chunks,
                                                            const float* __restrict__ scales,
@@ -673,11 +716,18 @@ __global__ __launch_bounds__(kBlock) void k_qerror_batched(const float* __restri
   const adfl_slq_chunk c = chunks[blockIdx.x];
   const float s = scales[c.tensor];
   const float* xc = x + c.start;
-  const int8_t* qc = q + c.start;
   double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
   for (int i = threadIdx.x; i < c.len; i += kBlock) {
     const double xv = xc[i];
-    const double dv = (double)(s * (float)qc[i]);  // the dequantized fp32 value the reference compares
+    int code;
+    if (PACKED) {
+      const int64_t e = c.start + i;
+      const uint32_t b = reinterpret_cast<const uint8_t*>(q)[e >> 1];
+      code = (e & 1) ? (int)(b & 0xfu) - 8 : (int)((b >> 4) & 0xfu) - 8;
+    } else {
+      code = q[c.start + i];
+    }
+    const double dv = (double)(s * (float)code);  // the dequantized fp32 value the reference compares
     const double e = (double)(xc[i] - (float)dv);  // fp32 difference, as (a - b) in parameter_mse
     a0 += e * e;
     a1 += xv * xv;
@@ -893,8 +943,17 @@ int adfl_slq_dequantize_batched(const int8_t* d_q, const adfl_slq_chunk* d_chunk
 int adfl_slq_qerror_batched(const float* d_x, const int8_t* d_q, const adfl_slq_chunk* d_chunks, int64_t nchunks,
                             const float* d_scales, double* d_partials, void* stream) {
   if (!d_x || !d_q || !d_chunks || !d_scales || !d_partials || nchunks < 1 || nchunks > INT32_MAX) return ADFL_E_ARG;
-  hipLaunchKernelGGL(k_qerror_batched, dim3((unsigned)nchunks), dim3(kBlock), 0, (hipStream_t)stream, d_x, d_q,
-                     d_chunks, d_scales, d_partials);
+  hipLaunchKernelGGL(k_qerror_batched<false>, dim3((unsigned)nchunks), dim3(kBlock), 0, (hipStream_t)stream, d_x,
+                     d_q, d_chunks, d_scales, d_partials);
+  return launch_status();
+}
+
+int adfl_slq_qerror_batched_int4(const float* d_x, const uint8_t* d_packed, const adfl_slq_chunk* d_chunks,
+                                 int64_t nchunks, const float* d_scales, double* d_partials, void* stream) {
+  if (!d_x || !d_packed || !d_chunks || !d_scales || !d_partials || nchunks < 1 || nchunks > INT32_MAX)
+    return ADFL_E_ARG;
+  hipLaunchKernelGGL(k_qerror_batched<true>, dim3((unsigned)nchunks), dim3(kBlock), 0, (hipStream_t)stream, d_x,
+                     (const int8_t*)d_packed, d_chunks, d_scales, d_partials);
   return launch_status();
 }
 
@@ -962,10 +1021,19 @@ int adfl_unpack_int4(const uint8_t* d_packed, int64_t n, int8_t* d_q, void* stre
 
 int adfl_slq_dequantize_mean(const int8_t* d_q, int64_t row_stride_bytes, int32_t k, int64_t n,
                              const float* d_scales, int64_t scale_stride, float* d_out, void* stream) {
+  return adfl_slq_dequantize_mean_self(d_q, row_stride_bytes, k, n, d_scales, scale_stride, -1, nullptr, d_out,
+                                       stream);
+}
+
+int adfl_slq_dequantize_mean_self(const int8_t* d_q, int64_t row_stride_bytes, int32_t k, int64_t n,
+                                  const float* d_scales, int64_t scale_stride, int32_t self_row,
+                                  const float* d_self_x, float* d_out, void* stream) {
   if (!d_q || !d_scales || !d_out || n < 1 || k < 1 || row_stride_bytes < n || scale_stride < 1) return ADFL_E_ARG;
+  if (self_row >= k || self_row < -1 || (self_row >= 0 && !d_self_x)) return ADFL_E_ARG;
   if (!aligned16(d_q) || !aligned16(d_out) || (row_stride_bytes & 15) != 0) return ADFL_E_ALIGN;
+  if (self_row >= 0 && !aligned16(d_self_x)) return ADFL_E_ALIGN;
   hipLaunchKernelGGL(k_dequantize_mean, dim3(tile_grid(n / kTile)), dim3(kBlock), 0, (hipStream_t)stream, d_q,
-                     row_stride_bytes, (int)k, n, d_scales, scale_stride, d_out);
+                     row_stride_bytes, (int)k, n, d_scales, scale_stride, (int)self_row, d_self_x, d_out);
   return launch_status();
 }
 
@@ -983,11 +1051,20 @@ int adfl_slq_dequantize_add_batched(const int8_t* d_q, const adfl_slq_chunk* d_c
 
 int adfl_slq_dequantize_mean_int4(const uint8_t* d_packed, int64_t row_stride_bytes, int32_t k, int64_t n,
                                   const float* d_scales, int64_t scale_stride, float* d_out, void* stream) {
+  return adfl_slq_dequantize_mean_self_int4(d_packed, row_stride_bytes, k, n, d_scales, scale_stride, -1, nullptr,
+                                            d_out, stream);
+}
+
+int adfl_slq_dequantize_mean_self_int4(const uint8_t* d_packed, int64_t row_stride_bytes, int32_t k, int64_t n,
+                                       const float* d_scales, int64_t scale_stride, int32_t self_row,
+                                       const float* d_self_x, float* d_out, void* stream) {
   if (!d_packed || !d_scales || !d_out || n < 1 || k < 1 || row_stride_bytes < (n + 1) / 2 || scale_stride < 1)
     return ADFL_E_ARG;
+  if (self_row >= k || self_row < -1 || (self_row >= 0 && !d_self_x)) return ADFL_E_ARG;
   if (!aligned16(d_packed) || !aligned16(d_out) || (row_stride_bytes & 15) != 0) return ADFL_E_ALIGN;
+  if (self_row >= 0 && !aligned16(d_self_x)) return ADFL_E_ALIGN;
   hipLaunchKernelGGL(k_dequantize_mean_int4, dim3(tile_grid(n / kTile4)), dim3(kBlock), 0, (hipStream_t)stream,
-                     d_packed, row_stride_bytes, (int)k, n, d_scales, scale_stride, d_out);
+                     d_packed, row_stride_bytes, (int)k, n, d_scales, scale_stride, (int)self_row, d_self_x, d_out);
   return launch_status();
 }
 

@@ -18,11 +18,17 @@ Also reported on the same line:
   all-gather's bus bandwidth. Never part of `value`.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
+
+`--gpus N` with N > 1 outside torchrun starts N rank processes of this script itself (RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_* set per child, one free 127.0.0.1 port) before anything touches the GPU, and exits
+with their status; under torchrun WORLD_SIZE must equal --gpus.
 """
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -50,7 +56,61 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget for the CPU baseline sample")
     p.add_argument("--exchange", choices=("auto", "on", "off"), default="auto",
                    help="C4 peer-exchange leg (encode + RCCL all-gather + decode-mean); auto = only when N > 1")
+    p.add_argument("--plumbing-check", action="store_true",
+                   help="CPU-only check of the rank launcher / barrier / max-over-ranks (gloo); no GPU, no bench")
     return p.parse_args()
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n_gpus: int, script: str, argv) -> int:
+    """Run `script argv` as `n_gpus` rank processes, one per GPU (the torchrun contract: RANK, LOCAL_RANK,
+    WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT). The caller must not have touched the GPU. If a rank
+    fails, the others are terminated (they would otherwise wait at a barrier). Returns the exit status:
+    0, or the first failing rank's."""
+    port = free_port()
+    procs = []
+    for r in range(n_gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n_gpus),
+                   LOCAL_WORLD_SIZE=str(n_gpus), GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script] + list(argv), env=env))
+    status = 0
+    try:
+        while procs:
+            for p in list(procs):
+                rc = p.poll()
+                if rc is None:
+                    continue
+                procs.remove(p)
+                if rc != 0 and status == 0:
+                    status = rc if rc > 0 else 128 - rc
+                    for q in procs:
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for q in procs:
+            q.kill()
+    return status
+
+
+def maybe_launch(n_gpus: int, script: str, argv) -> "int | None":
+    """Multi-GPU entry: None when this process is the (only) rank to run — N=1, or a rank already started by
+    torchrun / launch_ranks — otherwise the exit status of the N ranks it started."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if int(env_world) != n_gpus:
+            raise SystemExit(f"bench: --gpus {n_gpus} disagrees with WORLD_SIZE={env_world}; "
+                             f"launch with torchrun --nproc-per-node {n_gpus} or without torchrun")
+        return None
+    if n_gpus < 1:
+        raise SystemExit(f"bench: --gpus must be >= 1, got {n_gpus}")
+    if n_gpus == 1:
+        return None
+    return launch_ranks(n_gpus, script, argv)
 
 
 def dist_setup(args, backend: str = "nccl"):
@@ -86,42 +146,99 @@ def max_over_ranks(v: float, world: int) -> float:
 
 
 def pmc_traffic(kernel: str):
-    """HBM bytes per launch from the committed PMC summary (profiles/pmc_traffic.json), if present."""
+    """HBM bytes per launch from the committed PMC summary (profiles/pmc_traffic.json), only while the kernel
+    source it was measured on is the one built now (its SHA-256 is recorded by tools/pmc_summary.py); a
+    stale or missing summary gives None."""
+    import hashlib
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    src = os.path.join(REPO, "ad-federatedlearning_amd", "csrc", "slq_codec.hip")
     try:
         with open(path) as f:
             d = json.load(f)
+        with open(src, "rb") as f:
+            if d.get("kernel_source_sha256") != hashlib.sha256(f.read()).hexdigest():
+                return None
         return d["kernels"][KERNEL_SYMBOLS[kernel]]["hbm_bytes_per_launch"]
     except (OSError, KeyError, ValueError):
         return None
 
 
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
 def cpu_baseline(x_dev: torch.Tensor, bits: int, budget_s: float, q_dev: torch.Tensor, s_dev: torch.Tensor):
-    """The reference's own op sequence on host cores, timed on a bounded sample of the workload."""
+    """The reference's own op sequence (quant.py:100-103,110) on host cores, timed on the full 1 GiB workload
+    at three thread counts — ATen's default (the job's share of cores, OMP_NUM_THREADS), 1, and
+    os.cpu_count() — best of >= 3 round trips each (fewer only if one round trip exceeds the budget).
+    `value`/`cores` report the fastest of the three."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import slq_oracle as oracle  # test infrastructure: the checker / baseline leg only
 
-    threads = torch.get_num_threads()
+    default_threads = torch.get_num_threads()
     x = x_dev.cpu()
-    # sample: the full 1 GiB buffer, as many round trips as fit the budget (at least one)
-    times, parity = [], None
-    t_start = time.perf_counter()
-    while True:
-        t0 = time.perf_counter()
-        q, scale = oracle.aten_encode(x, bits)
-        d = oracle.aten_decode(q)
-        times.append(time.perf_counter() - t0)
-        if parity is None:  # the GPU result on this very workload must equal the reference's
-            parity = bool(torch.equal(q.int_repr(), q_dev.cpu())) and float(s_dev.item()) == scale
-        del q, d
-        if time.perf_counter() - t_start + min(times) > budget_s or len(times) >= 5:
-            break
-    best = min(times)
-    cpu = {"value": round((x.numel() * 4 / GIB) / best, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-           "sample": f"{len(times)} x full 1 GiB round trip (torch.abs/max/quantize_per_tensor/dequantize, "
-                     f"quant.py:100-110) on {threads} host threads, best-of; {os.cpu_count()} CPUs visible",
-           "ms_per_round_trip": round(best * 1e3, 1)}
+    parity = None
+    per_threads = {}
+    counts = []
+    for t in (default_threads, 1, os.cpu_count() or default_threads):
+        if t not in counts:
+            counts.append(t)
+    share = budget_s / len(counts)
+    for threads in counts:
+        torch.set_num_threads(threads)
+        times = []
+        t_start = time.perf_counter()
+        while True:
+            t0 = time.perf_counter()
+            q, scale = oracle.aten_encode(x, bits)
+            d = oracle.aten_decode(q)
+            times.append(time.perf_counter() - t0)
+            if parity is None:  # the GPU result on this very workload must equal the reference's
+                parity = bool(torch.equal(q.int_repr(), q_dev.cpu())) and float(s_dev.item()) == scale
+            del q, d
+            if len(times) >= 5 or (len(times) >= 3 and time.perf_counter() - t_start + min(times) > share) \
+                    or time.perf_counter() - t_start > 2 * share:
+                break
+        per_threads[threads] = (min(times), len(times))
+    torch.set_num_threads(default_threads)
+    gib = x.numel() * 4 / GIB
+    best_threads = min(per_threads, key=lambda k: per_threads[k][0])
+    best = per_threads[best_threads][0]
+    cpu = {"value": round(gib / best, 3), "unit": "GiB/s", "cores": best_threads, "kind": "port",
+           "sample": f"full 1 GiB round trip (torch.abs/max/quantize_per_tensor/dequantize, quant.py:100-110), "
+                     f"best of >= 3 per thread count, thread counts {counts}; {os.cpu_count()} CPUs visible, "
+                     f"{len(os.sched_getaffinity(0))} in this process's affinity mask",
+           "cpu_model": cpu_model(), "ms_per_round_trip": round(best * 1e3, 1),
+           "by_threads": {str(t): {"GiB_per_s": round(gib / v[0], 3), "ms_per_round_trip": round(v[0] * 1e3, 1),
+                                   "runs": v[1]} for t, v in per_threads.items()}}
     return cpu, parity
+
+
+def cold_decode_ms(lib, qp, n, sp, op, stream, reps: int = 10) -> float:
+    """Decode with the Infinity Cache holding none of the payload: a 512 MiB read between the encode and the
+    decode evicts it (a READ, so no dirty lines drain into the timed decode). The timed headline decodes
+    right after the encode, and decode starts on the payload bytes the encode wrote last (DESIGN.md §4);
+    a receiving peer decodes a payload that arrived from elsewhere — this number."""
+    from adfl_amd import _lib
+    junk = torch.ones(128 << 20, dtype=torch.float32, device=stream.device)
+    sh = stream.cuda_stream
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for e0, e1 in evs:
+        junk.amax()
+        e0.record(stream)
+        _lib.check(lib.adfl_slq_dequantize(qp, n, sp, op, sh))
+        e1.record(stream)
+    torch.cuda.synchronize()
+    del junk
+    return sorted(e0.elapsed_time(e1) for e0, e1 in evs)[reps // 2]
 
 
 def exchange_leg(x: torch.Tensor, out: torch.Tensor, bits: int, world: int, steps: int, warmup: int):
@@ -175,9 +292,40 @@ def exchange_leg(x: torch.Tensor, out: torch.Tensor, bits: int, world: int, step
             "backend": dist.get_backend()}
 
 
+def plumbing_check(args):
+    """--plumbing-check: the N-rank path of this script without a GPU (gloo): every rank joins, reports
+    itself, spins for (rank + 1) * 50 ms between the two barriers, and rank 0 prints the max over ranks."""
+    world, rank, _ = dist_setup(args, backend="gloo")
+    import torch.distributed as dist
+    if os.environ.get("ADFL_PLUMBING_FAIL_RANK") == str(rank):   # tests: a rank that dies before the barrier
+        sys.exit(3)
+    barrier(world)
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 0.05 * (rank + 1):
+        pass
+    barrier(world)
+    slowest = max_over_ranks(time.perf_counter() - t0, world)
+    ranks = [None] * world
+    if world > 1:
+        dist.all_gather_object(ranks, (rank, int(os.environ.get("LOCAL_RANK", "0"))))
+    else:
+        ranks = [(0, 0)]
+    if rank == 0:
+        print(json.dumps({"plumbing_check": True, "n_gpus": world, "ranks": ranks,
+                          "max_over_ranks_s": round(slowest, 4)}), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    rc = maybe_launch(args.gpus, os.path.abspath(__file__), sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
+    if args.plumbing_check:
+        return plumbing_check(args)
     world, rank, local = dist_setup(args)
+    assert world == args.gpus, (world, args.gpus)
     from adfl_amd import ops
     from adfl_amd import _lib
 
@@ -222,11 +370,13 @@ def main():
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(elapsed, world)
 
+    decode_cold = cold_decode_ms(lib, qp, n, sp, op, stream)
+
     exchange = None
     if args.exchange == "on" or (args.exchange == "auto" and world > 1):
         if world == 1:
             import torch.distributed as dist
-            dist.init_process_group("nccl", init_method="tcp://127.0.0.1:29577", rank=0, world_size=1,
+            dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{free_port()}", rank=0, world_size=1,
                                     device_id=dev)
         exchange = exchange_leg(x, out, args.bits, world, min(args.steps, 20), min(args.warmup, 3))
 
@@ -256,6 +406,7 @@ def main():
                      "traffic": pmc_traffic(dominant),
                      "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": round(per_kernel[dominant], 4)},
         "kernels_ms": {k: round(v, 4) for k, v in per_kernel.items()},
+        "decode_cold_ms": round(decode_cold, 4),
         "round_trip_roofline": {"alg_bytes": 14 * n, "kernel_ms": round(kernels_ms, 4),
                                 "achieved_GBs": round(14 * n / (kernels_ms * 1e-3) / 1e9, 1),
                                 "frac": round(14 * n / (kernels_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),

@@ -102,6 +102,10 @@ int adfl_slq_dequantize_batched(const int8_t* d_q, const adfl_slq_chunk* d_chunk
  * d_partials[4*c .. 4*c+3]: sum (x-d)^2, sum x^2, sum x*d, sum d^2 with d = fp32(scale*q). */
 int adfl_slq_qerror_batched(const float* d_x, const int8_t* d_q, const adfl_slq_chunk* d_chunks, int64_t nchunks,
                             const float* d_scales, double* d_partials, void* stream);
+/* Same against an int4-packed bucket (adfl_slq_encode_batched_int4's payload: even tensor offsets,
+ * d = fp32(scale * (nibble - 8)), the value unpack_4bit + dequantize gives, compression.py:51-66). */
+int adfl_slq_qerror_batched_int4(const float* d_x, const uint8_t* d_packed, const adfl_slq_chunk* d_chunks,
+                                 int64_t nchunks, const float* d_scales, double* d_partials, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * int4 packed variant — compression.py pack_4bit / unpack_4bit (Src/ADFL/compression.py:35-66)
@@ -135,6 +139,17 @@ int adfl_slq_dequantize_mean(const int8_t* d_q, int64_t row_stride_bytes, int32_
 /* Same over K int4-packed rows (ceil(n/2) bytes of payload each, layout of adfl_slq_quantize_int4). */
 int adfl_slq_dequantize_mean_int4(const uint8_t* d_packed, int64_t row_stride_bytes, int32_t k, int64_t n,
                                   const float* d_scales, int64_t scale_stride, float* d_out, void* stream);
+/* The receiving peer's mean with its OWN update exact, as the reference forms it
+ * (Src/ADFL/Client/async_peer.py:170-174, Examples/ray_ad.py:183-188: the local fp32 parameters are
+ * appended after the received updates, then stack(...).mean(0)): row self_row is skipped, the other rows
+ * are summed in r order, d_self_x (n fp32, 16-byte aligned) is added last, then / K.
+ * self_row = -1 is adfl_slq_dequantize_mean. */
+int adfl_slq_dequantize_mean_self(const int8_t* d_q, int64_t row_stride_bytes, int32_t k, int64_t n,
+                                  const float* d_scales, int64_t scale_stride, int32_t self_row,
+                                  const float* d_self_x, float* d_out, void* stream);
+int adfl_slq_dequantize_mean_self_int4(const uint8_t* d_packed, int64_t row_stride_bytes, int32_t k, int64_t n,
+                                       const float* d_scales, int64_t scale_stride, int32_t self_row,
+                                       const float* d_self_x, float* d_out, void* stream);
 
 /* Fused decode + in-place accumulate into K models: for every model k and tensor t,
  *   model_k[t][i] = fp32(model_k[t][i] + fp32(scale_t * q[i]))

@@ -129,5 +129,32 @@ void oracle_slq_dequantize_mean_int4(const uint8_t* const* ps, const float* scal
     }
 }
 
+/* The receiving peer's mean with its own update exact (Src/ADFL/Client/async_peer.py:170-174,
+ * Examples/ray_ad.py:183-188: own fp32 parameters appended after the received updates, then
+ * stack(...).mean(0)): rows other than self_row in r order, then self_x, fp32, then / K. int4 rows when
+ * packed != 0 (compression.py:51-66). */
+void oracle_slq_dequantize_mean_self(const void* const* rows, const float* scales, int32_t k, int64_t n,
+                                     int32_t self_row, const float* self_x, int32_t packed, float* out) {
+    for (int64_t i = 0; i < n; ++i) {
+        float s = 0.0f;
+        int first = 1;
+        for (int32_t r = 0; r < k; ++r) {
+            if (r == self_row) continue;
+            int v;
+            if (packed) {
+                uint8_t b = ((const uint8_t*)rows[r])[i / 2];
+                v = (i & 1) ? ((b & 0xF) - 8) : (((b >> 4) & 0xF) - 8);
+            } else {
+                v = ((const int8_t*)rows[r])[i];
+            }
+            float d = scales[r] * (float)v;
+            s = first ? d : s + d;
+            first = 0;
+        }
+        if (self_row >= 0) s = first ? self_x[i] : s + self_x[i];
+        out[i] = s / (float)k;
+    }
+}
+
 /* Thread-free helper the tests use for SHA inputs of recipe cases. */
 uint32_t oracle_f32_bits(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }

@@ -57,6 +57,8 @@ def lib():
         L.oracle_slq_dequantize_mean.restype = None
         L.oracle_slq_dequantize_mean_int4.argtypes = [P, P, I32, I64, P]
         L.oracle_slq_dequantize_mean_int4.restype = None
+        L.oracle_slq_dequantize_mean_self.argtypes = [P, P, I32, I64, I32, P, I32, P]
+        L.oracle_slq_dequantize_mean_self.restype = None
         _lib = L
     return _lib
 
@@ -129,6 +131,18 @@ def dequantize_mean_int4(packed_rows, scales, n: int) -> np.ndarray:
     sc = np.ascontiguousarray(scales, dtype=np.float32)
     out = np.empty(n, np.float32)
     lib().oracle_slq_dequantize_mean_int4(arr, _ptr(sc), len(ps), n, _ptr(out))
+    return out
+
+
+def dequantize_mean_self(rows, scales, n: int, self_row: int, self_x, packed: bool = False) -> np.ndarray:
+    """Peer mean with the receiver's own update exact: rows (int8 payloads, or int4-packed with packed=True)
+    other than self_row summed in order, self_x (fp32) added last, / K (async_peer.py:170-174)."""
+    rs = [np.ascontiguousarray(r).view(np.uint8).reshape(-1) for r in rows]
+    arr = (ctypes.c_void_p * len(rs))(*[r.ctypes.data for r in rs])
+    sc = np.ascontiguousarray(scales, dtype=np.float32)
+    sx = np.ascontiguousarray(self_x, dtype=np.float32).reshape(-1)
+    out = np.empty(n, np.float32)
+    lib().oracle_slq_dequantize_mean_self(arr, _ptr(sc), len(rs), n, int(self_row), _ptr(sx), int(packed), _ptr(out))
     return out
 
 

@@ -41,3 +41,46 @@ def test_bench_max_over_ranks_gloo():
         p.join(timeout=60)
     assert all(r[1] != "error" for r in res), res
     assert sorted(res) == [(0, 1.5, 2 / 1.5), (1, 1.5, 2 / 1.5)]
+
+
+def _run_bench(argv, env_extra=None, timeout=180):
+    import json
+    import subprocess
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py")] + argv, env=env, capture_output=True,
+                       text=True, timeout=timeout)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r, [json.loads(ln) for ln in lines]
+
+
+def test_bench_gpus2_launches_two_ranks():
+    """`bench.py --gpus 2` outside torchrun starts two rank processes itself (the driver's scaling run),
+    and the line it prints is rank 0's, with n_gpus == 2 and the slowest rank's time."""
+    r, lines = _run_bench(["--gpus", "2", "--plumbing-check"])
+    assert r.returncode == 0, r.stderr
+    assert len(lines) == 1, r.stdout                     # one JSON line, from rank 0 only
+    line = lines[0]
+    assert line["n_gpus"] == 2
+    assert sorted(tuple(x) for x in line["ranks"]) == [(0, 0), (1, 1)]
+    assert line["max_over_ranks_s"] >= 0.1               # rank 1 spins 2 x 50 ms: its time is the max
+
+
+def test_bench_gpus1_runs_in_process():
+    r, lines = _run_bench(["--gpus", "1", "--plumbing-check"])
+    assert r.returncode == 0, r.stderr
+    assert lines[0]["n_gpus"] == 1 and lines[0]["ranks"] == [[0, 0]]
+
+
+def test_bench_refuses_gpus_world_size_mismatch():
+    r, lines = _run_bench(["--gpus", "2", "--plumbing-check"], {"WORLD_SIZE": "1", "RANK": "0"})
+    assert r.returncode != 0 and not lines
+    assert "disagrees with WORLD_SIZE" in r.stderr
+
+
+def test_bench_failing_rank_fails_launch():
+    """A rank that dies makes the launcher exit non-zero instead of hanging at the barrier."""
+    r, lines = _run_bench(["--gpus", "3", "--plumbing-check"], {"ADFL_PLUMBING_FAIL_RANK": "1"})
+    assert r.returncode == 3 and not lines

@@ -33,11 +33,14 @@ class OracleCodec:
         off = (payload_bytes + 15) // 16 * 16
         r[off:off + 4] = np.array([scale], np.float32).view(np.uint8)
 
-    def mean(self, rows, n, packed, payload_bytes, out):
+    def mean(self, rows, n, packed, payload_bytes, out, self_row=-1, self_x=None):
         r = rows.numpy()
         off = (payload_bytes + 15) // 16 * 16
         scales = np.ascontiguousarray(r[:, off:off + 4]).view(np.float32).reshape(-1)
-        if packed:
+        if self_row >= 0:
+            res = oracle.dequantize_mean_self([r[k, :payload_bytes] for k in range(r.shape[0])], scales, n,
+                                              self_row, self_x.numpy(), packed)
+        elif packed:
             res = oracle.dequantize_mean_int4([r[k, :payload_bytes] for k in range(r.shape[0])], scales, n)
         else:
             res = oracle.dequantize_mean([r[k, :payload_bytes].view(np.int8) for k in range(r.shape[0])], scales)
@@ -58,6 +61,14 @@ def _expected(world, numel, bits, packed):
     return decoded
 
 
+def _mean_self_numpy(rows):
+    """fp32 sum in list order, then / K — torch.stack(updates).mean(0)'s value up to its summation order."""
+    acc = rows[0].copy()
+    for d in rows[1:]:
+        acc = (acc + d).astype(np.float32)
+    return (acc.astype(np.float64) / len(rows)).astype(np.float32)
+
+
 def _worker(rank, world, port, cases, errors):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -66,13 +77,17 @@ def _worker(rank, world, port, cases, errors):
         here = os.path.dirname(os.path.abspath(__file__))
         sys.path.insert(0, os.path.join(os.path.dirname(here), "ad-federatedlearning_amd"))
         from adfl_amd.exchange import PeerExchange
-        for numel, bits, packed, chunks in cases:
+        for numel, bits, packed, chunks, exact_self in cases:
             ex = PeerExchange(numel, bits=bits, packed=packed, chunks=chunks, device=torch.device("cpu"),
-                              codec=OracleCodec())
+                              codec=OracleCodec(), exact_self=exact_self)
             x = torch.from_numpy(_update(rank, numel))
             got = ex.exchange_mean(x).numpy()
             decoded = _expected(world, numel, bits, packed)
-            if packed:
+            if exact_self:
+                # the reference's mean: received updates, then the local fp32 update appended last
+                decoded = [d for r, d in enumerate(decoded) if r != rank] + [_update(rank, numel)]
+                want = _mean_self_numpy(decoded)
+            elif packed:
                 want = oracle.dequantize_mean_int4(
                     [oracle.pack_int4(oracle.encode(_update(r, numel), bits)[0]) for r in range(world)],
                     [oracle.encode(_update(r, numel), bits)[1] for r in range(world)], numel)
@@ -97,11 +112,11 @@ def _free_port():
 
 @pytest.mark.parametrize("world", [2])
 def test_peer_exchange_gloo(world):
-    cases = [(1000, 8, False, 1), (4097, 8, False, 3), (12345, 4, True, 4), (33, 4, True, 1), (64, 2, False, 2)]
+    cases = [(1000, 8, False, 1, False), (4097, 8, False, 3, False), (12345, 4, True, 4, False),
+             (33, 4, True, 1, False), (64, 2, False, 2, False),
+             (1000, 8, False, 1, True), (4097, 8, False, 3, True), (12345, 4, True, 4, True), (33, 4, True, 1, True)]
     ctx = mp.get_context("spawn")
     errors = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, _free_port() if r == 0 else None, cases, errors))
-             for r in range(world)]
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, cases, errors)) for r in range(world)]
     for p in procs:

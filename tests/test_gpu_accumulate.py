@@ -82,3 +82,26 @@ def test_channel_receive_add_matches_reference_route(target_device):
             assert got.dtype == e[key].dtype
             assert torch.equal(got.view(-1).view(torch.int32) if got.is_floating_point() else got,
                                e[key].view(-1).view(torch.int32) if got.is_floating_point() else e[key]), key
+
+
+def test_receive_add_back_to_back_cpu_payloads():
+    """Consecutive receive_add_ calls with different CPU payloads: the pinned staging of call i+1 must not be
+    rewritten while call i's H2D still reads it. Each accumulation equals the reference route."""
+    ch = SLQChannel(8)
+    updates = []
+    for i in range(4):
+        u = {k: v * 10.0 ** (-i) if v.is_floating_point() else v for k, v in _model(100 + i, "cpu").items()}
+        updates.append(ch.on_client_send(u)[0])
+    targets = [_model(50, "cuda")]
+    expect = copy.deepcopy({k: v.cpu() for k, v in targets[0].items()})
+    for c in updates:
+        ch.receive_add_(c, targets)
+        dec, _ = ch.on_client_receive(c)
+        for key in dec:
+            expect[key].mul_(1).add_(dec[key], alpha=1)
+    for key in expect:
+        got = targets[0][key].cpu()
+        if got.is_floating_point():
+            assert torch.equal(got.view(-1).view(torch.int32), expect[key].view(-1).view(torch.int32)), key
+        else:
+            assert torch.equal(got, expect[key]), key

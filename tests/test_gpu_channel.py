@@ -276,3 +276,57 @@ def test_packed_channel_device_dict():
     dec, _ = PackedSLQChannel(4).on_server_receive(qp)
     ref, _ = SLQChannel(4).on_server_receive(SLQChannel(4).on_client_send({"w": x.cpu()})[0])
     assert torch.equal(dec["w"].cpu(), ref["w"])  # values in [-7, 7]: packing is lossless vs int8 SLQ
+
+
+def test_packed_send_with_q_error():
+    """PackedSLQChannel.send_with_q_error (inherited surface): payload identical to on_client_send, metrics
+    equal to the reference's formulas on the packed channel's own decode (model.py:256-323)."""
+    from adfl_amd.Channel import PackedSLQChannel
+    g = torch.Generator().manual_seed(4)
+    params = {f"w{i}": torch.randn(33 + 13 * i, 17, generator=g) * 10.0 ** (-i) for i in range(5)}
+    params["w_odd"] = torch.randn(3, 7, generator=g)       # odd element count: the zero-padded last byte
+    params["bias"] = torch.randn(17, generator=g)
+    ch = PackedSLQChannel(4)
+    qp, c_time, mse, cos = ch.send_with_q_error(params)
+    qp2, _ = ch.on_client_send(params)
+    for k in params:
+        a, b = qp.params[k].data, qp2.params[k].data
+        assert torch.equal(a, b) if params[k].ndim > 1 else a is b
+    dec, _ = ch.on_server_receive(qp)
+    keys = [k for k in params if params[k].ndim > 1]
+    a64 = torch.cat([params[k].flatten().double() for k in keys])
+    b64 = torch.cat([dec[k].flatten().double() for k in keys])
+    e64 = torch.cat([(params[k] - dec[k]).flatten().double() for k in keys])
+    assert mse == pytest.approx(((e64 ** 2).sum() / (a64 ** 2).sum()).item(), rel=1e-9)
+    assert cos == pytest.approx(((a64 * b64).sum() / (a64.norm() * b64.norm())).item(), rel=1e-12)
+    assert c_time > 0
+
+
+@pytest.mark.parametrize("channel", ["SLQChannel", "PackedSLQChannel", "QSGDChannel", "CNATChannel"])
+def test_decoded_tensors_are_independently_owned(channel):
+    """Decode hands back one owned tensor per entry, as the reference does (quant.py:107-112): no views of
+    a shared bucket, so keeping one update (FedBuff, Src/ADFL/Strategy/fed_buff.py:75,90) keeps only its
+    own bytes alive and pickling one tensor ships only that tensor. Encode payloads likewise."""
+    import adfl_amd.Channel as C
+    ch = getattr(C, channel)(4 if channel == "PackedSLQChannel" else 8)
+    g = torch.Generator().manual_seed(5)
+    params = {f"w{i}": torch.randn(256, 64 + i, generator=g) for i in range(6)}
+    params["b"] = torch.randn(64, generator=g)
+    qp, _ = ch.on_client_send(params)
+    dec, _ = ch.on_server_receive(qp)
+    for k in params:
+        if params[k].ndim <= 1:
+            continue
+        t = dec[k]
+        assert not t.is_pinned() and t.is_contiguous() and t.dtype == torch.float32
+        assert t.untyped_storage().nbytes() == t.nbytes, k
+        assert len(pickle.dumps(t)) < t.nbytes + 2048, k
+        d = qp.params[k].data
+        assert d.untyped_storage().nbytes() == d.nbytes, k
+    ptrs = sorted(dec[k].data_ptr() for k in params if params[k].ndim > 1)
+    assert len(set(ptrs)) == len(ptrs)
+    # a second call must not alias or overwrite the first call's outputs
+    before = {k: dec[k].clone() for k in dec}
+    ch.on_server_receive(ch.on_client_send({k: v * 3 for k, v in params.items()})[0])
+    for k in dec:
+        assert torch.equal(dec[k], before[k]), k

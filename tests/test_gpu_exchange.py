@@ -36,7 +36,7 @@ def test_exchange_world1_matches_oracle(rccl_world1, numel, bits, packed, chunks
     from adfl_amd.exchange import PeerExchange
     rng = np.random.default_rng(numel)
     x = rng.standard_normal(numel, dtype=np.float32) * np.float32(1e-3)
-    ex = PeerExchange(numel, bits=bits, packed=packed, chunks=chunks, device=DEV)
+    ex = PeerExchange(numel, bits=bits, packed=packed, chunks=chunks, device=DEV, exact_self=False)
     got = ex.exchange_mean(torch.from_numpy(x).to(DEV)).cpu().numpy()
     q, s = oracle.encode(x, bits)
     want = oracle.decode_int4(oracle.pack_int4(q), numel, s) if packed else oracle.decode(q, s)
@@ -46,6 +46,38 @@ def test_exchange_world1_matches_oracle(rccl_world1, numel, bits, packed, chunks
         r = rows.cpu().numpy()[0]
         scale = r[(pb + 15) // 16 * 16:(pb + 15) // 16 * 16 + 4].view(np.float32)[0]
         assert np.float32(scale).view(np.uint32) == np.float32(s).view(np.uint32)
+
+
+def test_exchange_world1_exact_self_is_identity(rccl_world1):
+    """With the reference's mean (own update exact, async_peer.py:170-174), one rank's mean is its update."""
+    from adfl_amd.exchange import PeerExchange
+    x = torch.randn(1000003, device=DEV) * 1e-3
+    for packed, bits in ((False, 8), (True, 4)):
+        ex = PeerExchange(x.numel(), bits=bits, packed=packed, chunks=3, device=DEV)
+        assert torch.equal(ex.exchange_mean(x), x)
+
+
+def test_exchange_k8_rows_mean_self(rccl_world1):
+    """Rank 3 of an 8-way gather with its own update exact: rows 0-2, 4-7 decoded, then x added last."""
+    from adfl_amd import ops
+    k, n, me = 8, 300007, 3
+    rng = np.random.default_rng(9)
+    xs = [rng.standard_normal(n, dtype=np.float32) * np.float32(10.0 ** -r) for r in range(k)]
+    enc = [oracle.encode(x, 8) for x in xs]
+    row = (n + 15) // 16 * 16 + 16
+    rows = np.zeros((k, row), np.uint8)
+    for r, (q, s) in enumerate(enc):
+        rows[r, :n] = q.view(np.uint8)
+        rows[r, row - 16:row - 12] = np.array([s], np.float32).view(np.uint8)
+    rows_d = torch.from_numpy(rows).to(DEV)
+    scales = rows_d[:, row - 16:].view(torch.float32)[:, :1].contiguous()
+    got = ops.dequantize_mean(rows_d.view(torch.int8), scales, n, self_row=me,
+                              self_x=torch.from_numpy(xs[me]).to(DEV)).cpu().numpy()
+    want = oracle.dequantize_mean_self([q for q, _ in enc], [s for _, s in enc], n, me, xs[me])
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    stack = [oracle.decode(q, s) for r, (q, s) in enumerate(enc) if r != me] + [xs[me]]
+    ref = torch.stack([torch.from_numpy(d) for d in stack]).mean(0).numpy()
+    np.testing.assert_allclose(got, ref, rtol=1e-6, atol=1e-30)
 
 
 def test_exchange_k8_rows_mean(rccl_world1):

@@ -31,7 +31,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "ad-federatedlearning_amd"))
 
-from bench import GIB, HBM_PEAK_GBS, barrier, dist_setup, max_over_ranks  # noqa: E402
+from bench import GIB, HBM_PEAK_GBS, barrier, dist_setup, free_port, max_over_ranks, maybe_launch  # noqa: E402
 
 RESNET18 = 11_689_512
 
@@ -157,7 +157,7 @@ def mode_exchange(args, world, rank, dev):
     from adfl_amd.exchange import PeerExchange
     import torch.distributed as dist
     if world == 1 and not dist.is_initialized():
-        dist.init_process_group("nccl", init_method="tcp://127.0.0.1:29577", rank=0, world_size=1,
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{free_port()}", rank=0, world_size=1,
                                 device_id=dev)
     n = args.elems or (1 << 28)
     bits = 4 if args.packed else 8
@@ -402,7 +402,11 @@ def main():
     p.add_argument("--chunks", type=int, default=1)
     p.add_argument("--no-cpu", action="store_true", help="stoch: skip the host reference timing")
     args = p.parse_args()
+    rc = maybe_launch(args.gpus, os.path.abspath(__file__), sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
     world, rank, local = dist_setup(args)
+    assert world == args.gpus, (world, args.gpus)
     dev = torch.device("cuda", local)
     line = {"c3": mode_c3, "c5_int4": mode_c5_int4, "exchange": mode_exchange, "pcie": mode_pcie,
             "channel": mode_channel, "stoch": mode_stoch}[args.mode](

@@ -9,8 +9,19 @@ streaming stores. Both are in KiB. Infinity-Cache hits are counted in FETCH_SIZE
 """
 import collections
 import csv
+import hashlib
 import json
+import os
 import sys
+
+KERNEL_SRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ad-federatedlearning_amd",
+                          "csrc", "slq_codec.hip")
+
+
+def source_sha256(path: str = KERNEL_SRC) -> str:
+    """The kernel source the counters were taken on: bench.py reports `traffic` only while it matches."""
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
 
 ALG = {"k_absmax_flat": 4, "k_quantize_flat": 5, "k_dequantize_flat": 5}  # bytes per element (SURVEY §8d)
 N = 1 << 28
@@ -32,7 +43,7 @@ def main(fetch_csv, write_csv, out):
     fetch, write = load(fetch_csv, "FETCH_SIZE"), load(write_csv, "WRITE_SIZE")
     res = {"source": [fetch_csv, write_csv], "workload": "bench.py C2: 2^28 fp32 elements per launch",
            "correction": "hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE halves 16-B streaming reads)",
-           "kernels": {}}
+           "kernel_source_sha256": source_sha256(), "kernels": {}}
     for k in ALG:
         if k in fetch and k in write:
             hbm = (2 * fetch[k] + write[k]) * 1024
