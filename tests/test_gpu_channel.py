@@ -307,7 +307,8 @@ def test_decoded_tensors_are_independently_owned(channel):
     """Decode hands back one owned tensor per entry, as the reference does (quant.py:107-112): no views of
     a shared bucket, so keeping one update (FedBuff, Src/ADFL/Strategy/fed_buff.py:75,90) keeps only its
     own bytes alive and pickling one tensor ships only that tensor. Encode payloads likewise."""
-    import adfl_amd.Channel as C
+    import importlib
+    C = importlib.import_module("adfl_amd.Channel")
     ch = getattr(C, channel)(4 if channel == "PackedSLQChannel" else 8)
     g = torch.Generator().manual_seed(5)
     params = {f"w{i}": torch.randn(256, 64 + i, generator=g) for i in range(6)}
