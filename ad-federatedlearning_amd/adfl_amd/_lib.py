@@ -22,6 +22,7 @@ INT = ctypes.c_int
 
 ALIGN_ELEMS = 64     # ADFL_SLQ_ALIGN_ELEMS
 CHUNK_ELEMS = 8192   # ADFL_SLQ_CHUNK_ELEMS
+RESIDENT_CHUNKS = 8  # ADFL_SLQ_RESIDENT_CHUNKS
 ABI_VERSION = 1      # ADFL_SLQ_ABI_VERSION
 
 
@@ -45,6 +46,8 @@ SIGNATURES = {
     "adfl_slq_dequantize": (INT, [P, I64, P, P, P]),
     "adfl_slq_build_chunks": (I64, [P, P, I32, P, I64]),
     "adfl_slq_encode_batched": (INT, [P, P, I64, INT, P, P, P, P]),
+    "adfl_slq_build_encode_work": (I64, [P, I64, P, I64]),
+    "adfl_slq_encode_batched_work": (INT, [P, P, I64, P, I64, INT, P, P, P, P]),
     "adfl_slq_dequantize_batched": (INT, [P, P, I64, P, P, P]),
     "adfl_slq_qerror_batched": (INT, [P, P, P, I64, P, P, P]),
     "adfl_slq_qerror_batched_int4": (INT, [P, P, P, I64, P, P, P]),

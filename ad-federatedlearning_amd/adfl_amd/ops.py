@@ -184,7 +184,17 @@ class BucketLayout:
         if got != count:
             check(int(got) if got < 0 else -1)
         self.nchunks = int(count)
+        # the one-launch encode's work list (adfl_slq_build_encode_work): the first chunk of every tensor
+        # when all of them fit one block's registers, else empty (the two-pass encode)
+        nwork = lib.adfl_slq_build_encode_work(self.chunks, count, None, 0)
+        if nwork < 0:
+            raise ValueError(f"BucketLayout: encode work list failed ({nwork})")
+        self.work = np.zeros(max(nwork, 1), dtype=np.int32)
+        if nwork:
+            lib.adfl_slq_build_encode_work(self.chunks, count, self.work.ctypes.data, nwork)
+        self.nwork = int(nwork)
         self._device_chunks = {}
+        self._device_work = {}
 
     def device_chunks(self, device: torch.device) -> torch.Tensor:
         key = (device.type, device.index)
@@ -193,6 +203,14 @@ class BucketLayout:
             host = torch.frombuffer(bytearray(bytes(self.chunks)), dtype=torch.uint8)
             t = host.to(device)
             self._device_chunks[key] = t
+        return t
+
+    def device_work(self, device: torch.device) -> torch.Tensor:
+        key = (device.type, device.index)
+        t = self._device_work.get(key)
+        if t is None:
+            t = torch.from_numpy(self.work).to(device)
+            self._device_work[key] = t
         return t
 
 
@@ -209,9 +227,10 @@ def encode_batched(flat: torch.Tensor, layout: BucketLayout, bits: int, *, q: Op
     q = torch.empty(layout.total, dtype=torch.int8, device=dev) if q is None else q
     scales = torch.empty(layout.ntensors, dtype=torch.float32, device=dev) if scales is None else scales
     partials = torch.empty(layout.nchunks, dtype=torch.int32, device=dev) if partials is None else partials
-    check(_lib.load().adfl_slq_encode_batched(flat.data_ptr(), layout.device_chunks(dev).data_ptr(), layout.nchunks,
-                                              bits, q.data_ptr(), scales.data_ptr(), partials.data_ptr(),
-                                              _stream(dev)))
+    check(_lib.load().adfl_slq_encode_batched_work(flat.data_ptr(), layout.device_chunks(dev).data_ptr(),
+                                                   layout.nchunks, layout.device_work(dev).data_ptr(),
+                                                   layout.nwork, bits, q.data_ptr(),
+                                                   scales.data_ptr(), partials.data_ptr(), _stream(dev)))
     return q, scales
 
 

@@ -646,6 +646,87 @@ __global__ __launch_bounds__(kBlock) void k_quantize_batched(const float* __rest
   chunk_store(c, r, si.inv, q, lds[wave], lane, wave);
 }
 
+
+// ---- one-launch encode of a bucket of small tensors (a whole tensor per block, x read once) -------
+// A tensor of up to kSegChunks chunks (<= 65536 elements) fits the VGPRs of one 1024-thread block
+// (16 waves x 4 wave tiles x 4 float4 per lane = 64 VGPRs). When EVERY tensor of the bucket does, the
+// encode is one launch: each block loads its whole tensor, reduces max|x| in-block, forms the scale and
+// quantizes from registers — no cross-block dependency, no second pass, x read once (5 B/element
+// instead of 9). C3's 256 x 45,662 layout: encode 22.8 -> 16.4 us, round trip 0.63 -> 0.78 of 8 TB/s
+// with the Infinity Cache flushed (profiles/r02/microbench_c3.txt).
+// Blocks walk a host-built work list (adfl_slq_build_encode_work: the first chunk of every tensor), so no
+// block is launched only to exit: a 1024-thread block takes a whole CU's wave slots, and idle ones queued
+// behind the working blocks (27.6 us with the chunk table as the grid).
+// With any larger tensor the two-pass encode runs instead: big blocks pay off only while there are about
+// as many of them as CUs, and segmenting the large tensors (one absmax per 65,536-element segment, then
+// a segment quantize launch) measured slower than the two passes (log-uniform layout: 28.4 vs 23.9 us).
+constexpr int kSegBlock = 1024;
+constexpr int kSegWaves = kSegBlock / 64;
+constexpr int kSegTilesPerWave = 4;
+constexpr int64_t kSegMaxElems = (int64_t)kSegWaves * kSegTilesPerWave * kTile;  // 65536
+constexpr int kSegChunks = (int)(kSegMaxElems / ADFL_SLQ_CHUNK_ELEMS);            // 8
+static_assert(kSegChunks == ADFL_SLQ_RESIDENT_CHUNKS, "header constant");
+static_assert(kSegMaxElems % ADFL_SLQ_CHUNK_ELEMS == 0, "segment = whole chunks");
+static_assert(kSegBlock == kTile, "tail: one element per thread");
+
+__device__ __forceinline__ uint32_t block_max_seg(uint32_t v) {
+  __shared__ uint32_t red[kSegWaves];
+  v = wave_max(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint32_t m = red[0];
+#pragma unroll
+  for (int w = 1; w < kSegWaves; ++w) m = max(m, red[w]);
+  return m;
+}
+
+// work[b] = the first chunk of tensor b (every tensor <= kSegChunks chunks).
+__global__ __launch_bounds__(kSegBlock) void k_encode_resident(const float* __restrict__ x,
+                                                               const adfl_slq_chunk* __restrict__ chunks,
+                                                               const int32_t* __restrict__ work, float qmax,
+                                                               int8_t* __restrict__ q, float* __restrict__ scales) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kSegWaves][kTile / 4];
+  const int64_t ci = work[blockIdx.x];
+  const adfl_slq_chunk c = chunks[ci];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int len = (c.nchunks - 1) * ADFL_SLQ_CHUNK_ELEMS + chunks[ci + c.nchunks - 1].len;
+  const float* xt = x + c.start;
+  // all of the tensor's loads in flight at once (x non-temporal: dead after this pass)
+  const int head = chunk_head(c.start, len, 16);
+  const int ntiles = (len - head) / kTile;
+  const float4* x4 = reinterpret_cast<const float4*>(xt + head);
+  float4 v[kSegTilesPerWave][4];
+#pragma unroll
+  for (int k = 0; k < kSegTilesPerWave; ++k) {
+    const int t = wave + k * kSegWaves;
+    if (t < ntiles) {
+      load_tile(x4 + t * (kTile / 4), v[k], lane);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[k][j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  const float hv = (int)threadIdx.x < head ? xt[threadIdx.x] : 0.0f;
+  const int ti = head + ntiles * kTile + (int)threadIdx.x;  // < 1024 tail elements: one per thread
+  const float tv = ti < len ? __builtin_nontemporal_load(xt + ti) : 0.0f;
+  uint32_t m = max(abs_bits(hv), abs_bits(tv));
+#pragma unroll
+  for (int k = 0; k < kSegTilesPerWave; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) m = max(m, abs_bits4(v[k][j]));
+  const ScaleInv si = make_scale(block_max_seg(m), qmax);
+  if (threadIdx.x == 0) scales[c.tensor] = si.scale;
+  int8_t* qt = q + c.start;
+  uint4* q16 = reinterpret_cast<uint4*>(qt + head);
+#pragma unroll
+  for (int k = 0; k < kSegTilesPerWave; ++k) {
+    const int t = wave + k * kSegWaves;
+    if (t < ntiles) quantize_tile_regs(v[k], q16 + t * (kTile / 16), si.inv, lds[wave], lane);
+  }
+  if ((int)threadIdx.x < head) qt[threadIdx.x] = (int8_t)quant1(hv, si.inv);
+  if (ti < len) qt[ti] = (int8_t)quant1(tv, si.inv);
+}
+
 __global__ __launch_bounds__(kBlock) void k_dequantize_batched(const int8_t* __restrict__ q,
                                                                const adfl_slq_chunk* __restrict__ chunks,
                                                                const float* __restrict__ scales,
@@ -928,6 +1009,38 @@ int adfl_slq_encode_batched(const float* d_x, const adfl_slq_chunk* d_chunks, in
   if (int s = launch_status()) return s;
   hipLaunchKernelGGL(k_quantize_batched, dim3((unsigned)nchunks), dim3(kBlock), 0, st, d_x, d_chunks, qmax_f(bits),
                      (const uint32_t*)d_partials, d_q, d_scales);
+  return launch_status();
+}
+
+int64_t adfl_slq_build_encode_work(const adfl_slq_chunk* chunks, int64_t nchunks, int32_t* work, int64_t capacity) {
+  if (!chunks || nchunks < 1 || nchunks > INT32_MAX) return ADFL_E_ARG;
+  int64_t n = 0;
+  for (int64_t i = 0; i < nchunks; ++i) {
+    const adfl_slq_chunk& c = chunks[i];
+    if (c.first_chunk < 0 || c.nchunks < 1 || i < c.first_chunk || i >= (int64_t)c.first_chunk + c.nchunks)
+      return ADFL_E_ARG;
+    if (c.nchunks > kSegChunks) return 0;  // a tensor too large for one block: the two-pass encode
+    if (i != c.first_chunk) continue;
+    if (work) {
+      if (n >= capacity) return ADFL_E_ARG;
+      work[n] = (int32_t)i;
+    }
+    ++n;
+  }
+  return n;
+}
+
+int adfl_slq_encode_batched_work(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks,
+                                 const int32_t* d_work, int64_t nwork, int bits, int8_t* d_q, float* d_scales,
+                                 uint32_t* d_partials, void* stream) {
+  if (nwork == 0) return adfl_slq_encode_batched(d_x, d_chunks, nchunks, bits, d_q, d_scales, d_partials, stream);
+  if (!d_x || !d_chunks || !d_work || !d_q || !d_scales || nchunks < 1 || nchunks > INT32_MAX || nwork < 0 ||
+      nwork > nchunks)
+    return ADFL_E_ARG;
+  if (int s = check_bits(bits)) return s;
+  if (!aligned16(d_x) || !aligned16(d_q)) return ADFL_E_ALIGN;
+  hipLaunchKernelGGL(k_encode_resident, dim3((unsigned)nwork), dim3(kSegBlock), 0, (hipStream_t)stream, d_x,
+                     d_chunks, d_work, qmax_f(bits), d_q, d_scales);
   return launch_status();
 }
 

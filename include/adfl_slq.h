@@ -90,9 +90,23 @@ typedef struct adfl_slq_chunk {
 int64_t adfl_slq_build_chunks(const int64_t* offsets, const int64_t* sizes, int32_t ntensors,
                               adfl_slq_chunk* chunks, int64_t capacity);
 
-/* d_partials: int64 nchunks * 4 bytes of device scratch. d_scales: ntensors floats. */
+/* d_partials: int64 nchunks * 4 bytes of device scratch. d_scales: ntensors floats.
+ * Two launches: per-chunk absmax partials, then per-chunk quantize (x read twice). */
 int adfl_slq_encode_batched(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, int bits,
                             int8_t* d_q, float* d_scales, uint32_t* d_partials, void* stream);
+
+/* One-launch encode (same output) for a bucket whose tensors ALL have at most ADFL_SLQ_RESIDENT_CHUNKS
+ * chunks (<= 65,536 elements): one block holds a whole tensor in registers, so x is read once and there is
+ * no second pass. Host-side: adfl_slq_build_encode_work() writes the first chunk of every tensor to `work`
+ * and returns the count; it returns 0 if some tensor is larger (call with work == NULL to size). The list
+ * is copied to the device once per layout, like the chunk table. adfl_slq_encode_batched_work() with
+ * nwork == 0 is adfl_slq_encode_batched (the two-pass encode), so a caller can always go through it.
+ * d_partials is used only by the two-pass encode. */
+#define ADFL_SLQ_RESIDENT_CHUNKS 8
+int64_t adfl_slq_build_encode_work(const adfl_slq_chunk* chunks, int64_t nchunks, int32_t* work, int64_t capacity);
+int adfl_slq_encode_batched_work(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks,
+                                 const int32_t* d_work, int64_t nwork, int bits, int8_t* d_q, float* d_scales,
+                                 uint32_t* d_partials, void* stream);
 int adfl_slq_dequantize_batched(const int8_t* d_q, const adfl_slq_chunk* d_chunks, int64_t nchunks,
                                 const float* d_scales, float* d_out, void* stream);
 

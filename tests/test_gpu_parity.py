@@ -148,6 +148,74 @@ def test_bucketed_ragged_and_specials_vs_oracle(align):
             assert same_f32(dn[o:o + n], oracle.decode(q_ref, s_ref)), (bits, t)
 
 
+@pytest.mark.parametrize("align", [64, 1])
+@pytest.mark.parametrize("legacy", [False, True])
+def test_bucketed_resident_boundary_vs_oracle(align, legacy):
+    """Tensors at the one-block limit (65,536 elements = 8 chunks) and just past it (9 chunks), compact or
+    aligned, NaN and +-inf at chunk edges: with a large tensor present the encode is the two-pass one;
+    without it (the second half) the one-launch resident encode. `legacy` calls adfl_slq_encode_batched
+    directly."""
+    from adfl_amd import _lib
+    rng = np.random.default_rng(21)
+    sizes = [65536, 65537, 1, 65535, 131072 + 5, 16, 49152, 8192 * 8 + 8191, 3000, 65536 - 15]
+    lay = ops.BucketLayout(sizes, align=align)
+    assert lay.nwork == 0  # tensors above 65,536 elements: the two-pass encode
+    flat = np.zeros(lay.total, np.float32)
+    for i, (o, n) in enumerate(zip(lay.offsets, lay.sizes)):
+        flat[o:o + n] = rng.standard_normal(n, dtype=np.float32) * np.float32(10.0 ** -(i % 5))
+    flat[lay.offsets[0] + 65535] = np.inf          # last element of a resident tensor
+    flat[lay.offsets[1] + 65536] = np.nan          # the 9th chunk's only element
+    flat[lay.offsets[6]:lay.offsets[6] + 49152] = 0.0   # all-zero resident tensor: payload all 127
+    flat[lay.offsets[9] + 7] = -np.inf
+    x = torch.from_numpy(flat).to(DEV)
+    for bits in (8, 3):
+        if legacy:
+            q = torch.empty(lay.total, dtype=torch.int8, device=DEV)
+            sc = torch.empty(lay.ntensors, dtype=torch.float32, device=DEV)
+            part = torch.empty(lay.nchunks, dtype=torch.int32, device=DEV)
+            _lib.check(_lib.load().adfl_slq_encode_batched(
+                x.data_ptr(), lay.device_chunks(DEV).data_ptr(), lay.nchunks, bits, q.data_ptr(), sc.data_ptr(),
+                part.data_ptr(), torch.cuda.current_stream(DEV).cuda_stream))
+        else:
+            q, sc = ops.encode_batched(x, lay, bits)
+        qn, sn = q.cpu().numpy(), sc.cpu().numpy()
+        for t, (o, n) in enumerate(zip(lay.offsets, lay.sizes)):
+            q_ref, s_ref = oracle.encode(flat[o:o + n], bits)
+            assert np.array_equal(qn[o:o + n], q_ref), (bits, t)
+            assert same_f32(sn[t], s_ref), (bits, t)
+    small = [n for n in sizes if n <= 65536]
+    lay = ops.BucketLayout(small, align=align)
+    assert lay.nwork == len(small)
+    flat = np.zeros(lay.total, np.float32)
+    for i, (o, n) in enumerate(zip(lay.offsets, lay.sizes)):
+        flat[o:o + n] = rng.standard_normal(n, dtype=np.float32) * np.float32(10.0 ** -(i % 5))
+    flat[lay.offsets[0] + 65535] = np.nan
+    flat[lay.offsets[3]:lay.offsets[3] + 49152] = 0.0
+    flat[lay.offsets[6] + 3] = -np.inf
+    q, sc = ops.encode_batched(torch.from_numpy(flat).to(DEV), lay, 8)
+    qn, sn = q.cpu().numpy(), sc.cpu().numpy()
+    for t, (o, n) in enumerate(zip(lay.offsets, lay.sizes)):
+        q_ref, s_ref = oracle.encode(flat[o:o + n], 8)
+        assert np.array_equal(qn[o:o + n], q_ref), t
+        assert same_f32(sn[t], s_ref), t
+
+
+def test_bucketed_all_resident_is_one_launch():
+    """C3's equal layout (256 x 45,662): every tensor fits one block, the encode is a single launch and still
+    equals the oracle per tensor."""
+    sizes = [11689512 // 256 + (1 if i < 11689512 % 256 else 0) for i in range(256)]
+    lay = ops.BucketLayout(sizes)
+    assert lay.nwork == 256
+    rng = np.random.default_rng(5)
+    flat = (rng.standard_normal(lay.total, dtype=np.float32) * np.float32(1e-3))
+    q, sc = ops.encode_batched(torch.from_numpy(flat).to(DEV), lay, 8)
+    qn, sn = q.cpu().numpy(), sc.cpu().numpy()
+    for t in range(0, 256, 17):
+        o, n = lay.offsets[t], lay.sizes[t]
+        q_ref, s_ref = oracle.encode(flat[o:o + n], 8)
+        assert np.array_equal(qn[o:o + n], q_ref) and same_f32(sn[t], s_ref), t
+
+
 @pytest.mark.parametrize("case", manifest()["int4"], ids=lambda c: c["name"])
 def test_int4_pack_unpack_vs_golden(case):
     I = int4()
