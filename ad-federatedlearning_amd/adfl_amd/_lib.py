@@ -52,6 +52,7 @@ SIGNATURES = {
     "adfl_slq_qerror_batched": (INT, [P, P, P, I64, P, P, P]),
     "adfl_slq_qerror_batched_int4": (INT, [P, P, P, I64, P, P, P]),
     "adfl_slq_encode_batched_int4": (INT, [P, P, I64, INT, P, P, P, P]),
+    "adfl_slq_encode_batched_int4_work": (INT, [P, P, I64, P, I64, INT, P, P, P, P]),
     "adfl_slq_dequantize_batched_int4": (INT, [P, P, I64, P, P, P]),
     "adfl_slq_quantize_int4": (INT, [P, I64, INT, P, P, P, P]),
     "adfl_slq_encode_int4": (INT, [P, I64, INT, P, P, P, I64, P]),

@@ -318,9 +318,10 @@ def encode_batched_int4(flat: torch.Tensor, layout: BucketLayout, bits: int = 4,
     packed = torch.empty(layout.total // 2, dtype=torch.uint8, device=dev) if packed is None else packed
     scales = torch.empty(layout.ntensors, dtype=torch.float32, device=dev) if scales is None else scales
     partials = torch.empty(layout.nchunks, dtype=torch.int32, device=dev) if partials is None else partials
-    check(_lib.load().adfl_slq_encode_batched_int4(flat.data_ptr(), layout.device_chunks(dev).data_ptr(),
-                                                   layout.nchunks, bits, packed.data_ptr(), scales.data_ptr(),
-                                                   partials.data_ptr(), _stream(dev)))
+    check(_lib.load().adfl_slq_encode_batched_int4_work(flat.data_ptr(), layout.device_chunks(dev).data_ptr(),
+                                                        layout.nchunks, layout.device_work(dev).data_ptr(),
+                                                        layout.nwork, bits, packed.data_ptr(), scales.data_ptr(),
+                                                        partials.data_ptr(), _stream(dev)))
     return packed, scales
 
 

@@ -727,6 +727,66 @@ __global__ __launch_bounds__(kSegBlock) void k_encode_resident(const float* __re
   if (ti < len) qt[ti] = (int8_t)quant1(tv, si.inv);
 }
 
+// int4 variant (PackedSLQChannel's buckets: even tensor offsets, packed byte e/2 = flat elements e, e+1):
+// 2048-element int4 wave tiles, 2 per wave (16 float4 per lane); the < 32-element head and the < 2048-
+// element tail go pairwise, one pair per thread, an odd tensor's last element paired with pack_4bit's
+// zero pad (compression.py:42-43).
+constexpr int kSegTiles4PerWave = (int)(kSegMaxElems / kTile4 / kSegWaves);  // 2
+static_assert(kSegTiles4PerWave * kTile4 * kSegWaves == kSegMaxElems, "int4 tiles cover a segment");
+static_assert(2 * kSegBlock == kTile4, "int4 tail: one pair per thread");
+
+__global__ __launch_bounds__(kSegBlock) void k_encode_resident_int4(const float* __restrict__ x,
+                                                                    const adfl_slq_chunk* __restrict__ chunks,
+                                                                    const int32_t* __restrict__ work, float qmax,
+                                                                    uint8_t* __restrict__ packed,
+                                                                    float* __restrict__ scales) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[kSegWaves][kTile4 / 4];
+  const int64_t ci = work[blockIdx.x];
+  const adfl_slq_chunk c = chunks[ci];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int len = (c.nchunks - 1) * ADFL_SLQ_CHUNK_ELEMS + chunks[ci + c.nchunks - 1].len;
+  const float* xt = x + c.start;
+  const int head = chunk_head(c.start, len, 32);  // even: tensor offsets are even
+  const int ntiles = (len - head) / kTile4;
+  const float4* x4 = reinterpret_cast<const float4*>(xt + head);
+  float4 v[kSegTiles4PerWave][8];
+#pragma unroll
+  for (int k = 0; k < kSegTiles4PerWave; ++k) {
+    const int t = wave + k * kSegWaves;
+    if (t < ntiles) {
+      load_tile_int4(x4 + t * (kTile4 / 4), v[k], lane);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[k][j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  // head pair (element 2*tid of [0, head)) and tail pair (t0 + 2*tid of [t0, len))
+  const int hi = 2 * (int)threadIdx.x;
+  const bool has_h = hi < head;
+  const float h0 = has_h ? xt[hi] : 0.0f, h1 = (has_h && hi + 1 < len) ? xt[hi + 1] : 0.0f;
+  const int ti = head + ntiles * kTile4 + 2 * (int)threadIdx.x;
+  const bool has_t = ti < len;
+  const float t0v = has_t ? __builtin_nontemporal_load(xt + ti) : 0.0f;
+  const float t1v = (has_t && ti + 1 < len) ? __builtin_nontemporal_load(xt + ti + 1) : 0.0f;
+  uint32_t m = max(max(abs_bits(h0), abs_bits(h1)), max(abs_bits(t0v), abs_bits(t1v)));
+#pragma unroll
+  for (int k = 0; k < kSegTiles4PerWave; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = max(m, abs_bits4(v[k][j]));
+  const ScaleInv si = make_scale(block_max_seg(m), qmax);
+  if (threadIdx.x == 0) scales[c.tensor] = si.scale;
+  uint8_t* pt = packed + (c.start >> 1);
+#pragma unroll
+  for (int k = 0; k < kSegTiles4PerWave; ++k) {
+    const int t = wave + k * kSegWaves;
+    if (t < ntiles)
+      quantize_tile_int4_regs(v[k], reinterpret_cast<uint4*>(pt + (head >> 1)) + t * 64, si.inv, lds[wave], lane);
+  }
+  // the pad of an odd tensor's last pair is a zero CODE (compression.py:42-43), not quant1(0)
+  if (has_h) pt[hi >> 1] = (uint8_t)pack_pair(quant1(h0, si.inv), hi + 1 < len ? quant1(h1, si.inv) : 0);
+  if (has_t) pt[ti >> 1] = (uint8_t)pack_pair(quant1(t0v, si.inv), ti + 1 < len ? quant1(t1v, si.inv) : 0);
+}
+
 __global__ __launch_bounds__(kBlock) void k_dequantize_batched(const int8_t* __restrict__ q,
                                                                const adfl_slq_chunk* __restrict__ chunks,
                                                                const float* __restrict__ scales,
@@ -1081,6 +1141,21 @@ int adfl_slq_encode_batched_int4(const float* d_x, const adfl_slq_chunk* d_chunk
   if (int s = launch_status()) return s;
   hipLaunchKernelGGL(k_quantize_batched_int4, dim3((unsigned)nchunks), dim3(kBlock), 0, st, d_x, d_chunks, nchunks,
                      qmax_f(bits), (const uint32_t*)d_partials, d_packed, d_scales);
+  return launch_status();
+}
+
+int adfl_slq_encode_batched_int4_work(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks,
+                                      const int32_t* d_work, int64_t nwork, int bits, uint8_t* d_packed,
+                                      float* d_scales, uint32_t* d_partials, void* stream) {
+  if (nwork == 0)
+    return adfl_slq_encode_batched_int4(d_x, d_chunks, nchunks, bits, d_packed, d_scales, d_partials, stream);
+  if (!d_x || !d_chunks || !d_work || !d_packed || !d_scales || nchunks < 1 || nchunks > INT32_MAX || nwork < 0 ||
+      nwork > nchunks)
+    return ADFL_E_ARG;
+  if (int s = check_bits(bits)) return s;
+  if (!aligned16(d_x) || !aligned16(d_packed)) return ADFL_E_ALIGN;
+  hipLaunchKernelGGL(k_encode_resident_int4, dim3((unsigned)nwork), dim3(kSegBlock), 0, (hipStream_t)stream, d_x,
+                     d_chunks, d_work, qmax_f(bits), d_packed, d_scales);
   return launch_status();
 }
 

@@ -137,6 +137,11 @@ int adfl_slq_dequantize_int4(const uint8_t* d_packed, int64_t n, const float* d_
  * last byte pairs its last element with a zero pad exactly as pack_4bit does per tensor. */
 int adfl_slq_encode_batched_int4(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, int bits,
                                  uint8_t* d_packed, float* d_scales, uint32_t* d_partials, void* stream);
+/* One-launch int4 encode for a bucket whose tensors all fit a block (work list of
+ * adfl_slq_build_encode_work; nwork == 0 is adfl_slq_encode_batched_int4). Same output. */
+int adfl_slq_encode_batched_int4_work(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks,
+                                      const int32_t* d_work, int64_t nwork, int bits, uint8_t* d_packed,
+                                      float* d_scales, uint32_t* d_partials, void* stream);
 int adfl_slq_dequantize_batched_int4(const uint8_t* d_packed, const adfl_slq_chunk* d_chunks, int64_t nchunks,
                                      const float* d_scales, float* d_out, void* stream);
 int adfl_pack_int4(const int8_t* d_q, int64_t n, uint8_t* d_packed, void* stream);

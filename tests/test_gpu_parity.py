@@ -322,18 +322,30 @@ def test_reference_errors():
         ops.encode(torch.randn(3, 3, device=DEV), 0)
 
 
+INT4_SIZES = {
+    "small": [1, 2, 3, 31, 32, 33, 2047, 2048, 2049, 8191, 8192, 8193, 20001, 5, 4096 * 3 + 7],
+    # one-block limit (65,536) and odd sizes right under it: the one-launch encode's head/tail pairs
+    "boundary": [65536, 65535, 7, 65533, 2049, 31, 65534, 1, 4099, 8193],
+    # a tensor past the limit: the two-pass encode for the whole bucket
+    "large": [65537, 1, 33, 70001, 2048, 131075, 3],
+}
+
+
 @pytest.mark.parametrize("align", [2, 64])
 @pytest.mark.parametrize("bits", [4, 2])
-def test_bucketed_int4_vs_oracle(align, bits):
+@pytest.mark.parametrize("kind", list(INT4_SIZES))
+def test_bucketed_int4_vs_oracle(align, bits, kind):
     """Packed int4 buckets (PackedSLQChannel's kernels): per tensor, pack_4bit(SLQ(x)) and its decode."""
     rng = np.random.default_rng(40 + align + bits)
-    sizes = [1, 2, 3, 31, 32, 33, 2047, 2048, 2049, 8191, 8192, 8193, 20001, 5, 4096 * 3 + 7]
+    sizes = INT4_SIZES[kind]
     lay = ops.BucketLayout(sizes, align=align)
+    assert (lay.nwork == 0) == (kind == "large")
     flat = np.zeros(lay.total, np.float32)
     for i, (o, n) in enumerate(zip(lay.offsets, lay.sizes)):
         flat[o:o + n] = rng.standard_normal(n, dtype=np.float32) * np.float32(2.0 ** -i)
     flat[lay.offsets[3]:lay.offsets[3] + lay.sizes[3]] = 0.0          # aliasing tensor (payload 127)
-    flat[lay.offsets[7] + 5] = np.nan
+    flat[lay.offsets[4] + lay.sizes[4] // 2] = np.nan
+    flat[lay.offsets[0] + lay.sizes[0] - 1] = -np.inf
     packed, scales = ops.encode_batched_int4(torch.from_numpy(flat).to(DEV), lay, bits)
     out = ops.decode_batched_int4(packed, scales, lay)
     pn, sn, dn = packed.cpu().numpy(), scales.cpu().numpy(), out.cpu().numpy()
