@@ -58,7 +58,8 @@ def _owned_host(buf: torch.Tensor, offsets, shapes: List[torch.Size]) -> List[to
 
 
 @_serialized
-def _encode_stoch(params: Parameters, names: List[str], codec: str, bits: int, uniforms=None, seed=None):
+def _encode_stoch(params: Parameters, names: List[str], codec: str, bits: int, uniforms=None, seed=None,
+                  torch_norm: bool = False):
     """Encode the ndim > 1 fp32 tensors `names` of `params` in one bucketed pass.
 
     Returns {name: (data, signs, scale, scale_2)} with CPU tensors for CPU inputs (device tensors for
@@ -77,7 +78,8 @@ def _encode_stoch(params: Parameters, names: List[str], codec: str, bits: int, u
     mins = None
     if codec == "qsgd":
         lv, sg, norms = sops.qsgd_encode_batched(x_dev, lay, bits, uniforms=uniforms, seed=seed, counter=0,
-                                                 levels=planes["levels"], signs=planes["signs"], norms=norms, ws=ws)
+                                                 levels=planes["levels"], signs=planes["signs"], norms=norms, ws=ws,
+                                                 torch_norm=torch_norm)
     elif codec == "rqsgd":
         mins = st.buf("s_mins", lay.ntensors, torch.float32)
         lv, sg, norms, mins = sops.rqsgd_encode_batched(x_dev, lay, bits, uniforms=uniforms, seed=seed, counter=0,
@@ -86,7 +88,7 @@ def _encode_stoch(params: Parameters, names: List[str], codec: str, bits: int, u
     else:
         lv, sg, norms = sops.cnat_encode_batched(x_dev, lay, bits, uniforms=uniforms, seed=seed, counter=0,
                                                  exps=planes["levels"].view(torch.int8), signs=planes["signs"],
-                                                 norms=norms, ws=ws)
+                                                 norms=norms, ws=ws, torch_norm=torch_norm)
     nm_host = st.buf("s_norms_host", 2 * lay.ntensors, torch.float32, pinned=True)
     nm_host[:lay.ntensors].copy_(norms, non_blocking=True)
     if mins is not None:
@@ -151,9 +153,14 @@ class _StochChannel(Channel):
     CODEC = "qsgd"
     NORM_BYTES = 4  # per quantized tensor: the norm (RQSGD: norm + minimum factor)
 
-    def __init__(self, bits: int) -> None:
+    def __init__(self, bits: int, torch_norm: bool = False) -> None:
+        """torch_norm=True: the L2 norm (QSGD, CNAT) in torch's own fp32 reduction order, bit-identical to
+        the reference's torch.linalg.vector_norm (sequential per tensor: slower on large tensors). The
+        default is the correctly rounded norm (fp64 accumulation), within torch's own summation error of it."""
         self.bits = bits
         self.levels = 2 ** bits - 1
+        if torch_norm:
+            self.torch_norm = True  # only set when asked: the default object has the reference's attributes
 
     def on_server_send(self, params: Parameters) -> Tuple[CompressedParameters, float]:
         return self._send(params)
@@ -205,7 +212,8 @@ class _StochChannel(Channel):
         names = [name for name, p in params.items() if p.ndim > 1 and p.numel() > 0]
         for name in names:
             _require_fp32(name, params[name], self.__class__.__name__)
-        encoded = _encode_stoch(params, names, self.CODEC, bits, uniforms, seed) if names else {}
+        encoded = (_encode_stoch(params, names, self.CODEC, bits, uniforms, seed, getattr(self, "torch_norm", False))
+                   if names else {})
         q_params = QuantParameters({}, 0)
         pass_signs = torch.zeros(1, dtype=torch.uint8)  # passthrough entries' unused signs, one per call
         for name, param in params.items():

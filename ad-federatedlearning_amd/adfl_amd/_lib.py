@@ -80,7 +80,7 @@ SIGNATURES = {
     "adfl_host_threads": (I32, []),
 }
 
-NORM_L2, NORM_LINF = 0, 1  # ADFL_NORM_*
+NORM_L2, NORM_LINF, NORM_L2_TORCH = 0, 1, 2  # ADFL_NORM_*
 
 _lib = None
 

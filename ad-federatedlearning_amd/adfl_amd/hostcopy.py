@@ -4,6 +4,8 @@ gather(): pieces of a CPU state dict -> one (pinned) host bucket; scatter(): a h
 storages. ctypes releases the GIL for the call, so the copy runs on the pool's threads plus the caller's.
 """
 
+import ctypes
+import os
 from typing import Sequence
 
 import numpy as np
@@ -12,6 +14,25 @@ import torch
 from . import _lib
 from ._lib import check
 
+_host = None
+
+
+def _host_lib():
+    """The library exporting adfl_host_copy: libadfl_slq.so, or — for CPU sanitizer runs only
+    (tools/sanitize/run.sh) — a separately built host-copy object named by ADFL_HOST_LIB."""
+    global _host
+    if _host is None:
+        path = os.environ.get("ADFL_HOST_LIB")
+        if path:
+            lib = ctypes.CDLL(path)
+            for name in ("adfl_host_copy", "adfl_host_threads"):
+                fn = getattr(lib, name)
+                fn.restype, fn.argtypes = _lib.SIGNATURES[name]
+            _host = lib
+        else:
+            _host = _lib.load()
+    return _host
+
 
 def copy_pieces(dst_ptrs: Sequence[int], src_ptrs: Sequence[int], nbytes: Sequence[int], threads: int = 0) -> None:
     d = np.asarray(dst_ptrs, dtype=np.uint64)
@@ -19,7 +40,7 @@ def copy_pieces(dst_ptrs: Sequence[int], src_ptrs: Sequence[int], nbytes: Sequen
     b = np.asarray(nbytes, dtype=np.int64)
     if not (len(d) == len(s) == len(b)):
         raise ValueError("copy_pieces: pointer and size lists differ in length")
-    check(_lib.load().adfl_host_copy(d.ctypes.data, s.ctypes.data, b.ctypes.data, len(b), threads))
+    check(_host_lib().adfl_host_copy(d.ctypes.data, s.ctypes.data, b.ctypes.data, len(b), threads))
 
 
 def gather(srcs: Sequence[torch.Tensor], dst: torch.Tensor, offsets: Sequence[int]) -> None:
@@ -44,4 +65,4 @@ def scatter(src: torch.Tensor, dsts: Sequence[torch.Tensor], offsets: Sequence[i
 
 
 def threads() -> int:
-    return int(_lib.load().adfl_host_threads())
+    return int(_host_lib().adfl_host_threads())

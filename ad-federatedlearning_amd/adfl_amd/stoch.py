@@ -21,12 +21,12 @@ from typing import Optional, Tuple
 import torch
 
 from . import _lib
-from ._lib import NORM_L2, NORM_LINF, check
+from ._lib import NORM_L2, NORM_L2_TORCH, NORM_LINF, check
 from .ops import BucketLayout, _dev, _stream
 
 __all__ = ["RngStream", "norms_batched", "qsgd_quantize_batched", "qsgd_encode_batched", "rqsgd_encode_batched",
            "qsgd_decode_batched", "rqsgd_decode_batched", "cnat_encode_batched", "cnat_decode_batched",
-           "philox_uniforms", "workspace", "NORM_L2", "NORM_LINF"]
+           "philox_uniforms", "workspace", "NORM_L2", "NORM_LINF", "NORM_L2_TORCH"]
 
 
 class RngStream:
@@ -76,7 +76,9 @@ def _ws(ws: Optional[torch.Tensor], layout: BucketLayout, dev) -> torch.Tensor:
 def norms_batched(flat: torch.Tensor, layout: BucketLayout, mode: int = NORM_L2, *,
                   norms: Optional[torch.Tensor] = None, mins: Optional[torch.Tensor] = None,
                   ws: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
-    """Per-tensor ||x||_2 (mode NORM_L2) or (max|x|, min|x|) (NORM_LINF)."""
+    """Per-tensor ||x||_2 (mode NORM_L2: fp64 accumulation, correctly rounded; NORM_L2_TORCH: torch's own
+    fp32 reduction order, bit-identical to the reference's norm, sequential per tensor) or
+    (max|x|, min|x|) (NORM_LINF)."""
     flat = _check_flat(flat, layout)
     dev = flat.device
     norms = torch.empty(layout.ntensors, dtype=torch.float32, device=dev) if norms is None else norms
@@ -113,13 +115,20 @@ def qsgd_quantize_batched(flat: torch.Tensor, layout: BucketLayout, bits: int, n
 def qsgd_encode_batched(flat: torch.Tensor, layout: BucketLayout, bits: int, *,
                         uniforms: Optional[torch.Tensor] = None, seed: int = 0, counter: int = 0,
                         levels: Optional[torch.Tensor] = None, signs: Optional[torch.Tensor] = None,
-                        norms: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None):
-    """QSGD encode of every tensor of a bucket: (levels u8, signs i8, L2 norms f32)."""
+                        norms: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None,
+                        torch_norm: bool = False):
+    """QSGD encode of every tensor of a bucket: (levels u8, signs i8, L2 norms f32). torch_norm=True takes
+    the norm in torch's reduction order (the reference's norm bit for bit; slower, sequential per tensor)."""
     flat = _check_flat(flat, layout)
     dev = flat.device
     levels, signs = _planes(layout, dev, levels, signs, torch.uint8)
     norms = torch.empty(layout.ntensors, dtype=torch.float32, device=dev) if norms is None else norms
     ws = _ws(ws, layout, dev)
+    if torch_norm:
+        norms_batched(flat, layout, NORM_L2_TORCH, norms=norms, ws=ws)
+        qsgd_quantize_batched(flat, layout, bits, norms, uniforms=uniforms, seed=seed, counter=counter,
+                              levels=levels, signs=signs)
+        return levels, signs, norms
     check(_lib.load().adfl_qsgd_encode_batched(flat.data_ptr(), layout.device_chunks(dev).data_ptr(), layout.nchunks,
                                                bits, _uniforms(uniforms, layout), seed, counter, ws.data_ptr(),
                                                ws.numel(), levels.data_ptr(), signs.data_ptr(), norms.data_ptr(),
@@ -172,9 +181,11 @@ def rqsgd_decode_batched(levels: torch.Tensor, signs: torch.Tensor, norms: torch
 def cnat_encode_batched(flat: torch.Tensor, layout: BucketLayout, bits: int, *,
                         uniforms: Optional[torch.Tensor] = None, seed: int = 0, counter: int = 0,
                         exps: Optional[torch.Tensor] = None, signs: Optional[torch.Tensor] = None,
-                        norms: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None):
+                        norms: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None,
+                        torch_norm: bool = False):
     """CNAT encode (x read once): (exponents i8, signs i8, L2 norms f32). A tensor whose norm is 0 gets
-    the reference's zero-branch bytes (0 / 1)."""
+    the reference's zero-branch bytes (0 / 1). torch_norm=True then replaces the norms with torch's own
+    (the exponents do not depend on the norm; both norms are 0 for exactly the same tensors)."""
     flat = _check_flat(flat, layout)
     dev = flat.device
     exps, signs = _planes(layout, dev, exps, signs, torch.int8)
@@ -184,6 +195,8 @@ def cnat_encode_batched(flat: torch.Tensor, layout: BucketLayout, bits: int, *,
                                                bits, _uniforms(uniforms, layout), seed, counter, ws.data_ptr(),
                                                ws.numel(), exps.data_ptr(), signs.data_ptr(), norms.data_ptr(),
                                                _stream(dev)))
+    if torch_norm:
+        norms_batched(flat, layout, NORM_L2_TORCH, norms=norms, ws=ws)
     return exps, signs, norms
 
 

@@ -473,6 +473,70 @@ __global__ __launch_bounds__(kBigBlock) void k_norm_finalize(const adfl_slq_chun
   }
 }
 
+// torch.linalg.vector_norm(x, ord=2) bit for bit as torch 2.10's CPU kernel computes it (the reference's
+// QSGD / CNAT norm, quant.py:226,512; restated and pinned to every golden norm in oracle/slq_oracle.c
+// oracle_torch_l2_norm): 8 fp32 lane accumulators acc[j] = fma(x[8i+j], x[8i+j], acc[j]) over i in order,
+// a left-to-right sum of the 8 lanes, then the n % 8 tail with fma; below 8 elements plain b + x*x.
+// The chains are inherently sequential (n / 8 dependent FMAs per lane), so one wave serves one tensor:
+// all 64 lanes load 64 consecutive elements (8 rows, coalesced), lanes 0..7 take their column's 8 values
+// in row order through cross-lane shuffles. Opt-in (ADFL_NORM_L2_TORCH): it is latency-bound, about one
+// element per cycle per tensor, against the fp64 default's full HBM rate.
+constexpr int kTorchNormGroups = 4;  // 64-element groups loaded ahead of the FMA chain
+
+__global__ __launch_bounds__(64) void k_norm_torch_order(const float* __restrict__ x,
+                                                         const adfl_slq_chunk* __restrict__ chunks,
+                                                         float* __restrict__ norms) {
+  const adfl_slq_chunk c = chunks[blockIdx.x];
+  if ((int64_t)blockIdx.x != c.first_chunk) return;  // one wave per tensor
+  const int lane = threadIdx.x;
+  const int64_t n = (int64_t)(c.nchunks - 1) * ADFL_SLQ_CHUNK_ELEMS + chunks[blockIdx.x + c.nchunks - 1].len;
+  const float* xt = x + c.start;
+  float b = 0.0f;
+  if (n < 8) {
+    if (lane == 0)
+      for (int i = 0; i < (int)n; ++i) {
+        const float sq = xt[i] * xt[i];
+        b = b + sq;
+      }
+  } else {
+    const int64_t nv = n - n % 8;
+    const int64_t ngroups = nv / 64;
+    const int col = lane & 7;
+    float acc = 0.0f;
+    for (int64_t g = 0; g < ngroups; g += kTorchNormGroups) {
+      float v[kTorchNormGroups];
+#pragma unroll
+      for (int u = 0; u < kTorchNormGroups; ++u) v[u] = (g + u < ngroups) ? xt[(g + u) * 64 + lane] : 0.0f;
+#pragma unroll
+      for (int u = 0; u < kTorchNormGroups; ++u) {
+        if (g + u >= ngroups) break;  // wave-uniform
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const float e = __shfl(v[u], col + 8 * r, 64);
+          acc = __builtin_fmaf(e, e, acc);
+        }
+      }
+    }
+    const int rem_rows = (int)((nv % 64) / 8);
+    if (rem_rows > 0) {
+      const float v = lane < rem_rows * 8 ? xt[ngroups * 64 + lane] : 0.0f;
+      for (int r = 0; r < rem_rows; ++r) {
+        const float e = __shfl(v, col + 8 * r, 64);
+        acc = __builtin_fmaf(e, e, acc);
+      }
+    }
+    float lanes[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) lanes[j] = __shfl(acc, j, 64);
+    b = lanes[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) b = b + lanes[j];
+    if (lane == 0)
+      for (int64_t i = nv; i < n; ++i) b = __builtin_fmaf(xt[i], xt[i], b);
+  }
+  if (lane == 0) norms[c.tensor] = (float)__builtin_sqrt((double)b);  // correctly rounded fp32 sqrt
+}
+
 __device__ __forceinline__ void fill_zero_norm(uint8_t* __restrict__ lv, int8_t* __restrict__ sg, int len) {
   for (int i = threadIdx.x; i < len; i += kBlock) {
     lv[i] = 0;
@@ -716,10 +780,14 @@ int adfl_stoch_norms_batched(const float* d_x, const adfl_slq_chunk* d_chunks, i
                              void* d_workspace, int64_t workspace_bytes, float* d_norms, float* d_mins,
                              void* stream) {
   if (!d_x || !d_norms || bad_table(d_chunks, nchunks)) return ADFL_E_ARG;
-  if (mode != ADFL_NORM_L2 && mode != ADFL_NORM_LINF) return ADFL_E_ARG;
-  if (int s = check_ws(d_workspace, workspace_bytes, nchunks)) return s;
+  if (mode != ADFL_NORM_L2 && mode != ADFL_NORM_LINF && mode != ADFL_NORM_L2_TORCH) return ADFL_E_ARG;
   if (!aligned16(d_x)) return ADFL_E_ALIGN;
   hipStream_t st = (hipStream_t)stream;
+  if (mode == ADFL_NORM_L2_TORCH) {  // no workspace: one wave per tensor
+    hipLaunchKernelGGL(k_norm_torch_order, dim3((unsigned)nchunks), dim3(64), 0, st, d_x, d_chunks, d_norms);
+    return launch_status();
+  }
+  if (int s = check_ws(d_workspace, workspace_bytes, nchunks)) return s;
   if (mode == ADFL_NORM_L2) {
     hipLaunchKernelGGL(k_norm_partials<ADFL_NORM_L2>, dim3((unsigned)nchunks), dim3(kBlock), 0, st, d_x, d_chunks,
                        nchunks - kKeepChunks, d_workspace);

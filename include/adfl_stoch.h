@@ -22,7 +22,8 @@
  *
  * Norm: fp32 squares accumulated in fp64 per chunk and per tensor (fixed order: deterministic), rounded
  * once to fp32, correctly rounded sqrt. torch's fp32 vector_norm differs from it only by torch's own
- * accumulation error; every other output bit follows the reference exactly.
+ * accumulation error; every other output bit follows the reference exactly. For bit parity
+ * with the reference's norm, compute it with ADFL_NORM_L2_TORCH and quantize with the given-norm entry.
  */
 #ifndef ADFL_STOCH_H
 #define ADFL_STOCH_H
@@ -35,7 +36,7 @@
 extern "C" {
 #endif
 
-enum { ADFL_NORM_L2 = 0, ADFL_NORM_LINF = 1 };
+enum { ADFL_NORM_L2 = 0, ADFL_NORM_LINF = 1, ADFL_NORM_L2_TORCH = 2 };
 
 /* Device workspace bytes the encode / norm calls need for a table of nchunks chunks (16 B per chunk). */
 int64_t adfl_stoch_workspace_bytes(int64_t nchunks);
@@ -43,7 +44,11 @@ int64_t adfl_stoch_workspace_bytes(int64_t nchunks);
 /* Per-tensor norms of a bucket (two launches: chunk partials, per-tensor finalize).
  *   ADFL_NORM_L2:   d_norms[t] = ||x_t||_2   (torch.linalg.vector_norm(x, ord=2), quant.py:226,512)
  *   ADFL_NORM_LINF: d_norms[t] = max|x_t|, d_mins[t] = min|x_t| (ord=inf / -inf, quant.py:367,380);
- *                   NaN anywhere in x_t makes both NaN. d_mins may be NULL for ADFL_NORM_L2. */
+ *                   NaN anywhere in x_t makes both NaN. d_mins may be NULL for ADFL_NORM_L2.
+ *   ADFL_NORM_L2_TORCH: ||x_t||_2 bit-identical to torch 2.10's CPU vector_norm (its fp32 reduction order:
+ *                   8 FMA lane accumulators, lane sum, FMA tail; plain multiply-add below 8 elements),
+ *                   i.e. the reference's own norm. One launch, no workspace (d_workspace may be NULL), but
+ *                   sequential per tensor: about one element per cycle per tensor. */
 int adfl_stoch_norms_batched(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, int mode,
                              void* d_workspace, int64_t workspace_bytes, float* d_norms, float* d_mins,
                              void* stream);

@@ -158,3 +158,31 @@ void oracle_slq_dequantize_mean_self(const void* const* rows, const float* scale
 
 /* Thread-free helper the tests use for SHA inputs of recipe cases. */
 uint32_t oracle_f32_bits(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+
+/* torch.linalg.vector_norm(x, ord=2) on an fp32 CPU tensor as torch 2.10 computes it (the reference's
+ * QSGD / CNAT scale, Src/ADFL/Channel/quant.py:226,512), restated from its observed behaviour — pinned
+ * bit for bit to every L2 norm in tests/golden/stoch.npz (the reference executed in place):
+ *   n >= 8: the AVX2 norm kernel — 8 fp32 lane accumulators, acc[j] = fma(x[8i+j], x[8i+j], acc[j]) over
+ *           i in order; then b = acc[0] + acc[1] + ... + acc[7] left to right; then the n % 8 tail
+ *           elements b = fma(x, x, b) in order;
+ *   n < 8:  b = b + x*x in order (separate multiply and add).
+ *   result: the correctly rounded fp32 sqrt of b.
+ * fmaf() is C99's single-rounding fused multiply-add. */
+float oracle_torch_l2_norm(const float* x, int64_t n) {
+    float b = 0.0f;
+    if (n < 8) {
+        for (int64_t i = 0; i < n; ++i) {
+            const float sq = x[i] * x[i];
+            b = b + sq;
+        }
+        return sqrtf(b);
+    }
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int64_t nv = n - n % 8;
+    for (int64_t i = 0; i < nv; i += 8)
+        for (int j = 0; j < 8; ++j) acc[j] = fmaf(x[i + j], x[i + j], acc[j]);
+    b = acc[0];
+    for (int j = 1; j < 8; ++j) b = b + acc[j];
+    for (int64_t i = nv; i < n; ++i) b = fmaf(x[i], x[i], b);
+    return sqrtf(b);
+}

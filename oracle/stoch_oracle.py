@@ -87,6 +87,20 @@ def l2_norm(x: np.ndarray) -> np.float32:
     return np.float32(np.sqrt(np.float64(s32)))  # sqrt of an fp32 in fp64 rounded once = correctly rounded
 
 
+def torch_l2_norm(x: np.ndarray) -> np.float32:
+    """``torch.linalg.vector_norm(x, ord=2)`` bit for bit as torch 2.10's CPU kernel computes it (the
+    reference's own QSGD / CNAT norm, quant.py:226,512): 8 fp32 FMA lane accumulators in order, left-to-
+    right lane sum, FMA tail; plain multiply-add below 8 elements (oracle/slq_oracle.c
+    ``oracle_torch_l2_norm``; pinned to every golden L2 norm by tests/test_stoch_golden.py)."""
+    import ctypes
+    import slq_oracle
+    L = slq_oracle.lib()
+    fn = L.oracle_torch_l2_norm
+    fn.argtypes, fn.restype = [ctypes.c_void_p, ctypes.c_int64], ctypes.c_float
+    a = np.ascontiguousarray(np.asarray(x, dtype=np.float32).reshape(-1))
+    return np.float32(fn(a.ctypes.data, a.size))
+
+
 def linf_norm(x: np.ndarray) -> np.float32:
     """``vector_norm(x, ord=inf)`` = max|x|, NaN if any element is NaN."""
     a = np.abs(np.asarray(x, dtype=np.float32).reshape(-1))

@@ -335,3 +335,71 @@ def test_decode_accepts_reference_built_payloads():
         dec, _ = cls(8).on_server_receive(qp)
         for k, v in want.items():
             assert same_f32(dec[k].numpy(), v), k
+
+
+L2_CASES = [c for c in CASES if c["codec"] != "rqsgd"]
+
+
+@pytest.mark.parametrize("c", L2_CASES, ids=[c["name"] for c in L2_CASES])
+def test_golden_torch_order_norm_end_to_end(c):
+    """torch_norm=True: the norm in torch's own reduction order (ADFL_NORM_L2_TORCH) is the reference's
+    norm bit for bit, so with the recorded uniforms the WHOLE encode — levels / exponents, signs and the
+    scale — equals the reference's output with nothing injected but the uniforms."""
+    x, u, q_ref, s_ref, d_ref, norm, _ = load_case(c)
+    lay = ops.BucketLayout([x.size], align=1)
+    xd, ud = d(x), d(u)
+    nrm, _ = stoch.norms_batched(xd, lay, stoch.NORM_L2_TORCH)
+    assert same_f32(h(nrm)[:1], np.array([norm], np.float32)), c["name"]
+    if c["codec"] == "qsgd":
+        lv, s, nrm = stoch.qsgd_encode_batched(xd, lay, c["bits"], uniforms=ud, torch_norm=True)
+    else:
+        lv, s, nrm = stoch.cnat_encode_batched(xd, lay, c["bits"], uniforms=ud, torch_norm=True)
+    np.testing.assert_array_equal(h(lv).view(np.uint8), q_ref.reshape(-1).view(np.uint8))
+    np.testing.assert_array_equal(h(s), s_ref.reshape(-1))
+    assert same_f32(h(nrm)[:1], np.array([norm], np.float32))
+
+
+@pytest.mark.parametrize("align", [1, 64])
+def test_torch_order_norm_bucket_and_sizes(align):
+    """Per-tensor torch-order norms over a bucket: every golden L2 case plus sizes around the 8-lane and
+    64-element group edges and a multi-chunk tensor, against the oracle's restatement."""
+    xs = [load_case(c)[0].reshape(-1) for c in L2_CASES]
+    rng = np.random.default_rng(77)
+    for n in (1, 7, 8, 9, 63, 64, 65, 71, 72, 511, 513, 8192 * 3 + 13, 100003):
+        xs.append(rng.standard_normal(n, dtype=np.float32) * np.float32(0.37))
+    lay = ops.BucketLayout([x.size for x in xs], align=align)
+    flat = np.zeros(lay.total, np.float32)
+    for x, o in zip(xs, lay.offsets):
+        flat[o:o + x.size] = x
+    nrm, _ = stoch.norms_batched(d(flat), lay, stoch.NORM_L2_TORCH)
+    got = h(nrm)
+    for i, x in enumerate(xs):
+        assert same_f32(got[i:i + 1], np.array([so.torch_l2_norm(x)], np.float32)), (i, x.size)
+
+
+@pytest.mark.parametrize("c", [c for c in CASES if c["codec"] == "qsgd"], ids=lambda c: c["name"])
+def test_default_norm_deviation_is_bounded(c):
+    """The DEFAULT norm (fp64 accumulation, correctly rounded) against the reference's fp32-accumulated
+    norm, nothing injected but the uniforms: (1) the scale differs from the reference's by at most torch's
+    own accumulation error, n * 2^-24 relative (2^-23 at least); (2) every level equals the oracle's level
+    for OUR norm — the norm is the only difference; (3) the levels that differ from the reference's differ
+    by one, at a rate bounded by levels * relative norm difference (the width of the moved rounding band)
+    plus a 3-sigma allowance. DESIGN.md §10 reports the measured rates."""
+    x, u, q_ref, _, _, norm, _ = load_case(c)
+    lay = ops.BucketLayout([x.size], align=1)
+    lv, _, nrm = stoch.qsgd_encode_batched(d(x), lay, c["bits"], uniforms=d(u))
+    mine = h(nrm)[0]
+    if not np.isfinite(norm) or norm == 0:
+        assert same_f32(np.array([mine]), np.array([norm], np.float32))
+        return
+    rel = abs(float(mine) - float(norm)) / float(norm)
+    assert rel <= max(x.size * 2.0 ** -24, 2.0 ** -23), (mine, norm)
+    levels = 2 ** c["bits"] - 1
+    q_mine, _ = so.qsgd_quantize(x.reshape(-1), levels, mine, u.reshape(-1))
+    got = h(lv)
+    np.testing.assert_array_equal(got, q_mine)
+    diff = got.astype(np.int32) - q_ref.reshape(-1).astype(np.int32)
+    assert np.all(np.abs(diff) <= 1)
+    rate = np.count_nonzero(diff) / x.size
+    expect = levels * rel
+    assert rate <= expect + 3 * np.sqrt(expect / x.size) + 1.0 / x.size, (rate, expect)

@@ -73,6 +73,15 @@ def test_oracle_norms(c):
     assert abs(float(mine) - float(norm)) <= bound * float(norm), (mine, norm)
 
 
+@pytest.mark.parametrize("c", [c for c in CASES if c["codec"] != "rqsgd"], ids=lambda c: c["name"])
+def test_oracle_torch_order_norm_is_the_reference_norm(c):
+    """The torch-order L2 norm restatement (8 FMA lanes, left-to-right lane sum, FMA tail; plain below 8
+    elements) reproduces the reference's recorded norm BIT FOR BIT on every QSGD / CNAT golden case,
+    NaN / inf / 0 included (the norm == 0 branch records tensor(0.))."""
+    x, _, _, _, _, norm, _ = load_case(c)
+    assert same_f32(np.float32(so.torch_l2_norm(x)), np.float32(norm)), c["name"]
+
+
 def test_golden_covers_the_reference_branches():
     kinds = {(c["codec"], c["q_dtype"], "tensor" in c["scale"]) for c in CASES}
     for codec in ("qsgd", "rqsgd", "cnat"):
