@@ -9,4 +9,4 @@ done
 for m in c3 stoch; do
   echo "== $m"; timeout -k 10 300 python tools/bench_configs.py --mode $m --steps 50 --warmup 5 > gpurun_out/$m.json 2> gpurun_out/$m.err; rc=$?; cat gpurun_out/$m.json; [ $rc -eq 0 ] || exit $rc
 done
-echo "== bench"; timeout -k 10 300 python bench.py --steps 50 --warmup 10 --exchange on --no-cpu-baseline > gpurun_out/bench.json 2> gpurun_out/bench.err; rc=$?; cat gpurun_out/bench.json; exit $rc
+echo "== bench"; timeout -k 10 300 python bench.py --steps 50 --warmup 10 --exchange on --no-cpu-baseline --pmc off > gpurun_out/bench.json 2> gpurun_out/bench.err; rc=$?; cat gpurun_out/bench.json; exit $rc
