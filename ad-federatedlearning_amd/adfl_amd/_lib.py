@@ -74,6 +74,9 @@ SIGNATURES = {
     "adfl_rqsgd_dequantize_batched": (INT, [P, P, P, I64, INT, P, P, P, P]),
     "adfl_cnat_encode_batched": (INT, [P, P, I64, INT, P, U64, U64, P, I64, P, P, P, P]),
     "adfl_cnat_dequantize_batched": (INT, [P, P, P, I64, P, P, P]),
+    "adfl_qsgd_encode_batched_work": (INT, [P, P, I64, P, I64, INT, P, U64, U64, P, I64, P, P, P, P]),
+    "adfl_rqsgd_encode_batched_work": (INT, [P, P, I64, P, I64, INT, P, U64, U64, P, I64, P, P, P, P, P]),
+    "adfl_cnat_encode_batched_work": (INT, [P, P, I64, P, I64, INT, P, U64, U64, P, I64, P, P, P, P]),
     "adfl_philox_uniforms": (INT, [P, I64, I64, U64, U64, P]),
     # adfl_host.h
     "adfl_host_copy": (INT, [P, P, P, I64, I32]),

@@ -16,6 +16,7 @@ Randomness: pass ``uniforms`` (fp32 plane indexed like x, values in [0, 1)) to i
 ``torch.manual_seed`` makes a run reproducible the way it does for the reference.
 """
 
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -73,6 +74,17 @@ def _ws(ws: Optional[torch.Tensor], layout: BucketLayout, dev) -> torch.Tensor:
     return workspace(layout, dev) if ws is None else ws
 
 
+def _work(layout: BucketLayout, dev, resident: Optional[bool] = None):
+    """(work list pointer, count) for the *_encode_batched_work entries: the one-launch register-resident
+    encode when every tensor of the layout fits a block (layout.nwork > 0), else (any, 0) = multi-launch.
+    ADFL_STOCH_RESIDENT=0 in the environment forces the multi-launch path (A/B runs)."""
+    if resident is None:
+        resident = os.environ.get("ADFL_STOCH_RESIDENT", "1") != "0"
+    if not resident or layout.nwork == 0:
+        return 0, 0
+    return layout.device_work(dev).data_ptr(), layout.nwork
+
+
 def norms_batched(flat: torch.Tensor, layout: BucketLayout, mode: int = NORM_L2, *,
                   norms: Optional[torch.Tensor] = None, mins: Optional[torch.Tensor] = None,
                   ws: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
@@ -116,9 +128,11 @@ def qsgd_encode_batched(flat: torch.Tensor, layout: BucketLayout, bits: int, *,
                         uniforms: Optional[torch.Tensor] = None, seed: int = 0, counter: int = 0,
                         levels: Optional[torch.Tensor] = None, signs: Optional[torch.Tensor] = None,
                         norms: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None,
-                        torch_norm: bool = False):
+                        torch_norm: bool = False, resident: Optional[bool] = None):
     """QSGD encode of every tensor of a bucket: (levels u8, signs i8, L2 norms f32). torch_norm=True takes
-    the norm in torch's reduction order (the reference's norm bit for bit; slower, sequential per tensor)."""
+    the norm in torch's reduction order (the reference's norm bit for bit; slower, sequential per tensor).
+    resident: None = the one-launch register-resident encode whenever the layout allows it (same bytes as
+    the multi-launch path), False = always the multi-launch path."""
     flat = _check_flat(flat, layout)
     dev = flat.device
     levels, signs = _planes(layout, dev, levels, signs, torch.uint8)
@@ -129,10 +143,11 @@ def qsgd_encode_batched(flat: torch.Tensor, layout: BucketLayout, bits: int, *,
         qsgd_quantize_batched(flat, layout, bits, norms, uniforms=uniforms, seed=seed, counter=counter,
                               levels=levels, signs=signs)
         return levels, signs, norms
-    check(_lib.load().adfl_qsgd_encode_batched(flat.data_ptr(), layout.device_chunks(dev).data_ptr(), layout.nchunks,
-                                               bits, _uniforms(uniforms, layout), seed, counter, ws.data_ptr(),
-                                               ws.numel(), levels.data_ptr(), signs.data_ptr(), norms.data_ptr(),
-                                               _stream(dev)))
+    check(_lib.load().adfl_qsgd_encode_batched_work(flat.data_ptr(), layout.device_chunks(dev).data_ptr(),
+                                                    layout.nchunks, *_work(layout, dev, resident), bits,
+                                                    _uniforms(uniforms, layout), seed, counter, ws.data_ptr(),
+                                                    ws.numel(), levels.data_ptr(), signs.data_ptr(), norms.data_ptr(),
+                                                    _stream(dev)))
     return levels, signs, norms
 
 
@@ -140,18 +155,19 @@ def rqsgd_encode_batched(flat: torch.Tensor, layout: BucketLayout, bits: int, *,
                          uniforms: Optional[torch.Tensor] = None, seed: int = 0, counter: int = 0,
                          levels: Optional[torch.Tensor] = None, signs: Optional[torch.Tensor] = None,
                          norms: Optional[torch.Tensor] = None, mins: Optional[torch.Tensor] = None,
-                         ws: Optional[torch.Tensor] = None):
-    """RQSGD encode: (levels u8, signs i8, max|x| norms f32, min|x| factors f32)."""
+                         ws: Optional[torch.Tensor] = None, resident: Optional[bool] = None):
+    """RQSGD encode: (levels u8, signs i8, max|x| norms f32, min|x| factors f32). resident as for QSGD."""
     flat = _check_flat(flat, layout)
     dev = flat.device
     levels, signs = _planes(layout, dev, levels, signs, torch.uint8)
     norms = torch.empty(layout.ntensors, dtype=torch.float32, device=dev) if norms is None else norms
     mins = torch.empty(layout.ntensors, dtype=torch.float32, device=dev) if mins is None else mins
     ws = _ws(ws, layout, dev)
-    check(_lib.load().adfl_rqsgd_encode_batched(flat.data_ptr(), layout.device_chunks(dev).data_ptr(),
-                                                layout.nchunks, bits, _uniforms(uniforms, layout), seed, counter,
-                                                ws.data_ptr(), ws.numel(), levels.data_ptr(), signs.data_ptr(),
-                                                norms.data_ptr(), mins.data_ptr(), _stream(dev)))
+    check(_lib.load().adfl_rqsgd_encode_batched_work(flat.data_ptr(), layout.device_chunks(dev).data_ptr(),
+                                                     layout.nchunks, *_work(layout, dev, resident), bits,
+                                                     _uniforms(uniforms, layout), seed, counter, ws.data_ptr(),
+                                                     ws.numel(), levels.data_ptr(), signs.data_ptr(),
+                                                     norms.data_ptr(), mins.data_ptr(), _stream(dev)))
     return levels, signs, norms, mins
 
 
@@ -182,19 +198,20 @@ def cnat_encode_batched(flat: torch.Tensor, layout: BucketLayout, bits: int, *,
                         uniforms: Optional[torch.Tensor] = None, seed: int = 0, counter: int = 0,
                         exps: Optional[torch.Tensor] = None, signs: Optional[torch.Tensor] = None,
                         norms: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None,
-                        torch_norm: bool = False):
-    """CNAT encode (x read once): (exponents i8, signs i8, L2 norms f32). A tensor whose norm is 0 gets
-    the reference's zero-branch bytes (0 / 1). torch_norm=True then replaces the norms with torch's own
-    (the exponents do not depend on the norm; both norms are 0 for exactly the same tensors)."""
+                        torch_norm: bool = False, resident: Optional[bool] = None):
+    """CNAT encode (x read once; resident as for QSGD): (exponents i8, signs i8, L2 norms f32). A tensor
+    whose norm is 0 gets the reference's zero-branch bytes (0 / 1). torch_norm=True then replaces the norms
+    with torch's own (the exponents do not depend on the norm; both norms are 0 for exactly the same tensors)."""
     flat = _check_flat(flat, layout)
     dev = flat.device
     exps, signs = _planes(layout, dev, exps, signs, torch.int8)
     norms = torch.empty(layout.ntensors, dtype=torch.float32, device=dev) if norms is None else norms
     ws = _ws(ws, layout, dev)
-    check(_lib.load().adfl_cnat_encode_batched(flat.data_ptr(), layout.device_chunks(dev).data_ptr(), layout.nchunks,
-                                               bits, _uniforms(uniforms, layout), seed, counter, ws.data_ptr(),
-                                               ws.numel(), exps.data_ptr(), signs.data_ptr(), norms.data_ptr(),
-                                               _stream(dev)))
+    check(_lib.load().adfl_cnat_encode_batched_work(flat.data_ptr(), layout.device_chunks(dev).data_ptr(),
+                                                    layout.nchunks, *_work(layout, dev, resident), bits,
+                                                    _uniforms(uniforms, layout), seed, counter, ws.data_ptr(),
+                                                    ws.numel(), exps.data_ptr(), signs.data_ptr(), norms.data_ptr(),
+                                                    _stream(dev)))
     if torch_norm:
         norms_batched(flat, layout, NORM_L2_TORCH, norms=norms, ws=ws)
     return exps, signs, norms

@@ -56,6 +56,38 @@ __device__ __forceinline__ uint4 philox4x32_10(uint64_t ctr, uint64_t seed) {
 
 __device__ __forceinline__ float u24(uint32_t w) { return (float)(w >> 8) * 0x1p-24f; }
 
+// B independent Philox4x32-10 blocks with their rounds interleaved: a single block is a chain of 10
+// dependent 64-bit multiply rounds, which with only 4-5 waves per SIMD leaves the VALU waiting on latency
+// (tools/microbench_stoch_res.hip: 9.3 us of C3's resident QSGD encode); B chains in lockstep give the
+// scheduler B independent instructions per step. Same words as philox4x32_10, bit for bit.
+template <int B>
+__device__ __forceinline__ void philox4x32_10_batch(const uint64_t (&ctr)[B], uint64_t seed, uint4 (&out)[B]) {
+  uint32_t c0[B], c1[B], c2[B], c3[B];
+#pragma unroll
+  for (int i = 0; i < B; ++i) {
+    c0[i] = (uint32_t)ctr[i];
+    c1[i] = (uint32_t)(ctr[i] >> 32);
+    c2[i] = 0;
+    c3[i] = 0;
+  }
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+#pragma unroll
+    for (int i = 0; i < B; ++i) {
+      const uint64_t p0 = (uint64_t)0xD2511F53u * c0[i], p1 = (uint64_t)0xCD9E8D57u * c2[i];
+      c0[i] = (uint32_t)(p1 >> 32) ^ c1[i] ^ k0;
+      c1[i] = (uint32_t)p1;
+      c2[i] = (uint32_t)(p0 >> 32) ^ c3[i] ^ k1;
+      c3[i] = (uint32_t)p0;
+    }
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+#pragma unroll
+  for (int i = 0; i < B; ++i) out[i] = make_uint4(c0[i], c1[i], c2[i], c3[i]);
+}
+
 struct Uniforms {
   const float* inj;  // injected plane (indexed like x) or null
   uint64_t seed, counter;
@@ -274,16 +306,19 @@ __device__ __forceinline__ int chunk_head4(int64_t start, int len) {
 // issuing the next is latency-bound; blocks that walk a range of chunks serialise them and were slower
 // still (fresh blocks overlap one another's loads and compute).
 constexpr int kPer = ADFL_SLQ_CHUNK_ELEMS / 4 / kBlock;
+constexpr int kPbQuantize = 4;  // Philox blocks per batch in the multi-launch quantize kernels
+constexpr int kPbResident = 2;  // ... and in the resident encodes (their VGPRs hold two chunks per lane)
 constexpr int64_t kKeepBytes = 192ll << 20;  // x tail the norm pass leaves in the Infinity Cache
 constexpr int64_t kKeepChunks = kKeepBytes / (4 * ADFL_SLQ_CHUNK_ELEMS);
 
 // Per-element head / tail of a chunk: the < 4 elements before the first 4-element boundary and after the
 // last; thread t < head takes head element t, the next threads the tail elements. Returns -1 if none.
-__device__ __forceinline__ int edge_elem(int head, int tail, int len) {
-  const int t = threadIdx.x;
+__device__ __forceinline__ int edge_elem_t(int t, int head, int tail, int len) {
   if (t < head) return t;
   return (t - head < len - tail) ? tail + t - head : -1;
 }
+
+__device__ __forceinline__ int edge_elem(int head, int tail, int len) { return edge_elem_t(threadIdx.x, head, tail, len); }
 
 template <int MODE>
 struct NormAcc {
@@ -537,8 +572,9 @@ __global__ __launch_bounds__(64) void k_norm_torch_order(const float* __restrict
   if (lane == 0) norms[c.tensor] = (float)__builtin_sqrt((double)b);  // correctly rounded fp32 sqrt
 }
 
-__device__ __forceinline__ void fill_zero_norm(uint8_t* __restrict__ lv, int8_t* __restrict__ sg, int len) {
-  for (int i = threadIdx.x; i < len; i += kBlock) {
+__device__ __forceinline__ void fill_zero_norm(uint8_t* __restrict__ lv, int8_t* __restrict__ sg, int len,
+                                               int t = threadIdx.x) {
+  for (int i = t; i < len; i += kBlock) {
     lv[i] = 0;
     sg[i] = 1;
   }
@@ -546,46 +582,77 @@ __device__ __forceinline__ void fill_zero_norm(uint8_t* __restrict__ lv, int8_t*
 
 __device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0ull; }
 
-// The vector part of a quantize chunk: x (and injected uniforms) loaded up front, then per float4 group
-// the level / exponent bytes (fast form; exact form for the wave if any lane flagged its group) and the
-// sign bytes, stored as one dword each (contiguous across the wave). `all_exact` is block-uniform.
-template <class F, class E, class A>
-__device__ __forceinline__ void quantize_chunk_vec(const float4* __restrict__ x4, int n4, int64_t g0, const Uniforms& U,
-                                                   uint32_t* __restrict__ l4, uint32_t* __restrict__ s4, F fast,
-                                                   E exact, bool all_exact, A* acc) {
-  float4 v[kPer];
+// Quantize a chunk's float4 groups held in registers: v[j] is group tg + j * kBlock of the chunk (tg = the
+// thread's index in its 256-thread group). Per group the level / exponent bytes (fast form; exact form for
+// the wave if any lane flagged its group) and the sign bytes, stored as one dword each (contiguous across
+// the wave). `all_exact` is uniform over the group.
+// Philox uniforms are generated PB groups at a time (philox4x32_10_batch); injected uniforms (a test path)
+// are loaded group by group.
+// pre (LDS, or null): Philox words generated ahead of time, group j's at pre[j * pre_stride].
+template <int PB, class F, class E, class A>
+__device__ __forceinline__ void quantize_regs(const float4 (&v)[kPer], int tg, int n4, int64_t g0, const Uniforms& U,
+                                              uint32_t* __restrict__ l4, uint32_t* __restrict__ s4, F fast, E exact,
+                                              bool all_exact, A* acc, const uint4* pre = nullptr,
+                                              int pre_stride = 0) {
+  static_assert(kPer % PB == 0, "batches tile a chunk's groups");
 #pragma unroll
-  for (int j = 0; j < kPer; ++j) {
-    const int k = threadIdx.x + j * kBlock;
-    if (k < n4) v[j] = load4_nt(x4 + k);
-  }
-  float4 u[kPer];
-  if (U.inj) {
+  for (int jb = 0; jb < kPer; jb += PB) {
+    if (jb * kBlock >= n4) break;  // group-uniform: no thread has group jb or later
+    uint4 w[PB];
+    if (!U.inj && pre) {
 #pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-      const int k = threadIdx.x + j * kBlock;
-      if (k < n4) u[j] = U.group(g0 + 4 * (int64_t)k);
+      for (int i = 0; i < PB; ++i) w[i] = pre[(jb + i) * pre_stride];
+    } else if (!U.inj) {
+      uint64_t ctr[PB];
+#pragma unroll
+      for (int i = 0; i < PB; ++i) ctr[i] = U.counter + (uint64_t)((g0 >> 2) + tg + (jb + i) * kBlock);
+      philox4x32_10_batch(ctr, U.seed, w);
     }
-  }
 #pragma unroll
-  for (int j = 0; j < kPer; ++j) {
-    const int k = threadIdx.x + j * kBlock;
-    if (j * kBlock >= n4) break;  // block-uniform: no thread has group j
-    const bool live = k < n4;
-    const float4 uj = U.inj ? u[j] : U.group(g0 + 4 * (int64_t)k);
-    bool bad = all_exact;
-    uint32_t w = pack4(fast(v[j].x, uj.x, bad), fast(v[j].y, uj.y, bad), fast(v[j].z, uj.z, bad),
-                       fast(v[j].w, uj.w, bad));
-    if (wave_any(bad && live) && bad)
-      w = pack4(exact(v[j].x, uj.x), exact(v[j].y, uj.y), exact(v[j].z, uj.z), exact(v[j].w, uj.w));
-    if (live) {
-      l4[k] = w;
-      s4[k] = pack4(sign_byte(v[j].x), sign_byte(v[j].y), sign_byte(v[j].z), sign_byte(v[j].w));
-      if (acc) acc->add4(v[j]);
+    for (int i = 0; i < PB; ++i) {
+      const int j = jb + i;
+      const int k = tg + j * kBlock;
+      if (j * kBlock >= n4) break;  // group-uniform
+      const bool live = k < n4;
+      float4 uj;
+      if (!U.inj)
+        uj = make_float4(u24(w[i].x), u24(w[i].y), u24(w[i].z), u24(w[i].w));
+      else
+        uj = U.group(g0 + 4 * (int64_t)(live ? k : 0));
+      bool bad = all_exact;
+      uint32_t q = pack4(fast(v[j].x, uj.x, bad), fast(v[j].y, uj.y, bad), fast(v[j].z, uj.z, bad),
+                         fast(v[j].w, uj.w, bad));
+      if (wave_any(bad && live) && bad)
+        q = pack4(exact(v[j].x, uj.x), exact(v[j].y, uj.y), exact(v[j].z, uj.z), exact(v[j].w, uj.w));
+      if (live) {
+        l4[k] = q;
+        s4[k] = pack4(sign_byte(v[j].x), sign_byte(v[j].y), sign_byte(v[j].z), sign_byte(v[j].w));
+        if (acc) acc->add4(v[j]);
+      }
     }
   }
 }
 
+__device__ __forceinline__ void load_chunk_regs(const float4* __restrict__ x4, int n4, int tg, float4 (&v)[kPer]) {
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int k = tg + j * kBlock;
+    if (k < n4) v[j] = load4_nt(x4 + k);
+  }
+}
+
+// The vector part of a quantize chunk: x loaded up front, then quantize_regs.
+template <int PB, class F, class E, class A>
+__device__ __forceinline__ void quantize_chunk_vec(const float4* __restrict__ x4, int n4, int64_t g0, const Uniforms& U,
+                                                   uint32_t* __restrict__ l4, uint32_t* __restrict__ s4, F fast,
+                                                   E exact, bool all_exact, A* acc) {
+  float4 v[kPer];
+  load_chunk_regs(x4, n4, threadIdx.x, v);
+  quantize_regs<PB>(v, threadIdx.x, n4, g0, U, l4, s4, fast, exact, all_exact, acc);
+}
+
+// PB: Philox blocks generated per batch (philox4x32_10_batch); the product's choice is kPbQuantize.
+template <int PB>
 __global__ __launch_bounds__(kBlock) void k_qsgd_quantize(const float* __restrict__ x,
                                                           const adfl_slq_chunk* __restrict__ chunks, float s,
                                                           const float* __restrict__ norms, Uniforms U,
@@ -604,9 +671,9 @@ __global__ __launch_bounds__(kBlock) void k_qsgd_quantize(const float* __restric
   const int n4 = (c.len - head) >> 2;
   const auto fast = [&](float xv, float uv, bool& bad) { return qsgd_level_fast(xv, s, d, uv, bad); };
   const auto exact = [&](float xv, float uv) { return qsgd_level_exact(xv, s, norm, uv); };
-  quantize_chunk_vec(reinterpret_cast<const float4*>(xc + head), n4, c.start + head, U,
-                     reinterpret_cast<uint32_t*>(lv + head), reinterpret_cast<uint32_t*>(sg + head), fast, exact,
-                     !d.fast, (NormAcc<ADFL_NORM_L2>*)nullptr);
+  quantize_chunk_vec<PB>(reinterpret_cast<const float4*>(xc + head), n4, c.start + head, U,
+                         reinterpret_cast<uint32_t*>(lv + head), reinterpret_cast<uint32_t*>(sg + head), fast, exact,
+                         !d.fast, (NormAcc<ADFL_NORM_L2>*)nullptr);
   const int i = edge_elem(head, head + (n4 << 2), c.len);
   if (i >= 0) {
     lv[i] = (uint8_t)exact(xc[i], U.one(c.start + i));
@@ -615,6 +682,7 @@ __global__ __launch_bounds__(kBlock) void k_qsgd_quantize(const float* __restric
 }
 
 // CNAT: exponents + signs + the chunk's L2 partial in one read of x.
+template <int PB>
 __global__ __launch_bounds__(kBlock) void k_cnat_quantize(const float* __restrict__ x,
                                                           const adfl_slq_chunk* __restrict__ chunks, int min_e,
                                                           int max_e, Uniforms U, int8_t* __restrict__ exps,
@@ -628,9 +696,9 @@ __global__ __launch_bounds__(kBlock) void k_cnat_quantize(const float* __restric
   const auto fast = [=](float xv, float uv, bool& bad) { return cnat_exp_fast(xv, uv, min_e, max_e, bad); };
   const auto exact = [=](float xv, float uv) { return cnat_exp_exact(xv, uv, min_e, max_e); };
   NormAcc<ADFL_NORM_L2> acc;
-  quantize_chunk_vec(reinterpret_cast<const float4*>(xc + head), n4, c.start + head, U,
-                     reinterpret_cast<uint32_t*>(ex + head), reinterpret_cast<uint32_t*>(sg + head), fast, exact,
-                     false, &acc);
+  quantize_chunk_vec<PB>(reinterpret_cast<const float4*>(xc + head), n4, c.start + head, U,
+                         reinterpret_cast<uint32_t*>(ex + head), reinterpret_cast<uint32_t*>(sg + head), fast, exact,
+                         false, &acc);
   const int i = edge_elem(head, head + (n4 << 2), c.len);
   if (i >= 0) {
     const float v = xc[i];
@@ -648,6 +716,235 @@ __global__ __launch_bounds__(kBlock) void k_cnat_zero_fixup(const adfl_slq_chunk
   const adfl_slq_chunk c = chunks[blockIdx.x];
   if (norms[c.tensor] != 0.0f) return;
   fill_zero_norm(reinterpret_cast<uint8_t*>(exps) + c.start, signs + c.start, c.len);
+}
+
+// ---- one-launch encodes of a bucket of small tensors (a whole tensor per 1024-thread block) -------------
+// When every tensor of the bucket has at most ADFL_SLQ_RESIDENT_CHUNKS (8) chunks (the work list of
+// adfl_slq_build_encode_work holds each tensor's first chunk), one 1024-thread block takes one whole
+// tensor — 4 groups of 256 threads, group g takes chunks g and g + 4 — so the tensor's norm is a block
+// reduction and the encode is ONE launch instead of three:
+//  * QSGD / RQSGD (k_qsgd_encode_resident): the levels need the norm, so the block holds its whole tensor
+//    in VGPRs (16 float4 per lane), reduces the norm, then quantizes from the registers: x read once
+//    (6 B per element instead of 10);
+//  * CNAT (k_cnat_encode_resident): the exponents do not depend on the norm, so each group streams its
+//    chunks as k_cnat_quantize does (exponents + signs stored as they are made), and only an all-zero
+//    norm rewrites the tensor's bytes after the reduction — no finalize and no fix-up launch.
+// The outputs equal the multi-launch path's bit for bit: each group forms its chunks' L2 partials with
+// the same 256-thread arithmetic as k_norm_partials (QSGD: edge element first) or k_cnat_quantize (CNAT:
+// edge element last), the partials are summed in chunk order from 0.0 as finalize_small does, and the
+// Philox groups are indexed by bucket element as everywhere else.
+constexpr int kResBlock = 1024;
+constexpr int kResGroups = kResBlock / kBlock;                        // 4
+constexpr int kResPerGroup = ADFL_SLQ_RESIDENT_CHUNKS / kResGroups;  // 2
+constexpr int kResWaves = kResBlock / 64;
+static_assert(kResPerGroup * kResGroups == ADFL_SLQ_RESIDENT_CHUNKS, "groups cover a resident tensor");
+static_assert(ADFL_SLQ_RESIDENT_CHUNKS <= kSmallChunks, "partials summed in finalize_small's order");
+
+// The block's L2 norm from the per-wave partial sums red[r][wave] of chunk grp + 4r: each chunk's
+// partial as block_sum forms it over its group's 4 waves, summed in chunk order (finalize_small).
+__device__ __forceinline__ float resident_l2(const double (&red)[kResPerGroup][kResWaves], int nchunks) {
+  double t = 0.0;
+  for (int kc = 0; kc < nchunks; ++kc) {
+    const double* p = &red[kc / kResGroups][(kc % kResGroups) * kWaves];
+    t += (p[0] + p[1]) + (p[2] + p[3]);
+  }
+  return (float)__builtin_sqrt((double)(float)t);
+}
+
+template <int MODE, int PB>  // MODE ADFL_NORM_L2 (QSGD) or ADFL_NORM_LINF (RQSGD); PB as for k_qsgd_quantize
+__global__ __launch_bounds__(kResBlock) void k_qsgd_encode_resident(
+    const float* __restrict__ x, const adfl_slq_chunk* __restrict__ chunks, const int32_t* __restrict__ work,
+    float lev, Uniforms U, uint8_t* __restrict__ levels, int8_t* __restrict__ signs, float* __restrict__ norms,
+    float* __restrict__ mins) {
+  __shared__ double red_s[kResPerGroup][kResWaves];
+  __shared__ uint32_t red_mx[kResWaves], red_mn[kResWaves];
+  __shared__ uint4 pre[kPer][kResBlock];  // 128 KiB: the first chunk's Philox words, made while x streams in
+  const int64_t ci = work[blockIdx.x];
+  const adfl_slq_chunk ct = chunks[ci];
+  // group and wave are wave-uniform: in SGPRs, so the chunk metadata below is scalar
+  const int grp = __builtin_amdgcn_readfirstlane(threadIdx.x / kBlock);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tg = threadIdx.x % kBlock, lane = threadIdx.x & 63;
+  float4 v[kResPerGroup][kPer];
+  float ev[kResPerGroup];
+  int ei[kResPerGroup], n4s[kResPerGroup];
+#pragma unroll
+  for (int r = 0; r < kResPerGroup; ++r) {
+    const int kc = grp + r * kResGroups;
+    ei[r] = -1;
+    n4s[r] = 0;
+    ev[r] = 0.0f;
+    if (kc < ct.nchunks) {  // group-uniform
+      const adfl_slq_chunk c = chunks[ci + kc];
+      const int head = chunk_head4(c.start, c.len);
+      n4s[r] = (c.len - head) >> 2;
+      load_chunk_regs(reinterpret_cast<const float4*>(x + c.start + head), n4s[r], tg, v[r]);
+      ei[r] = edge_elem_t(tg, head, head + (n4s[r] << 2), c.len);
+      if (ei[r] >= 0) ev[r] = x[c.start + ei[r]];
+    }
+  }
+  // The quantize needs the norm, so without this the Philox work of the whole tensor would sit between the
+  // norm and the stores (about a third of the kernel on C3, tools/microbench_stoch_res.hip). Made here it
+  // overlaps the loads in flight; the first chunk's share fits the LDS (the second chunk's is made later).
+  if (!U.inj && grp < ct.nchunks) {
+    const adfl_slq_chunk c = chunks[ci + grp];
+    const int64_t q0 = (c.start + chunk_head4(c.start, c.len)) >> 2;
+#pragma unroll
+    for (int jb = 0; jb < kPer; jb += PB) {
+      if (jb * kBlock >= n4s[0]) break;  // group-uniform
+      uint64_t ctr[PB];
+      uint4 w[PB];
+#pragma unroll
+      for (int i = 0; i < PB; ++i) ctr[i] = U.counter + (uint64_t)(q0 + tg + (jb + i) * kBlock);
+      philox4x32_10_batch(ctr, U.seed, w);
+#pragma unroll
+      for (int i = 0; i < PB; ++i) pre[jb + i][threadIdx.x] = w[i];
+    }
+  }
+  float norm, mn = 0.0f;
+  if (MODE == ADFL_NORM_LINF) {  // max / min |x|: order-free
+    uint32_t mx = 0u, mi = 0xffffffffu;
+#pragma unroll
+    for (int r = 0; r < kResPerGroup; ++r) {
+      if (ei[r] >= 0) {
+        mx = max(mx, abs_bits(ev[r]));
+        mi = min(mi, abs_bits(ev[r]));
+      }
+#pragma unroll
+      for (int j = 0; j < kPer; ++j)
+        if (tg + j * kBlock < n4s[r]) {
+          const float4 a = v[r][j];
+          mx = max(mx, max(max(abs_bits(a.x), abs_bits(a.y)), max(abs_bits(a.z), abs_bits(a.w))));
+          mi = min(mi, min(min(abs_bits(a.x), abs_bits(a.y)), min(abs_bits(a.z), abs_bits(a.w))));
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+      mi = min(mi, (uint32_t)__shfl_xor((int)mi, o, 64));
+    }
+    if (lane == 0) {
+      red_mx[wave] = mx;
+      red_mn[wave] = mi;
+    }
+    __syncthreads();
+    mx = red_mx[0];
+    mi = red_mn[0];
+#pragma unroll
+    for (int w = 1; w < kResWaves; ++w) {
+      mx = max(mx, red_mx[w]);
+      mi = min(mi, red_mn[w]);
+    }
+    const bool nan = mx > 0x7f800000u;
+    norm = nan ? __builtin_nanf("") : __uint_as_float(mx);
+    mn = nan ? __builtin_nanf("") : __uint_as_float(mi);
+  } else {  // L2: k_norm_partials' per-chunk arithmetic (edge element first)
+#pragma unroll
+    for (int r = 0; r < kResPerGroup; ++r) {
+      double a = 0.0;
+      if (ei[r] >= 0) a += sq(ev[r]);
+#pragma unroll
+      for (int j = 0; j < kPer; ++j)
+        if (tg + j * kBlock < n4s[r]) a += (sq(v[r][j].x) + sq(v[r][j].y)) + (sq(v[r][j].z) + sq(v[r][j].w));
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+      if (lane == 0) red_s[r][wave] = a;
+    }
+    __syncthreads();
+    norm = resident_l2(red_s, ct.nchunks);
+  }
+  if (threadIdx.x == 0) {
+    norms[ct.tensor] = norm;
+    if (MODE == ADFL_NORM_LINF) mins[ct.tensor] = mn;
+  }
+  const Div d = make_div(norm);
+  const auto fast = [&](float xv, float uv, bool& bad) { return qsgd_level_fast(xv, lev, d, uv, bad); };
+  const auto exact = [&](float xv, float uv) { return qsgd_level_exact(xv, lev, norm, uv); };
+#pragma unroll
+  for (int r = 0; r < kResPerGroup; ++r) {
+    const int kc = grp + r * kResGroups;
+    if (kc >= ct.nchunks) continue;  // group-uniform
+    const adfl_slq_chunk c = chunks[ci + kc];
+    uint8_t* lv = levels + c.start;
+    int8_t* sg = signs + c.start;
+    if (norm == 0.0f) {  // quant.py:227-228
+      fill_zero_norm(lv, sg, c.len, tg);
+      continue;
+    }
+    const int head = chunk_head4(c.start, c.len);
+    quantize_regs<PB>(v[r], tg, n4s[r], c.start + head, U, reinterpret_cast<uint32_t*>(lv + head),
+                      reinterpret_cast<uint32_t*>(sg + head), fast, exact, !d.fast, (NormAcc<ADFL_NORM_L2>*)nullptr,
+                      r == 0 ? &pre[0][threadIdx.x] : nullptr, kResBlock);
+    if (ei[r] >= 0) {
+      lv[ei[r]] = (uint8_t)exact(ev[r], U.one(c.start + ei[r]));
+      sg[ei[r]] = (int8_t)sign_byte(ev[r]);
+    }
+  }
+}
+
+template <int PB>
+__global__ __launch_bounds__(kResBlock) void k_cnat_encode_resident(
+    const float* __restrict__ x, const adfl_slq_chunk* __restrict__ chunks, const int32_t* __restrict__ work,
+    int min_e, int max_e, Uniforms U, int8_t* __restrict__ exps, int8_t* __restrict__ signs,
+    float* __restrict__ norms) {
+  __shared__ double red_s[kResPerGroup][kResWaves];
+  const int64_t ci = work[blockIdx.x];
+  const adfl_slq_chunk ct = chunks[ci];
+  const int grp = __builtin_amdgcn_readfirstlane(threadIdx.x / kBlock);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tg = threadIdx.x % kBlock, lane = threadIdx.x & 63;
+  const auto fast = [=](float xv, float uv, bool& bad) { return cnat_exp_fast(xv, uv, min_e, max_e, bad); };
+  const auto exact = [=](float xv, float uv) { return cnat_exp_exact(xv, uv, min_e, max_e); };
+  // both chunks' loads issued up front: the second chunk streams in while the first one is quantized
+  float4 v[kResPerGroup][kPer];
+  int n4s[kResPerGroup];
+#pragma unroll
+  for (int r = 0; r < kResPerGroup; ++r) {
+    const int kc = grp + r * kResGroups;
+    n4s[r] = 0;
+    if (kc < ct.nchunks) {  // group-uniform
+      const adfl_slq_chunk c = chunks[ci + kc];
+      const int head = chunk_head4(c.start, c.len);
+      n4s[r] = (c.len - head) >> 2;
+      load_chunk_regs(reinterpret_cast<const float4*>(x + c.start + head), n4s[r], tg, v[r]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < kResPerGroup; ++r) {  // k_cnat_quantize per chunk, its partial kept in LDS
+    const int kc = grp + r * kResGroups;
+    NormAcc<ADFL_NORM_L2> acc;
+    if (kc < ct.nchunks) {
+      const adfl_slq_chunk c = chunks[ci + kc];
+      const float* xc = x + c.start;
+      int8_t* ex = exps + c.start;
+      int8_t* sg = signs + c.start;
+      const int head = chunk_head4(c.start, c.len);
+      quantize_regs<PB>(v[r], tg, n4s[r], c.start + head, U, reinterpret_cast<uint32_t*>(ex + head),
+                        reinterpret_cast<uint32_t*>(sg + head), fast, exact, false, &acc);
+      const int i = edge_elem_t(tg, head, head + (n4s[r] << 2), c.len);
+      if (i >= 0) {
+        const float e = xc[i];
+        ex[i] = (int8_t)exact(e, U.one(c.start + i));
+        sg[i] = (int8_t)sign_byte(e);
+        acc.add(e);
+      }
+    }
+    double a = acc.s;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+    if (lane == 0) red_s[r][wave] = a;
+  }
+  __syncthreads();  // also orders this block's byte stores before the zero-norm rewrite below
+  const float norm = resident_l2(red_s, ct.nchunks);
+  if (threadIdx.x == 0) norms[ct.tensor] = norm;
+  if (norm != 0.0f) return;  // block-uniform
+#pragma unroll
+  for (int r = 0; r < kResPerGroup; ++r) {  // quant.py:513-514: u8 zeros, int8 ones
+    const int kc = grp + r * kResGroups;
+    if (kc >= ct.nchunks) continue;
+    const adfl_slq_chunk c = chunks[ci + kc];
+    fill_zero_norm(reinterpret_cast<uint8_t*>(exps) + c.start, signs + c.start, c.len, tg);
+  }
 }
 
 __device__ __forceinline__ void store4_nt(float4* p, float4 d) {
@@ -767,6 +1064,32 @@ inline int launch_finalize(const adfl_slq_chunk* d_chunks, int64_t nchunks, cons
   return launch_status();
 }
 
+// KIND 0 QSGD, 1 RQSGD, 2 CNAT (d_a = levels, or CNAT's exponent bytes)
+template <int KIND>
+inline int launch_resident(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, const int32_t* d_work,
+                           int64_t nwork, int bits, const float* d_uniforms, uint64_t seed, uint64_t counter,
+                           uint8_t* d_a, int8_t* d_signs, float* d_norms, float* d_mins, void* stream) {
+  if (!d_x || !d_work || !d_a || !d_signs || !d_norms || (KIND == 1 && !d_mins) || bad_table(d_chunks, nchunks) ||
+      nwork < 1 || nwork > nchunks)
+    return ADFL_E_ARG;
+  if (int s = check_bits(bits)) return s;
+  if (!aligned16(d_x) || !aligned16(d_a) || !aligned16(d_signs) || (d_uniforms && !aligned16(d_uniforms)))
+    return ADFL_E_ALIGN;
+  const Uniforms U{d_uniforms, seed, counter};
+  const dim3 grid((unsigned)nwork), block(kResBlock);
+  hipStream_t st = (hipStream_t)stream;
+  if (KIND == 2) {
+    const int min_e = -(1 << (bits - 1)), max_e = (1 << (bits - 1)) - 1;  // quant.py:519-520
+    hipLaunchKernelGGL(k_cnat_encode_resident<kPbResident>, grid, block, 0, st, d_x, d_chunks, d_work, min_e, max_e, U,
+                       reinterpret_cast<int8_t*>(d_a), d_signs, d_norms);
+  } else {
+    constexpr int mode = KIND == 1 ? ADFL_NORM_LINF : ADFL_NORM_L2;
+    hipLaunchKernelGGL((k_qsgd_encode_resident<mode, kPbResident>), grid, block, 0, st, d_x, d_chunks, d_work,
+                       levels_f(bits), U, d_a, d_signs, d_norms, d_mins);
+  }
+  return launch_status();
+}
+
 }  // namespace
 
 // ================================================================================================
@@ -808,7 +1131,7 @@ int adfl_qsgd_quantize_batched(const float* d_x, const adfl_slq_chunk* d_chunks,
   if (!aligned16(d_x) || !aligned16(d_levels) || !aligned16(d_signs) || (d_uniforms && !aligned16(d_uniforms)))
     return ADFL_E_ALIGN;
   const Uniforms U{d_uniforms, seed, counter};
-  hipLaunchKernelGGL(k_qsgd_quantize, dim3((unsigned)nchunks), dim3(kBlock), 0, (hipStream_t)stream, d_x, d_chunks,
+  hipLaunchKernelGGL(k_qsgd_quantize<kPbQuantize>, dim3((unsigned)nchunks), dim3(kBlock), 0, (hipStream_t)stream, d_x, d_chunks,
                      levels_f(bits), d_norms, U, d_levels, d_signs);
   return launch_status();
 }
@@ -871,7 +1194,7 @@ int adfl_cnat_encode_batched(const float* d_x, const adfl_slq_chunk* d_chunks, i
   hipStream_t st = (hipStream_t)stream;
   const Uniforms U{d_uniforms, seed, counter};
   const int min_e = -(1 << (bits - 1)), max_e = (1 << (bits - 1)) - 1;  // quant.py:519-520
-  hipLaunchKernelGGL(k_cnat_quantize, dim3((unsigned)nchunks), dim3(kBlock), 0, st, d_x, d_chunks, min_e, max_e, U,
+  hipLaunchKernelGGL(k_cnat_quantize<kPbQuantize>, dim3((unsigned)nchunks), dim3(kBlock), 0, st, d_x, d_chunks, min_e, max_e, U,
                      d_exps, d_signs, (double*)d_workspace);
   if (int s = launch_status()) return s;
   if (int s = launch_finalize<ADFL_NORM_L2>(d_chunks, nchunks, d_workspace, d_norms, nullptr, st)) return s;
@@ -888,6 +1211,39 @@ int adfl_cnat_dequantize_batched(const int8_t* d_exps, const int8_t* d_signs, co
                      reinterpret_cast<const uint8_t*>(d_exps), d_signs, d_chunks, d_norms, (const float*)nullptr,
                      1.0f, d_out);
   return launch_status();
+}
+
+int adfl_qsgd_encode_batched_work(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks,
+                                  const int32_t* d_work, int64_t nwork, int bits, const float* d_uniforms,
+                                  uint64_t seed, uint64_t counter, void* d_workspace, int64_t workspace_bytes,
+                                  uint8_t* d_levels, int8_t* d_signs, float* d_norms, void* stream) {
+  if (nwork == 0)
+    return adfl_qsgd_encode_batched(d_x, d_chunks, nchunks, bits, d_uniforms, seed, counter, d_workspace,
+                                    workspace_bytes, d_levels, d_signs, d_norms, stream);
+  return launch_resident<0>(d_x, d_chunks, nchunks, d_work, nwork, bits, d_uniforms, seed, counter, d_levels, d_signs,
+                            d_norms, nullptr, stream);
+}
+
+int adfl_rqsgd_encode_batched_work(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks,
+                                   const int32_t* d_work, int64_t nwork, int bits, const float* d_uniforms,
+                                   uint64_t seed, uint64_t counter, void* d_workspace, int64_t workspace_bytes,
+                                   uint8_t* d_levels, int8_t* d_signs, float* d_norms, float* d_mins, void* stream) {
+  if (nwork == 0)
+    return adfl_rqsgd_encode_batched(d_x, d_chunks, nchunks, bits, d_uniforms, seed, counter, d_workspace,
+                                     workspace_bytes, d_levels, d_signs, d_norms, d_mins, stream);
+  return launch_resident<1>(d_x, d_chunks, nchunks, d_work, nwork, bits, d_uniforms, seed, counter, d_levels, d_signs,
+                            d_norms, d_mins, stream);
+}
+
+int adfl_cnat_encode_batched_work(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks,
+                                  const int32_t* d_work, int64_t nwork, int bits, const float* d_uniforms,
+                                  uint64_t seed, uint64_t counter, void* d_workspace, int64_t workspace_bytes,
+                                  int8_t* d_exps, int8_t* d_signs, float* d_norms, void* stream) {
+  if (nwork == 0)
+    return adfl_cnat_encode_batched(d_x, d_chunks, nchunks, bits, d_uniforms, seed, counter, d_workspace,
+                                    workspace_bytes, d_exps, d_signs, d_norms, stream);
+  return launch_resident<2>(d_x, d_chunks, nchunks, d_work, nwork, bits, d_uniforms, seed, counter,
+                            reinterpret_cast<uint8_t*>(d_exps), d_signs, d_norms, nullptr, stream);
 }
 
 int adfl_philox_uniforms(float* d_out, int64_t n, int64_t start, uint64_t seed, uint64_t counter, void* stream) {

@@ -94,6 +94,24 @@ int adfl_cnat_encode_batched(const float* d_x, const adfl_slq_chunk* d_chunks, i
 int adfl_cnat_dequantize_batched(const int8_t* d_exps, const int8_t* d_signs, const adfl_slq_chunk* d_chunks,
                                  int64_t nchunks, const float* d_norms, float* d_out, void* stream);
 
+/* One-launch encodes (same outputs, bit for bit) for a bucket whose tensors ALL have at most
+ * ADFL_SLQ_RESIDENT_CHUNKS chunks: d_work / nwork is the work list of adfl_slq_build_encode_work (the first
+ * chunk of every tensor; nwork == 0 when some tensor is larger). A 1024-thread block holds one whole tensor
+ * in registers, reduces its norm and quantizes it: x read once, no workspace, no fix-up launch. With
+ * nwork == 0 these run the multi-launch encodes above (which need the workspace). */
+int adfl_qsgd_encode_batched_work(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks,
+                                  const int32_t* d_work, int64_t nwork, int bits, const float* d_uniforms,
+                                  uint64_t seed, uint64_t counter, void* d_workspace, int64_t workspace_bytes,
+                                  uint8_t* d_levels, int8_t* d_signs, float* d_norms, void* stream);
+int adfl_rqsgd_encode_batched_work(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks,
+                                   const int32_t* d_work, int64_t nwork, int bits, const float* d_uniforms,
+                                   uint64_t seed, uint64_t counter, void* d_workspace, int64_t workspace_bytes,
+                                   uint8_t* d_levels, int8_t* d_signs, float* d_norms, float* d_mins, void* stream);
+int adfl_cnat_encode_batched_work(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks,
+                                  const int32_t* d_work, int64_t nwork, int bits, const float* d_uniforms,
+                                  uint64_t seed, uint64_t counter, void* d_workspace, int64_t workspace_bytes,
+                                  int8_t* d_exps, int8_t* d_signs, float* d_norms, void* stream);
+
 /* The Philox uniforms the codecs draw: d_out[i] = u(start + i) of stream (seed, counter), i < n.
  * (Exposed for tests and for callers that want the uniforms a call used.) */
 int adfl_philox_uniforms(float* d_out, int64_t n, int64_t start, uint64_t seed, uint64_t counter, void* stream);
