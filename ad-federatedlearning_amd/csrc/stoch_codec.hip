@@ -76,7 +76,7 @@ __device__ __forceinline__ void philox4x32_10_batch(const uint64_t (&ctr)[B], ui
 #pragma unroll
     for (int i = 0; i < B; ++i) {
       const uint64_t p0 = (uint64_t)0xD2511F53u * c0[i], p1 = (uint64_t)0xCD9E8D57u * c2[i];
-      c0[i] = (uint32_t)(p1 >> 32) ^ c1[i] ^ k0;
+      c0[i] = (uint32_t)(p1 >> 32) ^ c1[i] ^ k0;  // no v_xor3_b32 on gfx950: two v_xor_b32
       c1[i] = (uint32_t)p1;
       c2[i] = (uint32_t)(p0 >> 32) ^ c3[i] ^ k1;
       c3[i] = (uint32_t)p0;

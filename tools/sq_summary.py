@@ -14,7 +14,7 @@ def main(path, elems_json=None):
     elems = json.load(open(elems_json)) if elems_json else {}
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     for r in csv.DictReader(open(path)):
-        name = r["Kernel_Name"].split("(")[0].replace("(anonymous namespace)::", "").replace("void ", "")
+        name = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
         key = (name, int(r["Grid_Size"]))
         acc[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
     for (name, grid), cs in sorted(acc.items(), key=lambda kv: kv[0]):
