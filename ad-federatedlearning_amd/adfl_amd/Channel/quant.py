@@ -28,6 +28,7 @@ import time
 from collections import OrderedDict
 from typing import Dict, List, Optional, Tuple
 
+import numpy as np
 import torch
 
 from .. import hostcopy, ops
@@ -115,18 +116,30 @@ def _gather(tensors: List[torch.Tensor], lay: ops.BucketLayout, out: torch.Tenso
 _PIECE_BYTES = 8 << 20  # staging pieces of at least this size: one gather + one H2D each
 
 
-def _pieces(lay: ops.BucketLayout, elem_bytes: int) -> List[Tuple[int, int]]:
-    """Split the tensors of `lay` into consecutive runs [a, b) of about max(_PIECE_BYTES, total / 4) bytes."""
-    target = max(_PIECE_BYTES, lay.total * elem_bytes // 4)
-    out, a, acc = [], 0, 0
-    for i, n in enumerate(lay.padded.tolist()):
-        acc += n * elem_bytes
-        if acc >= target:
-            out.append((a, i + 1))
-            a, acc = i + 1, 0
-    if a < lay.ntensors:
-        out.append((a, lay.ntensors))
-    return out
+def _ranges(lay: ops.BucketLayout, elem_bytes: int) -> List[Tuple[int, int]]:
+    """The bucket split into element ranges [lo, hi) of about max(_PIECE_BYTES, total / 4) bytes. Ranges
+    may cut through a tensor (one 1 GiB tensor still stages in pipelined pieces)."""
+    step = max(_PIECE_BYTES // elem_bytes, -(-lay.total // 4))
+    return [(lo, min(lo + step, lay.total)) for lo in range(0, lay.total, step)]
+
+
+def _range_copies(ptrs: np.ndarray, lay: ops.BucketLayout, base: int, es: int, lo: int, hi: int, to_bucket: bool):
+    """Byte-copy lists moving bucket elements [lo, hi) between the host bucket at `base` and the tensors
+    whose data pointers are `ptrs` (tensor k at lay.offsets[k]; pads are never copied)."""
+    starts = lay.offsets
+    ends = lay.offsets + lay.sizes
+    a = np.maximum(starts, lo)
+    b = np.minimum(ends, hi)
+    k = np.nonzero(a < b)[0]
+    a, b = a[k], b[k]
+    t_ptr = (ptrs[k] + ((a - starts[k]) * es).astype(np.uint64)).astype(np.uint64)
+    b_ptr = (np.uint64(base) + (a * es).astype(np.uint64)).astype(np.uint64)
+    nbytes = ((b - a) * es).astype(np.int64)
+    return (b_ptr, t_ptr, nbytes) if to_bucket else (t_ptr, b_ptr, nbytes)
+
+
+def _ptrs(tensors: List[torch.Tensor]) -> np.ndarray:
+    return np.fromiter((t.data_ptr() for t in tensors), dtype=np.uint64, count=len(tensors))
 
 
 def _stage_in(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _DeviceStaging, key: str,
@@ -136,15 +149,14 @@ def _stage_in(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _DeviceSta
     kinds = {t.is_cuda for t in tensors}
     if kinds == {False}:
         host = st.buf(key + "_host", lay.total, dtype, pinned=True)
-        if all(t.is_contiguous() for t in tensors):
-            # Native parallel gather (csrc/host_copy.cpp) in tensor-aligned pieces, each piece's H2D
-            # enqueued as soon as it is staged so the copy engine overlaps the next piece's host copy.
-            # Pads of an aligned layout are never read.
-            offs = lay.offsets.tolist()
-            for a, b in _pieces(lay, host.element_size()):
-                hostcopy.gather(tensors[a:b], host, offs[a:b])
-                lo = offs[a]
-                hi = offs[b] if b < len(offs) else lay.total
+        es = host.element_size()
+        if all(t.is_contiguous() and t.element_size() == es for t in tensors):
+            # Native parallel gather (csrc/host_copy.cpp) in element ranges, each range's H2D enqueued as
+            # soon as it is staged so the copy engine overlaps the next range's host copy. Pads of an
+            # aligned layout are never read.
+            ptrs = _ptrs(tensors)
+            for lo, hi in _ranges(lay, es):
+                hostcopy.copy_pieces(*_range_copies(ptrs, lay, host.data_ptr(), es, lo, hi, to_bucket=True))
                 dev_buf[lo:hi].copy_(host[lo:hi], non_blocking=True)
         else:
             _gather(tensors, lay, host)
@@ -157,30 +169,40 @@ def _stage_in(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _DeviceSta
     return dev_buf
 
 
-def _piece_bounds(lay: ops.BucketLayout, a: int, b: int, offs: List[int]) -> Tuple[int, int]:
-    return offs[a], (offs[b] if b < len(offs) else lay.total)
+class _PendingD2H:
+    """D2H of a device bucket into the reused pinned staging, enqueued range by range with an event each;
+    finish() scatters every range into the per-tensor CPU storages as soon as its copy lands (the native
+    pool copies while the copy engine moves the next range). Whatever the caller does between the two —
+    allocating the output tensors — overlaps the copies."""
+
+    def __init__(self, dev_buf: torch.Tensor, lay: ops.BucketLayout, st: _DeviceStaging, key: str):
+        self.host = st.buf(key + "_host", lay.total, dev_buf.dtype, pinned=True)
+        self.lay = lay
+        stream = torch.cuda.current_stream(st.device)
+        self.ranges = _ranges(lay, self.host.element_size())
+        self.events = []
+        for lo, hi in self.ranges:
+            self.host[lo:hi].copy_(dev_buf[lo:hi], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            self.events.append(ev)
+
+    def finish(self, outs: List[torch.Tensor]) -> None:
+        """outs: contiguous CPU tensors owned by the caller, tensor k receiving bucket elements at offsets[k]."""
+        es = self.host.element_size()
+        for t in outs:
+            if t.is_cuda or not t.is_contiguous() or t.element_size() != es:
+                raise ValueError("staging: outputs must be contiguous CPU tensors of the bucket's element size")
+        ptrs = _ptrs(outs)
+        for (lo, hi), ev in zip(self.ranges, self.events):
+            ev.synchronize()
+            hostcopy.copy_pieces(*_range_copies(ptrs, self.lay, self.host.data_ptr(), es, lo, hi, to_bucket=False))
 
 
 def _stage_out(dev_buf: torch.Tensor, lay: ops.BucketLayout, st: _DeviceStaging, key: str,
                outs: List[torch.Tensor]) -> None:
-    """Copy the bucket `dev_buf` (on the device) into the per-tensor CPU storages `outs` (contiguous, owned
-    by the caller; tensor k at lay.offsets[k]): tensor-aligned pieces go D2H into a reused pinned staging
-    buffer, and each piece is scattered into its tensors by the native pool as soon as its copy lands,
-    while the copy engine moves the next piece."""
-    host = st.buf(key + "_host", lay.total, dev_buf.dtype, pinned=True)
-    stream = torch.cuda.current_stream(st.device)
-    offs = lay.offsets.tolist()
-    pieces = _pieces(lay, host.element_size())
-    events = []
-    for a, b in pieces:
-        lo, hi = _piece_bounds(lay, a, b, offs)
-        host[lo:hi].copy_(dev_buf[lo:hi], non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record(stream)
-        events.append(ev)
-    for (a, b), ev in zip(pieces, events):
-        ev.synchronize()
-        hostcopy.scatter(host, outs[a:b], offs[a:b])
+    """Copy the bucket `dev_buf` (on the device) into the per-tensor CPU storages `outs` (_PendingD2H)."""
+    _PendingD2H(dev_buf, lay, st, key).finish(outs)
 
 
 def _hand_out(out_dev: torch.Tensor, lay: ops.BucketLayout, shapes: List[torch.Size], on_cpu: List[bool],
@@ -188,24 +210,22 @@ def _hand_out(out_dev: torch.Tensor, lay: ops.BucketLayout, shapes: List[torch.S
     """Decoded tensors as the reference returns them (quant.py:107-112): one new, owned, writable tensor
     per entry — pageable CPU tensors for CPU payloads, device tensors for device payloads — never views
     of a shared bucket (a strategy keeps single updates alive, Src/ADFL/Strategy/fed_buff.py:75,90, and
-    pickling one must not ship the whole bucket)."""
+    pickling one must not ship the whole bucket). For an all-CPU dict the D2H is enqueued first and the
+    output tensors are allocated while it runs."""
     outs: List[Optional[torch.Tensor]] = [None] * len(shapes)
-    if any(on_cpu):
+    if all(on_cpu):
+        pending = _PendingD2H(out_dev, lay, st, key)
         host_outs = [torch.empty(s, dtype=out_dev.dtype) for s in shapes]
-        if all(on_cpu):
-            _stage_out(out_dev, lay, st, key, host_outs)
-        else:  # mixed host / device dict (rare): per-tensor copies
-            for i, (off, n) in enumerate(zip(lay.offsets.tolist(), lay.sizes.tolist())):
-                if on_cpu[i]:
-                    host_outs[i].view(-1).copy_(out_dev[off:off + n])
-        for i, cpu in enumerate(on_cpu):
-            if cpu:
-                outs[i] = host_outs[i]
-    if not all(on_cpu):
-        for i, (off, n, s) in enumerate(zip(lay.offsets.tolist(), lay.sizes.tolist(), shapes)):
-            if not on_cpu[i]:
-                outs[i] = out_dev[off:off + n].view(s).clone()
-        torch.cuda.current_stream(st.device).synchronize()
+        hostcopy.advise_huge(host_outs)
+        pending.finish(host_outs)
+        return host_outs
+    for i, (off, n, s) in enumerate(zip(lay.offsets.tolist(), lay.sizes.tolist(), shapes)):
+        if on_cpu[i]:  # mixed host / device dict (rare): per-tensor copies
+            outs[i] = torch.empty(s, dtype=out_dev.dtype)
+            outs[i].view(-1).copy_(out_dev[off:off + n])
+        else:
+            outs[i] = out_dev[off:off + n].view(s).clone()
+    torch.cuda.current_stream(st.device).synchronize()
     return outs
 
 
@@ -227,16 +247,23 @@ def _encode_dict(params: Parameters, names: List[str], bits: int, stats: Optiona
         stats.extend(ops.qerror_batched(x_dev, q_dev, s_dev, lay))
     scales_host = st.buf("scales_host", lay.ntensors, torch.float32, pinned=True)
     scales_host.copy_(s_dev, non_blocking=True)
-    torch.cuda.current_stream(dev).synchronize()
-    scales = scales_host.tolist()
     on_cpu = [not t.is_cuda for t in tensors]
     if all(on_cpu):
         # every payload tensor owns its bytes (compact pickles; the staging buffer is reused by the next
-        # call): empty qint8 tensors filled by the pipelined D2H + native scatter
+        # call): the payload D2H is enqueued right behind the scales, and the qint8 tensors (which need the
+        # scales) are allocated while it runs, then filled by the native scatter as its ranges land
+        scales_ready = torch.cuda.Event()
+        scales_ready.record(torch.cuda.current_stream(dev))
+        pending = _PendingD2H(q_dev, lay, st, "q")
+        scales_ready.synchronize()
+        scales = scales_host.tolist()
         qs = [torch._empty_affine_quantized(t.shape, scale=sc, zero_point=0, dtype=torch.qint8)
               for t, sc in zip(tensors, scales)]
-        _stage_out(q_dev, lay, st, "q", qs)
+        hostcopy.advise_huge(qs)
+        pending.finish(qs)
         return {name: (qt, sc) for name, qt, sc in zip(names, qs, scales)}
+    torch.cuda.current_stream(dev).synchronize()
+    scales = scales_host.tolist()
     out = {}
     offs, sizes = lay.offsets.tolist(), lay.sizes.tolist()
     for i, (name, t) in enumerate(zip(names, tensors)):

@@ -53,6 +53,7 @@ def _owned(parts: List[torch.Tensor], shapes: List[torch.Size]) -> List[torch.Te
 def _owned_host(buf: torch.Tensor, offsets, shapes: List[torch.Size]) -> List[torch.Tensor]:
     """_owned for a host bucket: fresh tensors filled by one native parallel scatter."""
     outs = [torch.empty(s, dtype=buf.dtype) for s in shapes]
+    hostcopy.advise_huge(outs)
     hostcopy.scatter(buf, outs, offsets)
     return outs
 

@@ -64,3 +64,43 @@ def test_argument_errors():
     assert lib.adfl_host_copy(None, None, None, 0, 0) == 0
     with pytest.raises(ValueError):
         hostcopy.gather([torch.zeros(4, dtype=torch.float64)], torch.zeros(8), [0])
+
+
+@pytest.mark.parametrize("align", [1, 64])
+@pytest.mark.parametrize("sizes,piece", [([5, 3_000_000, 17, 65_536, 1], 1 << 20), ([1 << 22], 1 << 20),
+                                         ([64] * 500 + [999_999], 1 << 16)])
+def test_channel_staging_ranges_cut_through_tensors(sizes, piece, align, monkeypatch):
+    """The Channel's host staging (Channel/quant.py _ranges / _range_copies): element ranges that cut through
+    tensors gather into the bucket and scatter back exactly, pads untouched, every element once."""
+    from adfl_amd import ops
+    from adfl_amd.Channel import quant
+    monkeypatch.setattr(quant, "_PIECE_BYTES", piece)
+    lay = ops.BucketLayout(sizes, align=align)
+    rng = np.random.default_rng(7)
+    srcs = [torch.from_numpy(rng.standard_normal(n).astype(np.float32)) for n in sizes]
+    bucket = torch.full((lay.total,), -7.0)
+    ranges = quant._ranges(lay, 4)
+    assert ranges[0][0] == 0 and ranges[-1][1] == lay.total
+    assert all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
+    ptrs = quant._ptrs(srcs)
+    for lo, hi in ranges:
+        hostcopy.copy_pieces(*quant._range_copies(ptrs, lay, bucket.data_ptr(), 4, lo, hi, to_bucket=True))
+    want = np.full(lay.total, -7.0, np.float32)
+    for s, o in zip(srcs, lay.offsets):
+        want[o:o + s.numel()] = s.numpy()
+    assert np.array_equal(bucket.numpy(), want)
+    outs = [torch.empty(n) for n in sizes]
+    optr = quant._ptrs(outs)
+    for lo, hi in reversed(ranges):
+        hostcopy.copy_pieces(*quant._range_copies(optr, lay, bucket.data_ptr(), 4, lo, hi, to_bucket=False))
+    for a, b in zip(outs, srcs):
+        assert torch.equal(a, b)
+
+
+def test_advise_huge_is_advice_only():
+    """hostcopy.advise_huge never changes bytes or raises (small, large, unaligned, device-less tensors)."""
+    ts = [torch.arange(10, dtype=torch.float32), torch.zeros(3 << 20), torch.empty(5 << 20, dtype=torch.int8)[1:]]
+    hostcopy.advise_huge(ts)
+    ts[2].fill_(3)
+    assert torch.equal(ts[0], torch.arange(10, dtype=torch.float32)) and int(ts[1].abs().sum()) == 0
+    assert int(ts[2].sum()) == 3 * ((5 << 20) - 1)
