@@ -6,7 +6,7 @@ half the bytes of a 16-B-per-lane streaming read; WRITE_SIZE is exact for 16-B-p
 Byte-plane stores of 4 B per lane are uncalibrated (the guide's caveat): ratios between variants still hold.
 
     python tools/pmc_kernels.py FETCH.csv WRITE.csv [alg.json] > out.json
-    alg.json: {"<kernel substring>@<grid>": algorithmic bytes per launch, ...}
+    alg.json: {"<kernel name>@<grid>": algorithmic bytes per launch, ...}
 """
 import collections
 import csv
@@ -37,7 +37,7 @@ def main(fetch_csv, write_csv, alg_json=None):
                "write_size_kib": round(write[key], 1), "hbm_bytes_per_launch": int(hbm)}
         for k, v in alg.items():
             sub, g = k.rsplit("@", 1)
-            if sub in name and int(g) == grid:
+            if sub == name and int(g) == grid:
                 row["alg_bytes_per_launch"] = v
                 row["traffic_over_alg"] = round(hbm / v, 4)
         out.append(row)
