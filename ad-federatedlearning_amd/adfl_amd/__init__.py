@@ -5,7 +5,8 @@ Layout mirrors the reference's ``Src/ADFL`` package for the one hot path this re
 * ``adfl_amd.Channel``      ``Channel``, ``IdentityChannel``, ``SLQChannel``, ``USLQChannel``
                             (drop-in for ``ADFL.Channel``; HIP-backed SLQ)
 * ``adfl_amd.model``        payload dataclasses + ``get_parameter_info`` (``ADFL.model``)
-* ``adfl_amd.compression``  ``pack_4bit`` / ``unpack_4bit`` (``ADFL.compression``) on the GPU
+* ``adfl_amd.compression``  ``quantize_tensor`` / ``dequantize_tensor`` / ``pack_4bit`` / ``unpack_4bit``
+                            (``ADFL.compression``'s hot-path functions) on the GPU
 * ``adfl_amd.ops``          device-resident codec ops; ``torch.ops.adfl.*`` custom ops
 * ``adfl_amd.exchange``     one-client-per-GPU peer exchange: encode -> RCCL all-gather -> mean
 
@@ -17,9 +18,10 @@ from . import _lib
 
 _lib.load()
 
-from . import model, ops, stoch  # noqa: E402
+from . import compression, model, ops, stoch  # noqa: E402
 from .Channel import (Channel, CNATChannel, IdentityChannel, PackedSLQChannel, QSGDChannel,  # noqa: E402
                       RQSGDChannel, SLQChannel, UCNATChannel, UQSGDChannel, URQSGDChannel, USLQChannel)
 
 __all__ = ["Channel", "IdentityChannel", "SLQChannel", "USLQChannel", "PackedSLQChannel", "QSGDChannel",
-           "UQSGDChannel", "RQSGDChannel", "URQSGDChannel", "CNATChannel", "UCNATChannel", "model", "ops", "stoch"]
+           "UQSGDChannel", "RQSGDChannel", "URQSGDChannel", "CNATChannel", "UCNATChannel", "compression", "model",
+           "ops", "stoch"]

@@ -4,7 +4,8 @@ claims that need the real ADFL modules in the same process.
 * With ADFL loaded first, adfl_amd's payload dataclasses ARE ADFL's classes, so the reference's own
   `assert isinstance(c_params, ...)` checks accept our payloads;
 * the reference's IdentityChannel decodes what ours encodes and vice versa (USLQ's fp32 direction);
-* bandwidth accounting and to_json agree on random state dicts (not just the golden one).
+* bandwidth accounting and to_json agree on random state dicts (not just the golden one);
+* adfl_amd.compression exposes the reference compression.py's hot-path functions with its parameter names.
 Runs in a subprocess so the ADFL stubs never leak into other tests."""
 
 import os
@@ -52,6 +53,12 @@ for trial in range(20):
     for name, p in params.items():
         assert torch.equal(back[name], p) and torch.equal(back2[name], p)
     assert model.get_parameter_info(params) == ref.model.get_parameter_info(params)
+# adfl_amd.compression: the reference's hot-path functions under the same names and parameter names
+import inspect
+from adfl_amd import compression
+for fn in ("quantize_tensor", "dequantize_tensor", "pack_4bit", "unpack_4bit"):
+    assert list(inspect.signature(getattr(compression, fn)).parameters) == \
+        list(inspect.signature(getattr(ref.compression, fn)).parameters), fn
 print("dropin ok")
 """
 
