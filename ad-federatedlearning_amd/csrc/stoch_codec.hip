@@ -205,15 +205,19 @@ __device__ __forceinline__ uint32_t cnat_exp_exact(float x, float u, int min_e, 
 
 // Fast form: finite non-zero x whose mantissa is outside every power of two's band (no band is wider
 // than kCnatMaxAbove / kCnatMaxBelow ulps): floor / ceil are e / e + 1. Zeros are handled inline.
+// prob = (2^(e+1) - |x|) / 2^e is formed as 2 - |x| * 2^-e: both are exact scalings of one rounding of the
+// same difference (every intermediate is normal on this path), so the bits are the exact form's, in two
+// fewer instructions. The band test is one unsigned range check on the mantissa (m <= A or m >= 2^23 - B
+// <=> (m + B) mod 2^23 <= A + B).
 __device__ __forceinline__ uint32_t cnat_exp_fast(float x, float u, int min_e, int max_e, bool& bad) {
   const float xa = __builtin_fabsf(x);
   const float v = xa + 0x1p-23f;
   const uint32_t bits = __float_as_uint(v);
-  const int e = (int)(bits >> 23) - 127;
-  const uint32_t m = bits & 0x7fffffu;
-  bad |= (x != 0.0f) & (!(v < 0x1p127f) | (m <= kCnatMaxAbove) | (0x800000u - m <= kCnatMaxBelow));
-  const float prob = __builtin_ldexpf(pow2i(e + 1) - xa, -e);
-  int r = (u < prob) ? e : e + 1;
+  const int ex = (int)(bits >> 23);
+  const int e = ex - 127;
+  bad |= (x != 0.0f) & (!(v < 0x1p127f) | (((bits + kCnatMaxBelow) & 0x7fffffu) <= kCnatMaxAbove + kCnatMaxBelow));
+  const float prob = 2.0f - __builtin_ldexpf(xa, 127 - ex);
+  int r = e + (u < prob ? 0 : 1);
   r = min(max(r, min_e), max_e);
   return (uint32_t)(x == 0.0f ? min_e : r) & 0xffu;
 }
@@ -622,7 +626,9 @@ __device__ __forceinline__ void quantize_regs(const float4 (&v)[kPer], int tg, i
       bool bad = all_exact;
       uint32_t q = pack4(fast(v[j].x, uj.x, bad), fast(v[j].y, uj.y, bad), fast(v[j].z, uj.z, bad),
                          fast(v[j].w, uj.w, bad));
-      if (wave_any(bad && live) && bad)
+      // the whole wave takes the exact form when any live lane flagged (equal results where the fast form
+      // holds): `bad` is then only a wave-wide OR of compare masks, never a per-lane value
+      if (wave_any(bad && live))
         q = pack4(exact(v[j].x, uj.x), exact(v[j].y, uj.y), exact(v[j].z, uj.z), exact(v[j].w, uj.w));
       if (live) {
         l4[k] = q;
@@ -1012,7 +1018,7 @@ __global__ __launch_bounds__(kBlock) void k_stoch_dequantize(const uint8_t* __re
     r.y = decode_fast<KIND>((l >> 8) & 0xffu, (g >> 8) & 0xffu, norm, mn, d, bad);
     r.z = decode_fast<KIND>((l >> 16) & 0xffu, (g >> 16) & 0xffu, norm, mn, d, bad);
     r.w = decode_fast<KIND>(l >> 24, g >> 24, norm, mn, d, bad);
-    if (KIND != 2 && wave_any(bad && live) && bad) {
+    if (KIND != 2 && wave_any(bad && live)) {  // whole wave exact, as in quantize_regs
       r.x = decode_exact<KIND>(l & 0xffu, g & 0xffu, norm, mn, s);
       r.y = decode_exact<KIND>((l >> 8) & 0xffu, (g >> 8) & 0xffu, norm, mn, s);
       r.z = decode_exact<KIND>((l >> 16) & 0xffu, (g >> 16) & 0xffu, norm, mn, s);
