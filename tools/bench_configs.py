@@ -247,6 +247,7 @@ def mode_pcie(args, world, rank, dev):
     segs = {k: round(seg_ms(evs, i, i + 1), 4) for i, k in
             enumerate(("h2d_x", "encode", "d2h_h2d_payload", "decode", "d2h_out"))}
     pcie_ms = segs["h2d_x"] + segs["d2h_h2d_payload"] + segs["d2h_out"]
+    stream = _pcie_stream(lib, n, x_h, dev, args)
     del x, q, q2, out, x_h, q_h, out_h
     # The same 1 GiB as ADFL hands it over: a pageable CPU state dict through SLQChannel (host to host). The
     # channel stages in element ranges (gather || H2D, D2H || scatter) and allocates its outputs while the
@@ -268,9 +269,102 @@ def mode_pcie(args, world, rank, dev):
     return {"metric": "PCIe-inclusive SLQ round trip, 1 GiB fp32 from and to pinned host memory", "unit": "GiB/s",
             "value": round(n * 4 / GIB / t, 2), "ms_per_step": round(t * 1e3, 4), "segments_ms": segs,
             "pcie_GBs": round(10 * n / (pcie_ms * 1e-3) / 1e9, 1),
+            "stream_of_updates": stream,
             "channel_pageable_dict": {"encode_ms": round(enc_ms, 3), "decode_ms": round(dec_ms, 3),
                                       "round_trip_GiB_per_s": round(n * 4 / GIB / ((enc_ms + dec_ms) * 1e-3), 2),
                                       "best_of": len(enc_t)}}
+
+
+def _pcie_stream(lib, n, x_h, dev, args, updates: int = 8):
+    """The same host-to-host round trip for a STREAM of 1 GiB updates (what a server decoding update after
+    update sees): three copy streams and one compute stream ordered only by events, device and pinned
+    buffers double-buffered. PCIe is full duplex, so update i+1's
+    H2D of x runs under update i's D2H of the output; per update each direction carries 5N bytes."""
+    from adfl_amd import _lib, ops
+    # four streams (the box runs 4 hardware queues per process; more streams would share them): x in, the
+    # payload's hop out and back in (sequential by nature), output out, compute
+    streams = {k: torch.cuda.Stream(dev) for k in ("x_in", "q_path", "o_out", "comp")}
+    streams["q_out"] = streams["q_in"] = streams["q_path"]
+    xs = [torch.empty(n, device=dev) for _ in range(2)]
+    qs = [torch.empty(n, dtype=torch.int8, device=dev) for _ in range(2)]
+    q2s = [torch.empty(n, dtype=torch.int8, device=dev) for _ in range(2)]
+    outs = [torch.empty(n, device=dev) for _ in range(2)]
+    ss = [torch.empty(1, device=dev) for _ in range(2)]
+    wss = [ops.new_workspace(dev) for _ in range(2)]
+    q_hs = [torch.empty(n, dtype=torch.int8).pin_memory() for _ in range(2)]
+    o_hs = [torch.empty(n).pin_memory() for _ in range(2)]
+    ev = lambda: torch.cuda.Event()  # noqa: E731
+    last = {}  # per buffer slot: events of the previous use, so a slot is reused only when free
+
+    def issue(i):
+        b = i % 2
+        e_x, e_enc, e_qo, e_qi, e_dec, e_oo = ev(), ev(), ev(), ev(), ev(), ev()
+        prev = last.get(b)
+        with torch.cuda.stream(streams["x_in"]):
+            if prev:
+                streams["x_in"].wait_event(prev["enc"])          # x[b] free once its encode has read it
+            xs[b].copy_(x_h, non_blocking=True)
+            e_x.record()
+        with torch.cuda.stream(streams["comp"]):
+            streams["comp"].wait_event(e_x)
+            if prev:
+                streams["comp"].wait_event(prev["qo"])           # q[b] free once sent
+            _lib.check(lib.adfl_slq_encode(xs[b].data_ptr(), n, 8, qs[b].data_ptr(), ss[b].data_ptr(),
+                                           wss[b].data_ptr(), wss[b].numel(), streams["comp"].cuda_stream))
+            e_enc.record()
+        with torch.cuda.stream(streams["q_out"]):
+            streams["q_out"].wait_event(e_enc)
+            if prev:
+                streams["q_out"].wait_event(prev["qi"])          # q_h[b] free once received
+            q_hs[b].copy_(qs[b], non_blocking=True)
+            e_qo.record()
+        with torch.cuda.stream(streams["q_in"]):
+            streams["q_in"].wait_event(e_qo)
+            if prev:
+                streams["q_in"].wait_event(prev["dec"])          # q2[b] free once decoded
+            q2s[b].copy_(q_hs[b], non_blocking=True)
+            e_qi.record()
+        with torch.cuda.stream(streams["comp"]):
+            streams["comp"].wait_event(e_qi)
+            if prev:
+                streams["comp"].wait_event(prev["oo"])           # out[b] free once sent
+            _lib.check(lib.adfl_slq_dequantize(q2s[b].data_ptr(), n, ss[b].data_ptr(), outs[b].data_ptr(),
+                                               streams["comp"].cuda_stream))
+            e_dec.record()
+        with torch.cuda.stream(streams["o_out"]):
+            streams["o_out"].wait_event(e_dec)
+            o_hs[b].copy_(outs[b], non_blocking=True)
+            e_oo.record()
+        last[b] = {"enc": e_enc, "qo": e_qo, "qi": e_qi, "dec": e_dec, "oo": e_oo}
+
+    for i in range(2):  # warmup
+        issue(i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(updates):
+        issue(i)
+    torch.cuda.synchronize()
+    t = (time.perf_counter() - t0) / updates
+    ok = bool(torch.equal(o_hs[(updates - 1) % 2], o_hs[(updates - 2) % 2]))  # same input, same output
+    # the duplex ceiling on this box: 1 GiB H2D and 1 GiB D2H at the same time, alone and together
+    def copy_ms(h2d, d2h, reps=3):
+        best = 1e9
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            if h2d:
+                with torch.cuda.stream(streams["x_in"]):
+                    xs[0].copy_(x_h, non_blocking=True)
+            if d2h:
+                with torch.cuda.stream(streams["o_out"]):
+                    o_hs[0].copy_(outs[0], non_blocking=True)
+            torch.cuda.synchronize()
+            best = min(best, time.perf_counter() - t1)
+        return round(best * 1e3, 3)
+    duplex = {"h2d_1GiB_ms": copy_ms(True, False), "d2h_1GiB_ms": copy_ms(False, True),
+              "both_at_once_ms": copy_ms(True, True)}
+    return {"updates": updates, "ms_per_update": round(t * 1e3, 3), "GiB_per_s": round(n * 4 / GIB / t, 2),
+            "pcie_GBs_per_direction": round(5 * n / t / 1e9, 1), "outputs_consistent": ok, "duplex_probe": duplex}
 
 
 def mode_channel(args, world, rank, dev):
