@@ -314,6 +314,22 @@ def cold_decode_ms(lib, qp, n, sp, op, stream, reps: int = 10) -> float:
     return sorted(e0.elapsed_time(e1) for e0, e1 in evs)[reps // 2]
 
 
+def copy_ceiling_GBs(x: torch.Tensor, out: torch.Tensor, stream, reps: int = 10) -> float:
+    """The device-to-device copy ceiling of this GPU (SURVEY.md §8d asks for it beside the roofline): torch's
+    own 1 GiB fp32 copy (read 1 GiB + write 1 GiB), median of `reps` HIP-event timings on the launch stream.
+    Reported only; the roofline fraction stays against the 8.0 TB/s spec peak."""
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    with torch.cuda.stream(stream):
+        out.copy_(x)
+        for e0, e1 in evs:
+            e0.record(stream)
+            out.copy_(x)
+            e1.record(stream)
+    torch.cuda.synchronize()
+    ms = sorted(e0.elapsed_time(e1) for e0, e1 in evs)[reps // 2]
+    return 2 * x.numel() * x.element_size() / (ms * 1e-3) / 1e9
+
+
 def exchange_leg(x: torch.Tensor, out: torch.Tensor, bits: int, world: int, steps: int, warmup: int):
     """BASELINE configs[3] (C4) on the same buffers: every rank is one simulated client that encodes its
     1 GiB update, all-gathers the int8 payloads (+ scale trailers) over RCCL and decodes the K payloads
@@ -446,6 +462,7 @@ def main():
     elapsed = max_over_ranks(elapsed, world)
 
     decode_cold = cold_decode_ms(lib, qp, n, sp, op, stream)
+    copy_ceiling = copy_ceiling_GBs(x, out, stream)
 
     exchange = None
     if args.exchange == "on" or (args.exchange == "auto" and world > 1):
@@ -482,6 +499,7 @@ def main():
                      "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": round(per_kernel[dominant], 4)},
         "kernels_ms": {k: round(v, 4) for k, v in per_kernel.items()},
         "decode_cold_ms": round(decode_cold, 4),
+        "copy_ceiling_GBs": round(copy_ceiling, 1),
         "round_trip_roofline": {"alg_bytes": 14 * n, "kernel_ms": round(kernels_ms, 4),
                                 "achieved_GBs": round(14 * n / (kernels_ms * 1e-3) / 1e9, 1),
                                 "frac": round(14 * n / (kernels_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
