@@ -128,8 +128,10 @@ def dist_setup(args, backend: str = "nccl"):
         torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
+        import datetime
         kw = {"device_id": torch.device("cuda", local)} if backend == "nccl" else {}
-        dist.init_process_group(backend, **kw)
+        # a stuck collective fails in minutes rather than torch's default 10
+        dist.init_process_group(backend, timeout=datetime.timedelta(seconds=180), **kw)
     return world, rank, local
 
 
@@ -470,7 +472,10 @@ def main():
             import torch.distributed as dist
             dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{free_port()}", rank=0, world_size=1,
                                     device_id=dev)
-        exchange = exchange_leg(x, out, args.bits, world, min(args.steps, 20), min(args.warmup, 3))
+        try:  # never at the cost of the headline line: a failure is reported in the `exchange` object
+            exchange = exchange_leg(x, out, args.bits, world, min(args.steps, 20), min(args.warmup, 3))
+        except Exception as e:  # noqa: BLE001
+            exchange = {"error": f"{type(e).__name__}: {e}"[:400]}
 
     per_kernel = {name: sum(e[i].elapsed_time(e[i + 1]) for e in events) / args.steps
                   for i, name in enumerate(("absmax", "quantize", "dequantize"))}
