@@ -451,6 +451,53 @@ def _ref_stoch_cpu(codec, x, bits=8):
     return t1 - t0, time.perf_counter() - t1
 
 
+def mode_channel_stoch(args, world, rank, dev):
+    """The stochastic channels on ADFL's call pattern: the C3 CPU state dict through QSGDChannel /
+    RQSGDChannel / CNATChannel(8).on_client_send + on_server_receive, against the reference's per-tensor op
+    sequence (quant.py:223-252, 364-398, 509-545; restated in _ref_stoch_cpu) on the same host and dict.
+    Outputs are not compared here (the uniforms differ by design; tests/test_gpu_stoch.py pins parity)."""
+    from adfl_amd.Channel import CNATChannel, QSGDChannel, RQSGDChannel
+    base, rem = divmod(RESNET18, 256)
+    g = torch.Generator().manual_seed(0)
+    params = {}
+    for i in range(256):
+        params[f"layer{i}.weight"] = torch.randn(1, base + (1 if i < rem else 0), generator=g) * 1e-3
+        params[f"layer{i}.bias"] = torch.randn(64, generator=g) * 1e-3
+    weights = [t for t in params.values() if t.ndim > 1]
+    gib = sum(t.numel() for t in params.values()) * 4 / GIB
+    res = {"metric": "stochastic channels on a CPU ResNet-18-sized state dict (256 weights + 256 biases), host "
+                     "to host", "unit": "ms", "reference_threads": torch.get_num_threads()}
+    for name, cls in (("qsgd", QSGDChannel), ("rqsgd", RQSGDChannel), ("cnat", CNATChannel)):
+        ch = cls(8)
+
+        def ours():
+            t0 = time.perf_counter()
+            qp, _ = ch.on_client_send(params)
+            t1 = time.perf_counter()
+            ch.on_server_receive(qp)
+            return t1 - t0, time.perf_counter() - t1
+
+        def reference():
+            e = d = 0.0
+            for t in weights:
+                a, b = _ref_stoch_cpu(name, t)
+                e += a
+                d += b
+            return e, d
+
+        for _ in range(args.warmup):
+            ours()
+        reference()
+        o = [ours() for _ in range(args.steps)]
+        r = [reference() for _ in range(3)]
+        best = lambda xs, i: min(x[i] for x in xs) * 1e3  # noqa: E731
+        res[name] = {"ours_encode_ms": round(best(o, 0), 3), "ours_decode_ms": round(best(o, 1), 3),
+                     "reference_encode_ms": round(best(r, 0), 3), "reference_decode_ms": round(best(r, 1), 3),
+                     "ours_GiB_s": round(gib / ((best(o, 0) + best(o, 1)) * 1e-3), 2),
+                     "reference_GiB_s": round(gib / ((best(r, 0) + best(r, 1)) * 1e-3), 3)}
+    return res
+
+
 def mode_stoch(args, world, rank, dev):
     """Stochastic codecs (QSGD / RQSGD / CNAT, bits = 8, in-kernel Philox) on C2 (one 2^28 tensor) and C3
     (256 tensors: one-launch resident encodes). Each timed span starts behind GPU work (a 512 MiB read that
@@ -552,7 +599,8 @@ def mode_stoch(args, world, rank, dev):
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--mode", choices=["c3", "c5_int4", "exchange", "pcie", "channel", "stoch"], required=True)
+    p.add_argument("--mode", choices=["c3", "c5_int4", "exchange", "pcie", "channel", "channel_stoch", "stoch"],
+                   required=True)
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
@@ -568,7 +616,7 @@ def main():
     assert world == args.gpus, (world, args.gpus)
     dev = torch.device("cuda", local)
     line = {"c3": mode_c3, "c5_int4": mode_c5_int4, "exchange": mode_exchange, "pcie": mode_pcie,
-            "channel": mode_channel, "stoch": mode_stoch}[args.mode](
+            "channel": mode_channel, "channel_stoch": mode_channel_stoch, "stoch": mode_stoch}[args.mode](
         args, world, rank, dev)
     if rank == 0:
         print(json.dumps(line), flush=True)
