@@ -34,7 +34,7 @@ from .. import hostcopy
 from .. import stoch as sops
 from ..model import CompressedParameters, Parameters, QuantParameter, QuantParameters, get_parameter_info
 from .channel import Channel, IdentityChannel
-from .quant import _hand_out, _serialized, _stage_in, _staging
+from .quant import _PendingD2H, _hand_out, _serialized, _stage_in, _staging
 
 _CODECS = ("qsgd", "rqsgd", "cnat")
 
@@ -95,6 +95,22 @@ def _encode_stoch(params: Parameters, names: List[str], codec: str, bits: int, u
     if mins is not None:
         nm_host[lay.ntensors:].copy_(mins, non_blocking=True)
     on_cpu = [not t.is_cuda for t in tensors]
+    if all(on_cpu):
+        # as SLQ's encode: both planes' D2H enqueued right behind the norms, the owned outputs allocated
+        # while they run, each range scattered as it lands
+        norms_ready = torch.cuda.Event()
+        norms_ready.record(torch.cuda.current_stream(dev))
+        pend_lv = _PendingD2H(lv.view(torch.uint8), lay, st, "s_levels")
+        pend_sg = _PendingD2H(sg, lay, st, "s_signs")
+        shapes = [t.shape for t in tensors]
+        lv_parts = [torch.empty(s_, dtype=lv.dtype) for s_ in shapes]
+        sg_parts = [torch.empty(s_, dtype=torch.int8) for s_ in shapes]
+        hostcopy.advise_huge(lv_parts + sg_parts)
+        norms_ready.synchronize()
+        nm = nm_host.tolist()
+        pend_lv.finish([t.view(torch.uint8) for t in lv_parts])
+        pend_sg.finish(sg_parts)
+        return _payloads(names, lv_parts, sg_parts, nm, lay.ntensors, codec)
     if any(on_cpu):
         lv_h = st.buf("s_levels_host", lay.total, torch.uint8, pinned=True).view(lv.dtype)
         sg_h = st.buf("s_signs_host", lay.total, torch.int8, pinned=True)
@@ -108,19 +124,24 @@ def _encode_stoch(params: Parameters, names: List[str], codec: str, bits: int, u
     sg_parts = _owned_host(sg_h, lay.offsets, shapes) if any(on_cpu) else None
     lv_dev = _owned(split(lv), shapes) if not all(on_cpu) else None
     sg_dev = _owned(split(sg), shapes) if not all(on_cpu) else None
+    datas = [(lv_parts if cpu else lv_dev)[i] for i, cpu in enumerate(on_cpu)]
+    signs = [(sg_parts if cpu else sg_dev)[i] for i, cpu in enumerate(on_cpu)]
+    return _payloads(names, datas, signs, nm, lay.ntensors, codec)
+
+
+def _payloads(names, datas, signs, nm, ntensors: int, codec: str):
+    """{name: (data, signs, scale, scale_2)} as the reference's _quantize_tensor returns them."""
     out = {}
-    for i, (name, cpu) in enumerate(zip(names, on_cpu)):
-        data = (lv_parts if cpu else lv_dev)[i]
-        signs = (sg_parts if cpu else sg_dev)[i]
-        norm = nm[i]
+    for i, name in enumerate(names):
+        data, norm = datas[i], nm[i]
         if norm == 0.0:  # the reference's norm == 0 branch: uint8 zeros, tensor(0.) scale
             scale = torch.tensor(0.0)
             data = data.view(torch.uint8)
             scale_2 = 0
         else:
             scale = norm
-            scale_2 = nm[lay.ntensors + i] if codec == "rqsgd" else 0
-        out[name] = (data, signs, scale, scale_2)
+            scale_2 = nm[ntensors + i] if codec == "rqsgd" else 0
+        out[name] = (data, signs[i], scale, scale_2)
     return out
 
 
