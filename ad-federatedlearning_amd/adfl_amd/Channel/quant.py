@@ -196,7 +196,8 @@ class _PendingD2H:
         ptrs = _ptrs(outs)
         for (lo, hi), ev in zip(self.ranges, self.events):
             ev.synchronize()
-            hostcopy.copy_pieces(*_range_copies(ptrs, self.lay, self.host.data_ptr(), es, lo, hi, to_bucket=False))
+            hostcopy.copy_pieces(*_range_copies(ptrs, self.lay, self.host.data_ptr(), es, lo, hi, to_bucket=False),
+                                 stream=True)
 
 
 def _stage_out(dev_buf: torch.Tensor, lay: ops.BucketLayout, st: _DeviceStaging, key: str,

@@ -80,6 +80,7 @@ SIGNATURES = {
     "adfl_philox_uniforms": (INT, [P, I64, I64, U64, U64, P]),
     # adfl_host.h
     "adfl_host_copy": (INT, [P, P, P, I64, I32]),
+    "adfl_host_copy_ex": (INT, [P, P, P, I64, I32, I32]),
     "adfl_host_threads": (I32, []),
 }
 

@@ -25,7 +25,7 @@ def _host_lib():
         path = os.environ.get("ADFL_HOST_LIB")
         if path:
             lib = ctypes.CDLL(path)
-            for name in ("adfl_host_copy", "adfl_host_threads"):
+            for name in ("adfl_host_copy", "adfl_host_copy_ex", "adfl_host_threads"):
                 fn = getattr(lib, name)
                 fn.restype, fn.argtypes = _lib.SIGNATURES[name]
             _host = lib
@@ -34,13 +34,20 @@ def _host_lib():
     return _host
 
 
-def copy_pieces(dst_ptrs: Sequence[int], src_ptrs: Sequence[int], nbytes: Sequence[int], threads: int = 0) -> None:
+STREAM = 1  # ADFL_HOST_COPY_STREAM
+
+
+def copy_pieces(dst_ptrs: Sequence[int], src_ptrs: Sequence[int], nbytes: Sequence[int], threads: int = 0,
+                stream: bool = False) -> None:
+    """stream=True: streaming (non-temporal) stores for large pieces — for fresh destinations nothing reads
+    soon (the scatter into per-tensor outputs); the gather into a pinned bucket keeps plain memcpy."""
     d = np.asarray(dst_ptrs, dtype=np.uint64)
     s = np.asarray(src_ptrs, dtype=np.uint64)
     b = np.asarray(nbytes, dtype=np.int64)
     if not (len(d) == len(s) == len(b)):
         raise ValueError("copy_pieces: pointer and size lists differ in length")
-    check(_host_lib().adfl_host_copy(d.ctypes.data, s.ctypes.data, b.ctypes.data, len(b), threads))
+    check(_host_lib().adfl_host_copy_ex(d.ctypes.data, s.ctypes.data, b.ctypes.data, len(b), threads,
+                                        STREAM if stream else 0))
 
 
 def gather(srcs: Sequence[torch.Tensor], dst: torch.Tensor, offsets: Sequence[int]) -> None:
@@ -61,7 +68,8 @@ def scatter(src: torch.Tensor, dsts: Sequence[torch.Tensor], offsets: Sequence[i
     for t in dsts:
         if t.is_cuda or not t.is_contiguous() or t.element_size() != es:
             raise ValueError("hostcopy.scatter: destinations must be contiguous CPU tensors of the bucket's element size")
-    copy_pieces([t.data_ptr() for t in dsts], [base + int(o) * es for o in offsets], [t.numel() * es for t in dsts])
+    copy_pieces([t.data_ptr() for t in dsts], [base + int(o) * es for o in offsets], [t.numel() * es for t in dsts],
+                stream=True)
 
 
 _HUGE = 2 << 20        # x86-64 transparent huge page

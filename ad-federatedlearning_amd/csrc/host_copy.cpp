@@ -2,6 +2,8 @@
 // that splits a list of memcpys into equal byte ranges. Used by the host-resident channel path to gather a
 // CPU state dict into the pinned bucket and to scatter payloads back into per-tensor storage.
 
+#include <emmintrin.h>
+
 #include <algorithm>
 #include <condition_variable>
 #include <cstdint>
@@ -19,6 +21,7 @@ constexpr int kMaxThreads = 16;
 constexpr int64_t kMinBytesPerThread = 256 << 10;  // below this, extra threads cost more than they copy
 
 struct Job {
+  bool stream;  // ADFL_HOST_COPY_STREAM
   void* const* dsts;
   const void* const* srcs;
   const int64_t* nbytes;
@@ -26,6 +29,33 @@ struct Job {
   const int64_t* prefix;  // prefix[k] = bytes before piece k; prefix[n] = total
   int parts;
 };
+
+constexpr int64_t kStreamBytes = 64 << 10;  // pieces at least this long take the streaming copy
+
+// memcpy with non-temporal 16-byte stores (SSE2, baseline x86-64), for ADFL_HOST_COPY_STREAM: fresh
+// per-tensor outputs nothing reads soon; streaming stores skip the read-for-ownership of every destination
+// line. Into the pinned bucket the plain memcpy measured faster (tools/hostcopy_ab.py), so the gather does
+// not ask for it. Weakly ordered: every part ends with _mm_sfence() (run_part) before it reports done.
+void stream_copy(char* d, const char* s, size_t n) {
+  size_t head = (16 - ((uintptr_t)d & 15)) & 15;
+  if (head > n) head = n;
+  std::memcpy(d, s, head);
+  d += head;
+  s += head;
+  n -= head;
+  const size_t m = n & ~(size_t)63;
+  for (size_t i = 0; i < m; i += 64) {
+    const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + i));
+    const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + i + 16));
+    const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + i + 32));
+    const __m128i e = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + i + 48));
+    _mm_stream_si128(reinterpret_cast<__m128i*>(d + i), a);
+    _mm_stream_si128(reinterpret_cast<__m128i*>(d + i + 16), b);
+    _mm_stream_si128(reinterpret_cast<__m128i*>(d + i + 32), c);
+    _mm_stream_si128(reinterpret_cast<__m128i*>(d + i + 48), e);
+  }
+  std::memcpy(d + m, s + m, n - m);
+}
 
 // Copy byte range [lo, hi) of the concatenated piece list.
 void copy_range(const Job& j, int64_t lo, int64_t hi) {
@@ -35,7 +65,12 @@ void copy_range(const Job& j, int64_t lo, int64_t hi) {
     const int64_t take = std::min(hi, piece_end) - lo;
     if (take > 0) {
       const int64_t off = lo - j.prefix[k];
-      std::memcpy(static_cast<char*>(j.dsts[k]) + off, static_cast<const char*>(j.srcs[k]) + off, (size_t)take);
+      char* d = static_cast<char*>(j.dsts[k]) + off;
+      const char* s = static_cast<const char*>(j.srcs[k]) + off;
+      if (j.stream && take >= kStreamBytes)
+        stream_copy(d, s, (size_t)take);
+      else
+        std::memcpy(d, s, (size_t)take);
       lo += take;
     }
     ++k;
@@ -46,6 +81,7 @@ void run_part(const Job& j, int p) {
   const int64_t total = j.prefix[j.n];
   const int64_t lo = total * p / j.parts, hi = total * (p + 1) / j.parts;
   copy_range(j, lo, hi);
+  _mm_sfence();  // the streaming stores are visible before this part counts as done
 }
 
 class Pool {
@@ -131,7 +167,12 @@ extern "C" {
 int32_t adfl_host_threads(void) { return Pool::get().size(); }
 
 int adfl_host_copy(void* const* dsts, const void* const* srcs, const int64_t* nbytes, int64_t n, int32_t nthreads) {
-  if (n < 0 || (n > 0 && (!dsts || !srcs || !nbytes))) return ADFL_E_ARG;
+  return adfl_host_copy_ex(dsts, srcs, nbytes, n, nthreads, 0);
+}
+
+int adfl_host_copy_ex(void* const* dsts, const void* const* srcs, const int64_t* nbytes, int64_t n, int32_t nthreads,
+                      int32_t flags) {
+  if (n < 0 || (n > 0 && (!dsts || !srcs || !nbytes)) || (flags & ~ADFL_HOST_COPY_STREAM)) return ADFL_E_ARG;
   std::vector<int64_t> prefix((size_t)n + 1, 0);
   for (int64_t k = 0; k < n; ++k) {
     if (nbytes[k] < 0 || (nbytes[k] > 0 && (!dsts[k] || !srcs[k]))) return ADFL_E_ARG;
@@ -142,7 +183,7 @@ int adfl_host_copy(void* const* dsts, const void* const* srcs, const int64_t* nb
   Pool& pool = Pool::get();
   int parts = nthreads > 0 ? std::min<int>(nthreads, pool.size()) : pool.size();
   parts = (int)std::max<int64_t>(1, std::min<int64_t>(parts, total / kMinBytesPerThread));
-  Job job{dsts, srcs, nbytes, n, prefix.data(), parts};
+  Job job{(flags & ADFL_HOST_COPY_STREAM) != 0, dsts, srcs, nbytes, n, prefix.data(), parts};
   if (parts == 1) {
     run_part(job, 0);
     return ADFL_OK;

@@ -23,6 +23,13 @@ extern "C" {
  * Returns 0, or ADFL_E_ARG (-1) for a null pointer or negative size. */
 int adfl_host_copy(void* const* dsts, const void* const* srcs, const int64_t* nbytes, int64_t n, int32_t nthreads);
 
+/* adfl_host_copy with flags. ADFL_HOST_COPY_STREAM: pieces of 64 KiB or more are written with
+ * non-temporal (streaming) stores, for destinations nothing reads soon (fresh per-tensor outputs: measured
+ * faster for the scatter, slower for the gather into a pinned bucket, tools/hostcopy_ab.py). */
+enum { ADFL_HOST_COPY_STREAM = 1 };
+int adfl_host_copy_ex(void* const* dsts, const void* const* srcs, const int64_t* nbytes, int64_t n, int32_t nthreads,
+                      int32_t flags);
+
 /* Threads the pool would use for nthreads <= 0 (for logging and tests). */
 int32_t adfl_host_threads(void);
 

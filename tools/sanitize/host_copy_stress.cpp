@@ -31,7 +31,8 @@ static int run_caller(int id, int iters) {
       b[k] = len;
     }
     const int threads = (int)(rng() % 20) - 2;  // <= 0: the default
-    if (adfl_host_copy(d.data(), s.data(), b.data(), n, threads) != 0) ++bad;
+    const int flags = (int)(rng() % 2);  // plain memcpy or streaming stores (ADFL_HOST_COPY_STREAM)
+    if (adfl_host_copy_ex(d.data(), s.data(), b.data(), n, threads, flags) != 0) ++bad;
     for (int k = 0; k < n; ++k) {
       if (b[k] && std::memcmp(dst[k].data(), src[k].data(), (size_t)b[k]) != 0) ++bad;
       if (dst[k][(size_t)b[k]] != 0xEE) ++bad;  // nothing written past the piece
@@ -43,6 +44,7 @@ static int run_caller(int id, int iters) {
 int main() {
   if (adfl_host_copy(nullptr, nullptr, nullptr, 1, 0) != -1) return 2;
   if (adfl_host_copy(nullptr, nullptr, nullptr, 0, 0) != 0) return 2;
+  if (adfl_host_copy_ex(nullptr, nullptr, nullptr, 0, 0, 4) != -1) return 2;  // unknown flag
   const int callers = 8, iters = 12;
   std::vector<int> bad(callers, 0);
   std::vector<std::thread> ts;
