@@ -66,6 +66,29 @@ def parse():
     return p.parse_args()
 
 
+_JSON_FD = None
+
+
+def reserve_stdout() -> None:
+    """The driver reads ONE JSON line from stdout, but RCCL prints its banner (version, host, library path)
+    to fd 1 when a process group starts. Keep the real stdout for the JSON line only and send everything
+    else written to fd 1 — by this process, torch or RCCL — to stderr."""
+    global _JSON_FD
+    if _JSON_FD is None:
+        sys.stdout.flush()
+        _JSON_FD = os.dup(1)
+        os.dup2(2, 1)
+
+
+def emit(obj) -> None:
+    data = (json.dumps(obj) + "\n").encode()
+    if _JSON_FD is None:
+        sys.stdout.write(data.decode())
+        sys.stdout.flush()
+    else:
+        os.write(_JSON_FD, data)
+
+
 def free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -402,8 +425,7 @@ def plumbing_check(args):
     else:
         ranks = [(0, 0)]
     if rank == 0:
-        print(json.dumps({"plumbing_check": True, "n_gpus": world, "ranks": ranks,
-                          "max_over_ranks_s": round(slowest, 4)}), flush=True)
+        emit({"plumbing_check": True, "n_gpus": world, "ranks": ranks, "max_over_ranks_s": round(slowest, 4)})
     if dist.is_initialized():
         dist.destroy_process_group()
 
@@ -413,6 +435,7 @@ def main():
     rc = maybe_launch(args.gpus, os.path.abspath(__file__), sys.argv[1:])
     if rc is not None:
         sys.exit(rc)
+    reserve_stdout()
     if args.plumbing_check:
         return plumbing_check(args)
     if args.pmc_child:
@@ -527,7 +550,7 @@ def main():
                                          for name, k in KERNEL_SYMBOLS.items() if (v := live.get(k)) is not None}
         else:
             line["roofline"]["traffic_live_error"] = note
-    print(json.dumps(line), flush=True)
+    emit(line)
     if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
 
