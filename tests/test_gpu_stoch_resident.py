@@ -122,3 +122,21 @@ def test_layout_with_a_large_tensor_runs_multi_launch():
     b = _enc("qsgd", xd, lay, 8, False, seed=1, counter=0)
     torch.cuda.synchronize()
     assert all(_same(p, r) for p, r in zip(a, b))
+
+
+@pytest.mark.parametrize("codec", ["qsgd", "rqsgd", "cnat"])
+def test_full_size_sign_symmetry(codec):
+    """Size-independent property at the bench size (2^28 elements, C2, multi-launch path): with the same
+    Philox stream, encode(-x) has the same levels / exponents and norms as encode(x) and negated signs
+    (quant.py:230-236 uses |x|; torch.sign flips)."""
+    g = torch.Generator(device=DEV).manual_seed(3)
+    x = torch.randn(1 << 28, device=DEV, generator=g) * 1e-3
+    lay = ops.BucketLayout([x.numel()], align=1)
+    a = _enc(codec, x, lay, 8, None, seed=5, counter=0)
+    b = _enc(codec, -x, lay, 8, None, seed=5, counter=0)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[2], b[2])
+    assert torch.equal(a[1], -b[1])
+    if codec == "rqsgd":
+        assert torch.equal(a[3], b[3])
+    del x, a, b
+    torch.cuda.empty_cache()
