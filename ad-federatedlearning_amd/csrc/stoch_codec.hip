@@ -312,6 +312,9 @@ __device__ __forceinline__ int chunk_head4(int64_t start, int len) {
 constexpr int kPer = ADFL_SLQ_CHUNK_ELEMS / 4 / kBlock;
 constexpr int kPbQuantize = 4;  // Philox blocks per batch in the multi-launch quantize kernels
 constexpr int kPbResident = 2;  // ... and in the resident encodes (their VGPRs hold two chunks per lane)
+// k_qsgd_encode_resident: sign bytes stored before the norm barrier (true) or with the levels (false). A/B on
+// C3, tools/microbench_stoch_res.hip: 29.2 vs 28.5 us flushed — the product stores them with the levels.
+constexpr bool kEarlySigns = false;
 constexpr int64_t kKeepBytes = 192ll << 20;  // x tail the norm pass leaves in the Infinity Cache
 constexpr int64_t kKeepChunks = kKeepBytes / (4 * ADFL_SLQ_CHUNK_ELEMS);
 
@@ -592,7 +595,8 @@ __device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0ull; }
 // the wave). `all_exact` is uniform over the group.
 // Philox uniforms are generated PB groups at a time (philox4x32_10_batch); injected uniforms (a test path)
 // are loaded group by group.
-// pre (LDS, or null): Philox words generated ahead of time, group j's at pre[j * pre_stride].
+// pre (LDS, or null): Philox words generated ahead of time, group j's at pre[j * pre_stride]. s4 null: the
+// caller stores the sign bytes itself.
 template <int PB, class F, class E, class A>
 __device__ __forceinline__ void quantize_regs(const float4 (&v)[kPer], int tg, int n4, int64_t g0, const Uniforms& U,
                                               uint32_t* __restrict__ l4, uint32_t* __restrict__ s4, F fast, E exact,
@@ -632,7 +636,7 @@ __device__ __forceinline__ void quantize_regs(const float4 (&v)[kPer], int tg, i
         q = pack4(exact(v[j].x, uj.x), exact(v[j].y, uj.y), exact(v[j].z, uj.z), exact(v[j].w, uj.w));
       if (live) {
         l4[k] = q;
-        s4[k] = pack4(sign_byte(v[j].x), sign_byte(v[j].y), sign_byte(v[j].z), sign_byte(v[j].w));
+        if (s4) s4[k] = pack4(sign_byte(v[j].x), sign_byte(v[j].y), sign_byte(v[j].z), sign_byte(v[j].w));
         if (acc) acc->add4(v[j]);
       }
     }
@@ -757,7 +761,9 @@ __device__ __forceinline__ float resident_l2(const double (&red)[kResPerGroup][k
   return (float)__builtin_sqrt((double)(float)t);
 }
 
-template <int MODE, int PB>  // MODE ADFL_NORM_L2 (QSGD) or ADFL_NORM_LINF (RQSGD); PB as for k_qsgd_quantize
+// EARLY_SIGNS: the sign bytes (which do not depend on the norm) are stored while the loads drain, before the
+// block's norm barrier, instead of after it with the levels.
+template <int MODE, int PB, bool EARLY_SIGNS>  // MODE ADFL_NORM_L2 (QSGD) or ADFL_NORM_LINF (RQSGD)
 __global__ __launch_bounds__(kResBlock) void k_qsgd_encode_resident(
     const float* __restrict__ x, const adfl_slq_chunk* __restrict__ chunks, const int32_t* __restrict__ work,
     float lev, Uniforms U, uint8_t* __restrict__ levels, int8_t* __restrict__ signs, float* __restrict__ norms,
@@ -805,6 +811,23 @@ __global__ __launch_bounds__(kResBlock) void k_qsgd_encode_resident(
       philox4x32_10_batch(ctr, U.seed, w);
 #pragma unroll
       for (int i = 0; i < PB; ++i) pre[jb + i][threadIdx.x] = w[i];
+    }
+  }
+  if (EARLY_SIGNS) {
+#pragma unroll
+    for (int r = 0; r < kResPerGroup; ++r) {
+      const int kc = grp + r * kResGroups;
+      if (kc >= ct.nchunks) continue;  // group-uniform
+      const adfl_slq_chunk c = chunks[ci + kc];
+      int8_t* sg = signs + c.start;
+      uint32_t* s4 = reinterpret_cast<uint32_t*>(sg + chunk_head4(c.start, c.len));
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        const int k = tg + j * kBlock;
+        if (k < n4s[r])
+          s4[k] = pack4(sign_byte(v[r][j].x), sign_byte(v[r][j].y), sign_byte(v[r][j].z), sign_byte(v[r][j].w));
+      }
+      if (ei[r] >= 0) sg[ei[r]] = (int8_t)sign_byte(ev[r]);
     }
   }
   float norm, mn = 0.0f;
@@ -879,11 +902,11 @@ __global__ __launch_bounds__(kResBlock) void k_qsgd_encode_resident(
     }
     const int head = chunk_head4(c.start, c.len);
     quantize_regs<PB>(v[r], tg, n4s[r], c.start + head, U, reinterpret_cast<uint32_t*>(lv + head),
-                      reinterpret_cast<uint32_t*>(sg + head), fast, exact, !d.fast, (NormAcc<ADFL_NORM_L2>*)nullptr,
-                      r == 0 ? &pre[0][threadIdx.x] : nullptr, kResBlock);
+                      EARLY_SIGNS ? nullptr : reinterpret_cast<uint32_t*>(sg + head), fast, exact, !d.fast,
+                      (NormAcc<ADFL_NORM_L2>*)nullptr, r == 0 ? &pre[0][threadIdx.x] : nullptr, kResBlock);
     if (ei[r] >= 0) {
       lv[ei[r]] = (uint8_t)exact(ev[r], U.one(c.start + ei[r]));
-      sg[ei[r]] = (int8_t)sign_byte(ev[r]);
+      if (!EARLY_SIGNS) sg[ei[r]] = (int8_t)sign_byte(ev[r]);
     }
   }
 }
@@ -1090,8 +1113,8 @@ inline int launch_resident(const float* d_x, const adfl_slq_chunk* d_chunks, int
                        reinterpret_cast<int8_t*>(d_a), d_signs, d_norms);
   } else {
     constexpr int mode = KIND == 1 ? ADFL_NORM_LINF : ADFL_NORM_L2;
-    hipLaunchKernelGGL((k_qsgd_encode_resident<mode, kPbResident>), grid, block, 0, st, d_x, d_chunks, d_work,
-                       levels_f(bits), U, d_a, d_signs, d_norms, d_mins);
+    hipLaunchKernelGGL((k_qsgd_encode_resident<mode, kPbResident, kEarlySigns>), grid, block, 0, st, d_x, d_chunks,
+                       d_work, levels_f(bits), U, d_a, d_signs, d_norms, d_mins);
   }
   return launch_status();
 }

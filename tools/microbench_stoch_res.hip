@@ -89,7 +89,7 @@ int run(const char* label, const std::vector<int64_t>& sizes) {
                          "cnat multi-launch", "cnat resident", "qsgd norm pass (2 launches)",
                          "slq resident/two-pass encode", "qsgd quantize PB1", "qsgd quantize PB2", "qsgd quantize PB4",
                          "qsgd quantize PB8", "cnat quantize PB1", "cnat quantize PB2", "cnat quantize PB4",
-                         "cnat quantize PB8", "qsgd resident PB1", "qsgd resident PB4", "cnat resident PB1",
+                         "cnat quantize PB8", "qsgd resident late signs", "qsgd resident early signs", "cnat resident PB1",
                          "cnat resident PB2"};
   const int nv = sizeof(names) / sizeof(names[0]);
   const int reps = g_reps;
@@ -118,8 +118,8 @@ int run(const char* label, const std::vector<int64_t>& sizes) {
           case 13: hipLaunchKernelGGL(k_cnat_quantize<2>, gq, bq, 0, 0, x, dch, -128, 127, U, sg, q, (double*)ws); break;
           case 14: hipLaunchKernelGGL(k_cnat_quantize<4>, gq, bq, 0, 0, x, dch, -128, 127, U, sg, q, (double*)ws); break;
           case 15: hipLaunchKernelGGL(k_cnat_quantize<8>, gq, bq, 0, 0, x, dch, -128, 127, U, sg, q, (double*)ws); break;
-          case 16: hipLaunchKernelGGL((k_qsgd_encode_resident<ADFL_NORM_L2, 1>), gr, br, 0, 0, x, dch, dwk, 255.0f, U, lv, sg, norms, mins); break;
-          case 17: hipLaunchKernelGGL((k_qsgd_encode_resident<ADFL_NORM_L2, 4>), gr, br, 0, 0, x, dch, dwk, 255.0f, U, lv, sg, norms, mins); break;
+          case 16: hipLaunchKernelGGL((k_qsgd_encode_resident<ADFL_NORM_L2, 2, false>), gr, br, 0, 0, x, dch, dwk, 255.0f, U, lv, sg, norms, mins); break;
+          case 17: hipLaunchKernelGGL((k_qsgd_encode_resident<ADFL_NORM_L2, 2, true>), gr, br, 0, 0, x, dch, dwk, 255.0f, U, lv, sg, norms, mins); break;
           case 18: hipLaunchKernelGGL(k_cnat_encode_resident<1>, gr, br, 0, 0, x, dch, dwk, -128, 127, U, sg, q, norms); break;
           default: hipLaunchKernelGGL(k_cnat_encode_resident<2>, gr, br, 0, 0, x, dch, dwk, -128, 127, U, sg, q, norms); break;
         }
