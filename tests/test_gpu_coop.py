@@ -125,8 +125,9 @@ def test_past_capacity_runs_two_pass():
     assert int(sync.count_nonzero()) == 0
 
 
-def test_two_streams_own_sync_buffers():
+def test_two_streams_own_sync_buffers(monkeypatch):
     """Encodes of one layout on two streams use separate sync buffers and both equal the oracle."""
+    monkeypatch.setenv("ADFL_SLQ_ENCODE", "coop")
     sizes = [8192 * 50, 8192 * 3 + 1, 100]
     lay = ops.BucketLayout(sizes)
     rng = np.random.default_rng(8)
