@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #define CK(x)                                                                                \
@@ -158,8 +159,84 @@ int run(const char* label, const std::vector<int64_t>& sizes) {
 }
 }  // namespace
 
+// The quantize kernels on the C3 bucket with chunk tables of smaller chunks (8192 / 4096 / 2048 elements):
+// more, shorter blocks, so the load and compute phases of different blocks can overlap.
+int run_chunk_sizes() {
+  const int nt = 256;
+  std::vector<int64_t> sizes(nt), offs(nt);
+  int64_t o = 0;
+  for (int i = 0; i < nt; ++i) {
+    sizes[i] = 11689512 / 256 + (i < 11689512 % 256 ? 1 : 0);
+    offs[i] = o;
+    o += (sizes[i] + 63) / 64 * 64;
+  }
+  const int64_t total = o;
+  float *x, *norms;
+  uint8_t* lv;
+  int8_t *sg, *q;
+  void* ws;
+  uint4* junk;
+  CK(hipMalloc(&x, total * 4));
+  CK(hipMalloc(&lv, total));
+  CK(hipMalloc(&sg, total));
+  CK(hipMalloc(&q, total));
+  CK(hipMalloc(&norms, nt * 4));
+  CK(hipMalloc(&ws, 8192 * kPartialBytes));
+  CK(hipMalloc(&junk, 512ll << 20));
+  hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, x, total);
+  hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, norms, nt);
+  const Uniforms U{nullptr, 7, 0};
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  printf("C3 quantize kernels by chunk size (flushed, median of %d)\n", g_reps);
+  for (int cs : {8192, 4096, 2048}) {
+    std::vector<adfl_slq_chunk> ch;
+    for (int t = 0; t < nt; ++t) {
+      const int first = (int)ch.size(), nc = (int)((sizes[t] + cs - 1) / cs);
+      for (int k = 0; k < nc; ++k)
+        ch.push_back({offs[t] + (int64_t)k * cs, (int32_t)std::min<int64_t>(cs, sizes[t] - (int64_t)k * cs), t, first, nc});
+    }
+    adfl_slq_chunk* dch;
+    CK(hipMalloc(&dch, ch.size() * sizeof(adfl_slq_chunk)));
+    CK(hipMemcpy(dch, ch.data(), ch.size() * sizeof(adfl_slq_chunk), hipMemcpyHostToDevice));
+    for (int v = 0; v < 2; ++v) {
+      std::vector<float> ts;
+      for (int rep = 0; rep < g_reps + 2; ++rep) {
+        hipLaunchKernelGGL(k_flush, dim3(4096), dim3(256), 0, 0, junk, (512ll << 20) / 16);
+        CK(hipEventRecord(e0, 0));
+        if (v == 0)
+          hipLaunchKernelGGL(k_cnat_quantize<4>, dim3((unsigned)ch.size()), dim3(kBlock), 0, 0, x, dch, -128, 127, U, sg, q,
+                             (double*)ws);
+        else
+          hipLaunchKernelGGL(k_qsgd_quantize<4>, dim3((unsigned)ch.size()), dim3(kBlock), 0, 0, x, dch, 255.0f, norms, U,
+                             lv, sg);
+        CK(hipGetLastError());
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (rep >= 2) ts.push_back(ms);
+      }
+      std::sort(ts.begin(), ts.end());
+      printf("  %-14s chunk %5d  blocks %5zu  %7.2f us\n", v == 0 ? "cnat quantize" : "qsgd quantize", cs, ch.size(),
+             ts[ts.size() / 2] * 1e3);
+    }
+    CK(hipFree(dch));
+  }
+  CK(hipFree(x));
+  CK(hipFree(lv));
+  CK(hipFree(sg));
+  CK(hipFree(q));
+  CK(hipFree(norms));
+  CK(hipFree(ws));
+  CK(hipFree(junk));
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc > 1) g_reps = atoi(argv[1]);  // e.g. 2 under rocprofv3 --pmc
+  if (argc > 2 && strcmp(argv[2], "chunks") == 0) return run_chunk_sizes();
   std::vector<int64_t> c3(256);
   for (int i = 0; i < 256; ++i) c3[i] = 11689512 / 256 + (i < 11689512 % 256 ? 1 : 0);
   run("C3", c3);
