@@ -30,6 +30,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -1155,20 +1156,22 @@ int adfl_slq_encode_batched(const float* d_x, const adfl_slq_chunk* d_chunks, in
   return launch_status();
 }
 
-// Co-resident block capacity of k_encode_coop on the current device (occupancy x CUs), cached per device.
+// Co-resident block capacity of k_encode_coop on the current device (occupancy x CUs), cached per device
+// (the stream passed to adfl_slq_encode_batched_coop must belong to the current device, as for every
+// launch here). Concurrent first calls compute the same value.
 static int64_t coop_capacity() {
-  static int64_t cap[64] = {0};
+  static std::atomic<int64_t> cap[64];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  if (cap[dev] == 0) {
+  if (cap[dev].load(std::memory_order_relaxed) == 0) {
     int per_cu = 0, cus = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k_encode_coop), kBlock,
                                                      0) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       return 0;
-    cap[dev] = (int64_t)per_cu * cus;
+    cap[dev].store((int64_t)per_cu * cus, std::memory_order_relaxed);
   }
-  return cap[dev];
+  return cap[dev].load(std::memory_order_relaxed);
 }
 
 int64_t adfl_slq_coop_capacity(void) { return coop_capacity(); }
