@@ -140,7 +140,8 @@ def c3_round_trip(lay, packed, args, world, rank, dev, lib, sh, junk, mode="auto
 
 def mode_c3(args, world, rank, dev):
     """C3: ResNet-18's 11,689,512 parameters in 256 tensors. The headline layout is equal sizes; the
-    log-uniform layout (64 .. 2.4 M elements, tests/golden/recipes.py) and the packed int4 variant are
+    log-uniform layout (sizes drawn in [64, 2.4 M] and scaled to the total: 64 .. 350,191 elements,
+    tests/golden/recipes.py) and the packed int4 variant are
     reported beside it."""
     sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
     import recipes
