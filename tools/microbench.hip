@@ -243,6 +243,24 @@ int main(int argc, char** argv) {
            14.0 * gb / (t * 1e-3) / 8000.0);
   }
 
+  // ---- 1b. cold decode: the Infinity Cache flushed (a 1 GiB read of another buffer) before each dequantize,
+  // as when the payload arrives from another process
+  {
+    printf("%-20s %8s %8s\n", "cold decode", "ms", "frac");
+    for (auto& d : D) {
+      std::vector<float> t;
+      for (int s = 0; s < 20; ++s) {
+        hipLaunchKernelGGL(mb::k_read<false>, dim3(2048), dim3(256), 0, st, (const float4*)tmp, n >> 2, ws);
+        (void)hipEventRecord(ev[0], st);
+        d.fn();
+        (void)hipEventRecord(ev[1], st);
+        CK(hipEventSynchronize(ev[1]));
+        t.push_back(ms(ev[0], ev[1]));
+      }
+      printf("%-20s %8.4f %6.3f\n", d.name.c_str(), med(t), 5.0 * gb / (med(t) * 1e-3) / 8000.0);
+    }
+  }
+
   // ---- 2. int4 round trip (13 B/elem algorithmic)
   {
     std::vector<float> a, qq, d;
