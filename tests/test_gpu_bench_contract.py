@@ -1,0 +1,37 @@
+"""bench.py's output contract on the GPU (the line the driver parses): exactly one JSON line on stdout with the
+headline keys, n_gpus = 1, a roofline object for the dominant kernel, and value consistent with ms_per_step.
+A short run: 3 timed steps, no CPU baseline, no PMC passes, no exchange leg (each is covered elsewhere)."""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_emits_one_contract_line():
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "3", "--warmup", "1",
+                        "--no-cpu-baseline", "--pmc", "off", "--exchange", "off"],
+                       cwd=REPO, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["warmup"] == 1
+    assert d["unit"] == "GiB/s" and d["higher_is_better"] is True and d["scaling"] == "weak"
+    assert d["config"]["workload"].startswith("C2") and d["config"]["elements_per_gpu"] == 1 << 28
+    # value = 1 GiB per step / step time
+    assert abs(d["value"] - 1.0 / (d["ms_per_step"] * 1e-3)) / d["value"] < 0.01
+    rf = d["roofline"]
+    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
+    assert 0.0 < rf["frac"] < 1.0 and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
+    assert rf["alg_bytes_per_launch"] > 0 and rf["avg_launch_ms"] > 0
+    assert d["cpu_baseline"] is None  # --no-cpu-baseline
