@@ -138,6 +138,20 @@ def test_bucket_layout():
     assert sum(c.len for c in lay.chunks) == recipes.RESNET18_PARAMS
     with pytest.raises(ValueError):
         ops.BucketLayout([4, 0])
+    assert lay.max_tensor_chunks == max(c.nchunks for c in lay.chunks) and lay.nwork == 0  # loguniform: two-pass
+
+
+def test_encode_mode_selection(monkeypatch):
+    """ADFL_SLQ_ENCODE picks the bucketed encode; the product default is 'auto' (resident / two-pass) and a
+    bad value fails loudly instead of silently choosing one."""
+    monkeypatch.delenv("ADFL_SLQ_ENCODE", raising=False)
+    assert ops._encode_mode() == "auto"
+    for m in ("auto", "resident", "coop", "twopass"):
+        monkeypatch.setenv("ADFL_SLQ_ENCODE", m)
+        assert ops._encode_mode() == m
+    monkeypatch.setenv("ADFL_SLQ_ENCODE", "fastest")
+    with pytest.raises(ValueError, match="ADFL_SLQ_ENCODE"):
+        ops._encode_mode()
 
 
 def test_oracle_not_imported_by_product_package():
