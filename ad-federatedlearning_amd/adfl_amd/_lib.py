@@ -41,6 +41,7 @@ SIGNATURES = {
     "adfl_slq_strerror": (ctypes.c_char_p, [INT]),
     "adfl_slq_workspace_bytes": (I64, []),
     "adfl_slq_absmax": (INT, [P, I64, P, I64, P]),
+    "adfl_slq_absmax_value": (INT, [P, P, P]),
     "adfl_slq_quantize": (INT, [P, I64, INT, P, P, P, P]),
     "adfl_slq_encode": (INT, [P, I64, INT, P, P, P, I64, P]),
     "adfl_slq_dequantize": (INT, [P, I64, P, P, P]),

@@ -117,8 +117,10 @@ class PeerExchange:
         self.row_bytes = [_pad16(p) + 16 for p in self.payload]
         self.local = [torch.empty(rb, dtype=torch.uint8, device=device) for rb in self.row_bytes]
         self.gathered = [torch.empty(self.world, rb, dtype=torch.uint8, device=device) for rb in self.row_bytes]
-        # device rows over a host-only backend (gloo): stage each row through pinned host memory
-        self.host_staged = device.type == "cuda" and dist.get_backend(group) != "nccl"
+        # device rows over a host-only backend (gloo): stage each row through pinned host memory. A group
+        # made without an explicit backend reports a combined string ("cpu:gloo,cuda:nccl"): its CUDA
+        # tensors go through RCCL, so any string naming nccl is device-direct
+        self.host_staged = device.type == "cuda" and "nccl" not in str(dist.get_backend(group))
         if self.host_staged:
             self.local_host = [torch.empty(rb, dtype=torch.uint8, pin_memory=True) for rb in self.row_bytes]
             self.gathered_host = [torch.empty(self.world, rb, dtype=torch.uint8, pin_memory=True)
@@ -134,7 +136,10 @@ class PeerExchange:
 
     def encode_and_gather(self, x: torch.Tensor) -> List:
         """Encode this rank's update chunk by chunk; each chunk's all-gather is issued as soon as it is
-        quantized. Returns the pending collective works."""
+        quantized. Returns the pending collective works.
+
+        With exact_self, `x` itself is this rank's term of the mean: it must stay unchanged until mean()
+        returns (the peers received its quantized values as of this call), and is released there."""
         if x.numel() != self.numel or x.dtype != torch.float32:
             raise ValueError(f"PeerExchange: expected {self.numel} fp32 elements, got {x.numel()} {x.dtype}")
         x = x.reshape(-1)
@@ -157,11 +162,14 @@ class PeerExchange:
         is a chunk whose collective the caller has already waited on)."""
         out = torch.empty(self.numel, dtype=torch.float32, device=self.device) if out is None else out
         self_row = self.rank if self.exact_self else -1
+        if self_row >= 0 and self._x is None:
+            raise RuntimeError("PeerExchange.mean: no pending encode_and_gather (exact_self needs its update)")
         for (c0, c1), rows, pb, w in zip(self.bounds, self.gathered, self.payload, works):
             if w is not None:
                 w.wait()
             self.codec.mean(rows, c1 - c0, self.packed, pb, out[c0:c1], self_row,
                             self._x[c0:c1] if self_row >= 0 else None)
+        self._x = None   # the caller's update is not kept alive past the exchange (1-4 GiB at C4/C5)
         return out
 
     def exchange_mean(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:

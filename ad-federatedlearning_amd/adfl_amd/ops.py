@@ -10,11 +10,14 @@ synchronises. Semantics are the reference's, bit for bit:
 * ``encode_int4`` / ``decode_int4`` / ``pack_int4`` / ``unpack_int4`` — Src/ADFL/compression.py:35-66
 * ``dequantize_mean`` — the peer mean after the exchange (Examples/ray_ad.py:188)
 
-The same ops are registered as PyTorch custom ops ``torch.ops.adfl.*`` at the bottom of this file.
+The same ops are registered as PyTorch custom ops ``torch.ops.adfl.*`` (with fake implementations, so
+they trace under torch.compile) at the bottom of this file: slq_absmax, slq_encode / slq_decode,
+slq_encode_int4 / slq_decode_int4, slq_encode_batched / slq_decode_batched and their _int4 variants over
+caller-placed tensors (host offsets / sizes), pack_int4 / unpack_int4 and slq_dequantize_mean.
 """
 
 import os
-from typing import Optional, Sequence, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -62,6 +65,18 @@ def new_workspace(device) -> torch.Tensor:
 # ------------------------------------------------------------------------------------------------
 # flat codec
 # ------------------------------------------------------------------------------------------------
+def absmax(x: torch.Tensor, *, workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """torch.max(torch.abs(t)) (quant.py:100) on the device: fp32 tensor of shape [] (NaN propagates)."""
+    require_quantizable(x)
+    x = _dev(x, "x")
+    ws = new_workspace(x.device) if workspace is None else workspace
+    out = torch.empty((), dtype=torch.float32, device=x.device)
+    lib, st = _lib.load(), _stream(x.device)
+    check(lib.adfl_slq_absmax(x.data_ptr(), x.numel(), ws.data_ptr(), ws.numel(), st))
+    check(lib.adfl_slq_absmax_value(ws.data_ptr(), out.data_ptr(), st))
+    return out
+
+
 def encode(x: torch.Tensor, bits: int, *, q: Optional[torch.Tensor] = None, scale: Optional[torch.Tensor] = None,
            workspace: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """quant.py:97-104 on the device: returns (int8 payload shaped like x, fp32 scale of shape [1])."""
@@ -162,18 +177,31 @@ class BucketLayout:
     align=1 packs them back to back (compact: what the Channel stages through host memory, so the
     host-side gather is one plain concatenation)."""
 
-    def __init__(self, sizes: Sequence[int], align: int = ALIGN_ELEMS):
+    def __init__(self, sizes: Sequence[int], align: int = ALIGN_ELEMS, offsets: Optional[Sequence[int]] = None):
         sizes = [int(s) for s in sizes]
         if not sizes or min(sizes) < 1:
             raise ValueError("BucketLayout: every tensor needs at least one element")
         if align < 1:
             raise ValueError("BucketLayout: align must be >= 1")
-        self.align = align
         self.sizes = np.asarray(sizes, dtype=np.int64)
-        padded = (self.sizes + align - 1) // align * align
-        self.padded = padded.astype(np.int64)  # per-tensor slot size (size rounded up to the alignment)
-        self.offsets = np.concatenate([[0], np.cumsum(padded)[:-1]]).astype(np.int64)
-        self.total = int(padded.sum())
+        if offsets is None:
+            self.align = align
+            padded = (self.sizes + align - 1) // align * align
+            self.padded = padded.astype(np.int64)  # per-tensor slot size (size rounded up to the alignment)
+            self.offsets = np.concatenate([[0], np.cumsum(padded)[:-1]]).astype(np.int64)
+            self.total = int(padded.sum())
+        else:  # caller-placed tensors (the torch.ops.adfl batched ops): any order, no overlap
+            self.offsets = np.asarray([int(o) for o in offsets], dtype=np.int64)
+            if self.offsets.shape != self.sizes.shape or (self.offsets < 0).any():
+                raise ValueError("BucketLayout: offsets must be one non-negative offset per tensor")
+            order = np.argsort(self.offsets, kind="stable")
+            ends = self.offsets[order] + self.sizes[order]
+            if (self.offsets[order][1:] < ends[:-1]).any():
+                raise ValueError("BucketLayout: tensors overlap")
+            self.total = int(ends.max())
+            self.padded = self.sizes.copy()
+            nz = self.offsets[self.offsets > 0]
+            self.align = int(np.gcd.reduce(nz)) if nz.size else ALIGN_ELEMS
         self.ntensors = len(sizes)
         lib = _lib.load()
         off_p, siz_p = self.offsets.ctypes.data, self.sizes.ctypes.data
@@ -314,9 +342,8 @@ def dequantize_add_batched(q: torch.Tensor, scales: torch.Tensor, layout: Bucket
     once, accumulate into K device-resident models (Src/ADFL/Client/pool.py:62-75, model.py:337-347).
 
     targets: K sequences of T contiguous, 16-byte aligned fp32 device tensors, tensor t with
-    layout.sizes[t] elements. The layout's offsets must be multiples of 4 (an aligned bucket)."""
-    if (layout.offsets % 4).any():
-        raise ValueError("dequantize_add_batched: tensor offsets must be multiples of 4 (use an aligned layout)")
+    layout.sizes[t] elements. Any layout: an aligned bucket's tensors take 16-byte accesses, a compact
+    bucket's (offsets not multiples of 4) are decoded element-wise, with the same result."""
     q = _dev(q, "q")
     dev = q.device
     ptrs = []
@@ -416,3 +443,139 @@ def slq_decode_int4_op(packed: torch.Tensor, n: int, scale: torch.Tensor) -> tor
 @slq_decode_int4_op.register_fake
 def _(packed, n, scale):
     return packed.new_empty((n,), dtype=torch.float32)
+
+
+@torch.library.custom_op("adfl::slq_absmax", mutates_args=())
+def slq_absmax_op(x: torch.Tensor) -> torch.Tensor:
+    return absmax(x)
+
+
+@slq_absmax_op.register_fake
+def _(x):
+    return x.new_empty((), dtype=torch.float32)
+
+
+# Batched ops over caller-placed tensors: `offsets` / `sizes` are host (CPU) int64 tensors, tensor t owning
+# flat[offsets[t] : offsets[t] + sizes[t]] (any order, no overlap; quant.py:74-94's loop over a state dict
+# in one launch per pass). Outputs are shaped like the flat input; positions no tensor owns are zero.
+_LAYOUT_CACHE: "dict" = {}
+_LAYOUT_CACHE_MAX = 64
+
+
+def layout_for(offsets: torch.Tensor, sizes: torch.Tensor) -> BucketLayout:
+    """The BucketLayout (host chunk table + its device copies) for caller-placed tensors, cached by value so a
+    repeated state-dict layout pays the table build and its H2D copy once."""
+    if offsets.device.type != "cpu" or sizes.device.type != "cpu":
+        raise ValueError("adfl batched ops: offsets and sizes must be host (CPU) int64 tensors")
+    key = (tuple(offsets.tolist()), tuple(sizes.tolist()))
+    lay = _LAYOUT_CACHE.pop(key, None)
+    if lay is None:
+        lay = BucketLayout(key[1], offsets=key[0])
+    _LAYOUT_CACHE[key] = lay                       # most recently used last
+    while len(_LAYOUT_CACHE) > _LAYOUT_CACHE_MAX:
+        _LAYOUT_CACHE.pop(next(iter(_LAYOUT_CACHE)))
+    return lay
+
+
+def _filled(n: int, dtype, device, lay: BucketLayout) -> torch.Tensor:
+    """Output buffer of n elements: zeros when some element belongs to no tensor (gaps, or a buffer longer
+    than the layout), so the op's result is deterministic; otherwise left for the kernel to fill."""
+    covered = int(lay.sizes.sum()) == n
+    return (torch.empty if covered else torch.zeros)(n, dtype=dtype, device=device)
+
+
+@torch.library.custom_op("adfl::slq_encode_batched", mutates_args=())
+def slq_encode_batched_op(flat: torch.Tensor, offsets: torch.Tensor, sizes: torch.Tensor,
+                          bits: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    lay = layout_for(offsets, sizes)
+    flat = flat.reshape(-1)
+    if flat.numel() < lay.total:
+        raise ValueError("slq_encode_batched: flat buffer smaller than the layout")
+    q = _filled(flat.numel(), torch.int8, flat.device, lay)
+    return encode_batched(flat, lay, bits, q=q)
+
+
+@slq_encode_batched_op.register_fake
+def _(flat, offsets, sizes, bits):
+    return flat.new_empty((flat.numel(),), dtype=torch.int8), flat.new_empty((sizes.numel(),), dtype=torch.float32)
+
+
+@torch.library.custom_op("adfl::slq_decode_batched", mutates_args=())
+def slq_decode_batched_op(q: torch.Tensor, scales: torch.Tensor, offsets: torch.Tensor,
+                          sizes: torch.Tensor) -> torch.Tensor:
+    lay = layout_for(offsets, sizes)
+    q = q.reshape(-1)
+    if q.numel() < lay.total:
+        raise ValueError("slq_decode_batched: payload smaller than the layout")
+    return decode_batched(q, scales, lay, out=_filled(q.numel(), torch.float32, q.device, lay))
+
+
+@slq_decode_batched_op.register_fake
+def _(q, scales, offsets, sizes):
+    return q.new_empty((q.numel(),), dtype=torch.float32)
+
+
+@torch.library.custom_op("adfl::slq_encode_batched_int4", mutates_args=())
+def slq_encode_batched_int4_op(flat: torch.Tensor, offsets: torch.Tensor, sizes: torch.Tensor,
+                               bits: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    lay = layout_for(offsets, sizes)
+    flat = flat.reshape(-1)
+    if flat.numel() < lay.total:
+        raise ValueError("slq_encode_batched_int4: flat buffer smaller than the layout")
+    nbytes = (flat.numel() + 1) // 2
+    gap = int(lay.sizes.sum()) != flat.numel()
+    packed = (torch.zeros if gap else torch.empty)(nbytes, dtype=torch.uint8, device=flat.device)
+    return encode_batched_int4(flat, lay, bits, packed=packed)
+
+
+@slq_encode_batched_int4_op.register_fake
+def _(flat, offsets, sizes, bits):
+    return (flat.new_empty(((flat.numel() + 1) // 2,), dtype=torch.uint8),
+            flat.new_empty((sizes.numel(),), dtype=torch.float32))
+
+
+@torch.library.custom_op("adfl::slq_decode_batched_int4", mutates_args=())
+def slq_decode_batched_int4_op(packed: torch.Tensor, scales: torch.Tensor, offsets: torch.Tensor,
+                               sizes: torch.Tensor, n: int) -> torch.Tensor:
+    lay = layout_for(offsets, sizes)
+    if n < lay.total or packed.numel() < (lay.total + 1) // 2:
+        raise ValueError("slq_decode_batched_int4: n / packed smaller than the layout")
+    gap = int(lay.sizes.sum()) != n
+    out = (torch.zeros if gap else torch.empty)(n, dtype=torch.float32, device=packed.device)
+    return decode_batched_int4(packed.reshape(-1), scales, lay, out=out)
+
+
+@slq_decode_batched_int4_op.register_fake
+def _(packed, scales, offsets, sizes, n):
+    return packed.new_empty((n,), dtype=torch.float32)
+
+
+@torch.library.custom_op("adfl::pack_int4", mutates_args=())
+def pack_int4_op(q: torch.Tensor) -> torch.Tensor:
+    return pack_int4(q)
+
+
+@pack_int4_op.register_fake
+def _(q):
+    return q.new_empty(((q.numel() + 1) // 2,), dtype=torch.uint8)
+
+
+@torch.library.custom_op("adfl::unpack_int4", mutates_args=())
+def unpack_int4_op(packed: torch.Tensor, shape: List[int]) -> torch.Tensor:
+    return unpack_int4(packed, shape)
+
+
+@unpack_int4_op.register_fake
+def _(packed, shape):
+    return packed.new_empty(tuple(shape), dtype=torch.int8)
+
+
+@torch.library.custom_op("adfl::slq_dequantize_mean", mutates_args=())
+def slq_dequantize_mean_op(q_rows: torch.Tensor, scales: torch.Tensor, n: int, self_row: int = -1,
+                           self_x: Optional[torch.Tensor] = None) -> torch.Tensor:
+    return dequantize_mean(q_rows, scales, n, self_row=self_row, self_x=self_x)
+
+
+@slq_dequantize_mean_op.register_fake
+def _(q_rows, scales, n, self_row=-1, self_x=None):
+    return q_rows.new_empty((n,), dtype=torch.float32)

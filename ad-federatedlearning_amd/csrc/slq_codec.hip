@@ -300,6 +300,14 @@ __global__ __launch_bounds__(kBlock) void k_quantize_flat(const float* __restric
     for (int64_t i = ntiles * kTile + threadIdx.x; i < n; i += kBlock) q[i] = (int8_t)quant1(x[i], si.inv);
 }
 
+// max|x| as a value (torch.max(torch.abs(t)), quant.py:100): pass 1's partials reduced by one block. The
+// abs bit patterns order like the magnitudes, and a NaN's pattern exceeds +inf's, so NaN propagates.
+__global__ __launch_bounds__(kBlock) void k_absmax_value(const uint32_t* __restrict__ partials,
+                                                         float* __restrict__ out) {
+  const uint32_t m = reduce_partials(partials, (int)partials[kCountSlot]);
+  if (threadIdx.x == 0) *out = __uint_as_float(m);
+}
+
 // Decode: tiles walked forwards (pass 2 wrote the head of the payload last). ABI: <false, false>.
 template <bool REVERSE, bool LD_NT>
 __global__ __launch_bounds__(kBlock) void k_dequantize_flat(const int8_t* __restrict__ q, int64_t n,
@@ -772,6 +780,10 @@ __global__ __launch_bounds__(kSegBlock) void k_encode_resident(const float* __re
   __shared__ __attribute__((aligned(16))) uint32_t lds[kSegWaves][kTile / 4];
   const int64_t ci = work[blockIdx.x];
   const adfl_slq_chunk c = chunks[ci];
+  if (c.nchunks > kSegChunks) {  // not a resident work list (a direct C caller's): NaN scale, nothing written
+    if (threadIdx.x == 0) scales[c.tensor] = __builtin_nanf("");
+    return;
+  }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int len = (c.nchunks - 1) * ADFL_SLQ_CHUNK_ELEMS + chunks[ci + c.nchunks - 1].len;
   const float* xt = x + c.start;
@@ -827,6 +839,10 @@ __global__ __launch_bounds__(kSegBlock) void k_encode_resident_int4(const float*
   __shared__ __attribute__((aligned(16))) uint16_t lds[kSegWaves][kTile4 / 4];
   const int64_t ci = work[blockIdx.x];
   const adfl_slq_chunk c = chunks[ci];
+  if (c.nchunks > kSegChunks) {  // not a resident work list (a direct C caller's): NaN scale, nothing written
+    if (threadIdx.x == 0) scales[c.tensor] = __builtin_nanf("");
+    return;
+  }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int len = (c.nchunks - 1) * ADFL_SLQ_CHUNK_ELEMS + chunks[ci + c.nchunks - 1].len;
   const float* xt = x + c.start;
@@ -892,8 +908,10 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_batched(const int8_t* __r
 
 // Decode + accumulate into K models (pool.py:62-75, qafel.py:176-179 via model.py:337-347): the chunk's
 // payload is decoded once into registers (8 float4 per thread), then every model's slice is read, added
-// (fp32(a + d), what mul_(1).add_(d, alpha=1) computes) and written back with 16-byte accesses. Tensor
-// offsets in the bucket are multiples of 4, so the payload dwords and the targets' float4s line up.
+// (fp32(a + d), what mul_(1).add_(d, alpha=1) computes) and written back with 16-byte accesses when the
+// tensor's offset in the bucket is a multiple of 4 (the payload dwords and the targets' float4s line up).
+// Any other offset (a compact bucket) takes an element-wise path with the same sums: every chunk of a
+// tensor shares its offset's residue mod 4, so the branch is block-uniform.
 __global__ __launch_bounds__(kBlock) void k_dequantize_add_batched(const int8_t* __restrict__ q,
                                                                    const adfl_slq_chunk* __restrict__ chunks,
                                                                    const float* __restrict__ scales,
@@ -904,6 +922,13 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_add_batched(const int8_t*
   const float s = scales[c.tensor];
   const int64_t in_tensor = (int64_t)(blockIdx.x - c.first_chunk) * ADFL_SLQ_CHUNK_ELEMS;
   const int8_t* qc = q + c.start;
+  if (c.start & 3) {
+    for (int m = 0; m < ntargets; ++m) {
+      float* tg = targets[(int64_t)m * ntensors + c.tensor] + in_tensor;
+      for (int i = threadIdx.x; i < c.len; i += kBlock) tg[i] = tg[i] + s * (float)qc[i];
+    }
+    return;
+  }
   const uint32_t* q4 = reinterpret_cast<const uint32_t*>(qc);
   const int n4 = c.len >> 2;
   float4 dv[kPer];
@@ -1090,6 +1115,14 @@ int adfl_slq_absmax(const float* d_x, int64_t n, void* d_workspace, int64_t work
   if (workspace_bytes < kWorkspaceBytes) return ADFL_E_WORKSPACE;
   hipLaunchKernelGGL(k_absmax_flat<8>, dim3(absmax_grid(n)), dim3(kBlock), 0, (hipStream_t)stream, d_x, n,
                      (int64_t)(kCacheKeepBytes / 16), (uint32_t*)d_workspace);
+  return launch_status();
+}
+
+int adfl_slq_absmax_value(const void* d_workspace, float* d_absmax, void* stream) {
+  if (!d_workspace || !d_absmax) return ADFL_E_ARG;
+  if (!aligned16(d_workspace)) return ADFL_E_ALIGN;
+  hipLaunchKernelGGL(k_absmax_value, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, (const uint32_t*)d_workspace,
+                     d_absmax);
   return launch_status();
 }
 

@@ -773,6 +773,10 @@ __global__ __launch_bounds__(kResBlock) void k_qsgd_encode_resident(
   __shared__ uint4 pre[kPer][kResBlock];  // 128 KiB: the first chunk's Philox words, made while x streams in
   const int64_t ci = work[blockIdx.x];
   const adfl_slq_chunk ct = chunks[ci];
+  if (ct.nchunks > ADFL_SLQ_RESIDENT_CHUNKS) {  // not a resident work list: NaN norm, nothing written
+    if (threadIdx.x == 0) norms[ct.tensor] = __builtin_nanf("");
+    return;
+  }
   // group and wave are wave-uniform: in SGPRs, so the chunk metadata below is scalar
   const int grp = __builtin_amdgcn_readfirstlane(threadIdx.x / kBlock);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -919,6 +923,10 @@ __global__ __launch_bounds__(kResBlock) void k_cnat_encode_resident(
   __shared__ double red_s[kResPerGroup][kResWaves];
   const int64_t ci = work[blockIdx.x];
   const adfl_slq_chunk ct = chunks[ci];
+  if (ct.nchunks > ADFL_SLQ_RESIDENT_CHUNKS) {  // not a resident work list: NaN norm, nothing written
+    if (threadIdx.x == 0) norms[ct.tensor] = __builtin_nanf("");
+    return;
+  }
   const int grp = __builtin_amdgcn_readfirstlane(threadIdx.x / kBlock);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int tg = threadIdx.x % kBlock, lane = threadIdx.x & 63;

@@ -61,6 +61,9 @@ def parse():
     p.add_argument("--pmc", choices=("auto", "off"), default="auto",
                    help="roofline.traffic from live rocprofv3 PMC passes (auto: N=1 only, after the timed region)")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--cpu-child", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--cpu-input", help=argparse.SUPPRESS)
+    p.add_argument("--cpu-list", help=argparse.SUPPRESS)
     p.add_argument("--plumbing-check", action="store_true",
                    help="CPU-only check of the rank launcher / barrier / max-over-ranks (gloo); no GPU, no bench")
     return p.parse_args()
@@ -273,51 +276,123 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
-def cpu_baseline(x_dev: torch.Tensor, bits: int, budget_s: float, q_dev: torch.Tensor, s_dev: torch.Tensor):
-    """The reference's own op sequence (quant.py:100-103,110) on host cores, timed on the full 1 GiB workload
-    at three thread counts — ATen's default (the job's share of cores, OMP_NUM_THREADS), 1, and
-    os.cpu_count() — best of >= 3 round trips each (fewer only if one round trip exceeds the budget).
-    `value`/`cores` report the fastest of the three."""
+def cpu_round_trips(x: torch.Tensor, bits: int, budget_s: float, first=None):
+    """Best-of round-trip seconds of the reference's op sequence (quant.py:100-103,110) on host tensor x:
+    >= 3 round trips (fewer only when one exceeds the budget), at most 5. `first(q, scale)` sees the first
+    result. Returns (best seconds, runs)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import slq_oracle as oracle  # test infrastructure: the checker / baseline leg only
+    times = []
+    t_start = time.perf_counter()
+    while True:
+        t0 = time.perf_counter()
+        q, scale = oracle.aten_encode(x, bits)
+        d = oracle.aten_decode(q)
+        times.append(time.perf_counter() - t0)
+        if first is not None and len(times) == 1:
+            first(q, scale)
+        del q, d
+        if len(times) >= 5 or (len(times) >= 3 and time.perf_counter() - t_start + min(times) > budget_s) \
+                or time.perf_counter() - t_start > 2 * budget_s:
+            break
+    return min(times), len(times)
 
-    default_threads = torch.get_num_threads()
+
+def cpu_child(args):
+    """--cpu-child: one point of the CPU baseline sweep in a fresh process (never touches the GPU). Its
+    OMP_NUM_THREADS comes from the parent; the affinity mask is set here, before the first parallel region
+    creates ATen's thread pool, so every pool thread inherits it. Reads the bench's own 1 GiB input from
+    --cpu-input and prints {"best_s", "runs", "threads", "affinity"}."""
+    import numpy as np
+    os.sched_setaffinity(0, [int(c) for c in args.cpu_list.split(",")])
+    x = torch.from_numpy(np.fromfile(args.cpu_input, dtype=np.float32))
+    x = x.reshape(SHAPE) if x.numel() == N_ELEMS else x.reshape(1, -1)
+    best, runs = cpu_round_trips(x, args.bits, args.cpu_seconds)
+    emit({"best_s": best, "runs": runs, "threads": torch.get_num_threads(),
+          "affinity": len(os.sched_getaffinity(0))})
+
+
+def cpu_sweep_points():
+    """(label, cpus or None, threads) for the CPU baseline sweep: ATen's default (the job's share,
+    OMP_NUM_THREADS, no pinning), 1 thread, every physical core of one socket, every physical core of both
+    sockets (one hardware thread per core, pinned), and every CPU in the affinity mask (SMT included). The
+    topology is sysfs's, restricted to this process's affinity mask."""
+    allowed = sorted(os.sched_getaffinity(0))
+    cores = {}
+    for cpu in allowed:
+        base = f"/sys/devices/system/cpu/cpu{cpu}/topology"
+        try:
+            with open(base + "/physical_package_id") as f:
+                pkg = int(f.read())
+            with open(base + "/core_id") as f:
+                core = int(f.read())
+        except (OSError, ValueError):
+            pkg, core = 0, cpu
+        cores.setdefault((pkg, core), []).append(cpu)
+    first_thread = {k: min(v) for k, v in cores.items()}
+    packages = sorted({p for p, _ in cores})
+    pts = [("default", None, torch.get_num_threads()), ("1 thread", [allowed[0]], 1)]
+    one = sorted(c for (p, _), c in first_thread.items() if p == packages[0])
+    pts.append((f"socket {packages[0]} physical cores", one, len(one)))
+    if len(packages) > 1:
+        both = sorted(first_thread.values())
+        pts.append((f"{len(packages)} sockets physical cores", both, len(both)))
+    if len(allowed) > len(first_thread):
+        pts.append(("all CPUs (SMT)", allowed, len(allowed)))
+    return pts
+
+
+def cpu_baseline(x_dev: torch.Tensor, bits: int, budget_s: float, q_dev: torch.Tensor, s_dev: torch.Tensor):
+    """The reference's own op sequence (quant.py:100-103,110) on host cores, timed on the bench's own 1 GiB
+    input over the sweep of cpu_sweep_points(). The default point runs in this process (and checks the GPU
+    payload and scale against the reference ops on this very workload); every other point runs in a child
+    process pinned to its CPUs before torch starts. `value`/`cores` report the fastest point."""
+    import tempfile
     x = x_dev.cpu()
-    parity = None
-    per_threads = {}
-    counts = []
-    for t in (default_threads, 1, os.cpu_count() or default_threads):
-        if t not in counts:
-            counts.append(t)
-    share = budget_s / len(counts)
-    for threads in counts:
-        torch.set_num_threads(threads)
-        times = []
-        t_start = time.perf_counter()
-        while True:
-            t0 = time.perf_counter()
-            q, scale = oracle.aten_encode(x, bits)
-            d = oracle.aten_decode(q)
-            times.append(time.perf_counter() - t0)
-            if parity is None:  # the GPU result on this very workload must equal the reference's
-                parity = bool(torch.equal(q.int_repr(), q_dev.cpu())) and float(s_dev.item()) == scale
-            del q, d
-            if len(times) >= 5 or (len(times) >= 3 and time.perf_counter() - t_start + min(times) > share) \
-                    or time.perf_counter() - t_start > 2 * share:
-                break
-        per_threads[threads] = (min(times), len(times))
-    torch.set_num_threads(default_threads)
+    parity = []
+    points = cpu_sweep_points()
+    share = budget_s / len(points)
+
+    def check(q, scale):  # the GPU result on this very workload must equal the reference's
+        parity.append(bool(torch.equal(q.int_repr(), q_dev.cpu())) and float(s_dev.item()) == scale)
+
+    results = {}
+    with tempfile.TemporaryDirectory(prefix="adfl_cpu_", dir="/tmp") as tmp:
+        path = os.path.join(tmp, "x.f32")
+        x.numpy().tofile(path)
+        for label, cpus, threads in points:
+            if cpus is None:
+                best, runs = cpu_round_trips(x, bits, share, first=check)
+                results[label] = {"threads": threads, "best_s": best, "runs": runs}
+                continue
+            env = {k: v for k, v in os.environ.items()
+                   if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR",
+                                "MASTER_PORT")}
+            env.update(OMP_NUM_THREADS=str(threads), HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+            cmd = [sys.executable, os.path.abspath(__file__), "--cpu-child", "--cpu-input", path,
+                   "--cpu-list", ",".join(map(str, cpus)), "--bits", str(bits), "--cpu-seconds", str(share)]
+            try:
+                r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=60 + 4 * share)
+                res = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else None
+            except (subprocess.TimeoutExpired, ValueError, IndexError):
+                res = None
+            results[label] = ({"threads": threads, "pinned_cpus": len(cpus), "best_s": res["best_s"],
+                               "runs": res["runs"]} if res else {"threads": threads, "error": "child failed"})
     gib = x.numel() * 4 / GIB
-    best_threads = min(per_threads, key=lambda k: per_threads[k][0])
-    best = per_threads[best_threads][0]
-    cpu = {"value": round(gib / best, 3), "unit": "GiB/s", "cores": best_threads, "kind": "port",
+    ok = {k: v for k, v in results.items() if "best_s" in v}
+    best_label = min(ok, key=lambda k: ok[k]["best_s"])
+    best = ok[best_label]["best_s"]
+    cpu = {"value": round(gib / best, 3), "unit": "GiB/s", "cores": ok[best_label]["threads"], "kind": "port",
+           "best_point": best_label,
            "sample": f"full 1 GiB round trip (torch.abs/max/quantize_per_tensor/dequantize, quant.py:100-110), "
-                     f"best of >= 3 per thread count, thread counts {counts}; {os.cpu_count()} CPUs visible, "
-                     f"{len(os.sched_getaffinity(0))} in this process's affinity mask",
+                     f"best of >= 3 per point; points: " + ", ".join(f"{k} ({v['threads']} thr)"
+                                                                      for k, v in results.items())
+                     + f"; {os.cpu_count()} CPUs visible, {len(os.sched_getaffinity(0))} in the affinity mask",
            "cpu_model": cpu_model(), "ms_per_round_trip": round(best * 1e3, 1),
-           "by_threads": {str(t): {"GiB_per_s": round(gib / v[0], 3), "ms_per_round_trip": round(v[0] * 1e3, 1),
-                                   "runs": v[1]} for t, v in per_threads.items()}}
-    return cpu, parity
+           "by_point": {k: ({"threads": v["threads"], "GiB_per_s": round(gib / v["best_s"], 3),
+                             "ms_per_round_trip": round(v["best_s"] * 1e3, 1), "runs": v["runs"]}
+                            if "best_s" in v else v) for k, v in results.items()}}
+    return cpu, (all(parity) if parity else None)
 
 
 def cold_decode_ms(lib, qp, n, sp, op, stream, reps: int = 10) -> float:
@@ -353,6 +428,57 @@ def copy_ceiling_GBs(x: torch.Tensor, out: torch.Tensor, stream, reps: int = 10)
     torch.cuda.synchronize()
     ms = sorted(e0.elapsed_time(e1) for e0, e1 in evs)[reps // 2]
     return 2 * x.numel() * x.element_size() / (ms * 1e-3) / 1e9
+
+
+_FP_MUL = -7046029254386353131        # 0x9E3779B97F4A7C15 as int64 (golden-ratio multiplier)
+
+
+def fingerprint(t: torch.Tensor) -> int:
+    """A 64-bit, position-sensitive fingerprint of t's bytes, computed where t lives (wrapping int64
+    arithmetic): sum over 8-byte words w_i of mix(w_i * M + i), mix(y) = y ^ (y >> 29). Equal bytes give
+    equal fingerprints; a flipped, lost or misplaced word changes it except with negligible probability."""
+    b = t.detach().reshape(-1).view(torch.uint8)
+    if b.numel() % 8:
+        b = torch.cat([b, b.new_zeros(8 - b.numel() % 8)])
+    w = b.view(torch.int64)
+    y = w * _FP_MUL + torch.arange(w.numel(), device=w.device, dtype=torch.int64)
+    y = y ^ (y >> 29)
+    return int(y.sum().item())
+
+
+def exchange_verify(ex, flat: torch.Tensor, world: int) -> dict:
+    """Checks the exchange leg's last all-gather and mean on every rank (run after the timed steps):
+    * rows:  every rank all-gathers the fingerprint of each of its own message rows; every received row,
+             on every rank and chunk, must match its sender's fingerprint, and row `rank` must equal the
+             local row byte for byte — the RCCL/xGMI transport delivered exactly what was sent;
+    * mean:  one exact_self=False mean (all K decoded payloads in rank order) must be bit-identical on every
+             rank (fingerprints all-gathered).
+    The verdict is agreed over ranks (MIN all-reduce), so every rank reports the same `parity`."""
+    import torch.distributed as dist
+    works = ex.encode_and_gather(flat)
+    for w in works:
+        if w is not None:
+            w.wait()
+    own_ok = all(torch.equal(g[ex.rank], loc) for g, loc in zip(ex.gathered, ex.local))
+    sent = [None] * world
+    dist.all_gather_object(sent, [fingerprint(loc) for loc in ex.local])
+    bad_rows = [(r, c) for c, g in enumerate(ex.gathered) for r in range(world) if fingerprint(g[r]) != sent[r][c]]
+    saved = ex.exact_self
+    ex.exact_self = False
+    try:
+        m = ex.mean([None] * len(works))
+    finally:
+        ex.exact_self = saved
+    means = [None] * world
+    dist.all_gather_object(means, fingerprint(m))
+    mean_ok = len(set(means)) == 1
+    ok = own_ok and not bad_rows and mean_ok
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32,
+                        device=flat.device if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    return {"parity": bool(flag.item()), "own_row_equal": own_ok, "rows_checked": world * len(ex.gathered),
+            "rows_mismatched": bad_rows[:8], "mean_identical_on_all_ranks": mean_ok,
+            "mean_fingerprint": f"{means[0] & 0xFFFFFFFFFFFFFFFF:016x}"}
 
 
 def exchange_leg(x: torch.Tensor, out: torch.Tensor, bits: int, world: int, steps: int, warmup: int):
@@ -397,8 +523,10 @@ def exchange_leg(x: torch.Tensor, out: torch.Tensor, bits: int, world: int, step
     t = max_over_ranks(time.perf_counter() - t0, world) / steps
     seg = [max_over_ranks(sum(e[i].elapsed_time(e[i + 1]) for e in evs) / steps, world) for i in range(3)]
     recv = ex.bytes_per_rank * (world - 1)          # bytes each rank receives (rccl-tests: busbw)
+    check = exchange_verify(ex, flat, world)        # after the timed steps: never inside them
     return {"workload": f"C4: {world} simulated clients x 1 GiB fp32, SLQ bits={bits} encode + RCCL "
                         f"all_gather_into_tensor + fused decode-mean", "steps": steps,
+            "parity": check.pop("parity"), "check": check,
             "ms_per_step": round(t * 1e3, 4), "GiB_per_s": round(world * n * 4 / GIB / t, 2),
             "encode_ms": round(seg[0], 4), "allgather_wait_ms": round(seg[1], 4), "mean_ms": round(seg[2], 4),
             "bytes_per_rank_on_wire": ex.bytes_per_rank,
@@ -440,6 +568,8 @@ def main():
         return plumbing_check(args)
     if args.pmc_child:
         return pmc_child(args)
+    if args.cpu_child:
+        return cpu_child(args)
     world, rank, local = dist_setup(args)
     assert world == args.gpus, (world, args.gpus)
     from adfl_amd import ops
@@ -514,6 +644,7 @@ def main():
     alg_bytes = KERNEL_BYTES[dominant] * n
     achieved = alg_bytes / (per_kernel[dominant] * 1e-3) / 1e9
     kernels_ms = sum(per_kernel.values())
+    cold_ms = per_kernel["absmax"] + per_kernel["quantize"] + decode_cold
     line = {
         "metric": "GiB/s device-resident quantize+dequantize, 1 GiB fp32 grads, 1/2/4/8 GPU",
         "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -527,6 +658,10 @@ def main():
                      "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": round(per_kernel[dominant], 4)},
         "kernels_ms": {k: round(v, 4) for k, v in per_kernel.items()},
         "decode_cold_ms": round(decode_cold, 4),
+        # the receiver-side round trip: a peer decodes a payload that did not just leave its own encode
+        "cold_round_trip": {"kernel_ms": round(cold_ms, 4), "GiB_per_s": round(gib_per_rank / (cold_ms * 1e-3), 2),
+                            "achieved_GBs": round(14 * n / (cold_ms * 1e-3) / 1e9, 1),
+                            "frac": round(14 * n / (cold_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
         "copy_ceiling_GBs": round(copy_ceiling, 1),
         "round_trip_roofline": {"alg_bytes": 14 * n, "kernel_ms": round(kernels_ms, 4),
                                 "achieved_GBs": round(14 * n / (kernels_ms * 1e-3) / 1e9, 1),

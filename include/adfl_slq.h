@@ -52,6 +52,10 @@ int64_t adfl_slq_workspace_bytes(void);
 /* Pass 1 of encode: max|x| partials into d_workspace (torch.max(torch.abs(t)), quant.py:100). */
 int adfl_slq_absmax(const float* d_x, int64_t n, void* d_workspace, int64_t workspace_bytes, void* stream);
 
+/* max|x| of pass 1 as one fp32 value into d_absmax[0] (torch.max(torch.abs(t)), quant.py:100; NaN
+ * propagates): reduces the partials adfl_slq_absmax left in d_workspace, which stay valid for pass 2. */
+int adfl_slq_absmax_value(const void* d_workspace, float* d_absmax, void* stream);
+
 /* Pass 2 of encode: reduce the partials, scale = absmax/q_max (quant.py:99-100), write d_scale[0],
  * quantize x into d_q (torch.quantize_per_tensor(t, scale, 0, qint8), quant.py:102-103). */
 int adfl_slq_quantize(const float* d_x, int64_t n, int bits, const void* d_workspace, int8_t* d_q,
@@ -101,7 +105,8 @@ int adfl_slq_encode_batched(const float* d_x, const adfl_slq_chunk* d_chunks, in
  * and returns the count; it returns 0 if some tensor is larger (call with work == NULL to size). The list
  * is copied to the device once per layout, like the chunk table. adfl_slq_encode_batched_work() with
  * nwork == 0 is adfl_slq_encode_batched (the two-pass encode), so a caller can always go through it.
- * d_partials is used only by the two-pass encode. */
+ * d_partials is used only by the two-pass encode. A work list entry naming a tensor with more than
+ * ADFL_SLQ_RESIDENT_CHUNKS chunks (not one adfl_slq_build_encode_work made) gets a NaN scale and no payload. */
 #define ADFL_SLQ_RESIDENT_CHUNKS 8
 int64_t adfl_slq_build_encode_work(const adfl_slq_chunk* chunks, int64_t nchunks, int32_t* work, int64_t capacity);
 int adfl_slq_encode_batched_work(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks,
@@ -190,8 +195,9 @@ int adfl_slq_dequantize_mean_self_int4(const uint8_t* d_packed, int64_t row_stri
  * (Src/ADFL/model.py:337-347) for each model: the client pool's add_to_model / add_to_model_all
  * (Src/ADFL/Client/pool.py:62-75) and QAFeL's hidden-state update (Src/ADFL/Server/qafel.py:176-179).
  * The payload is read once for all K models; each model is read and written once.
- *   d_q, d_chunks  a bucketed payload whose tensor offsets are multiples of 4 elements (e.g. an
- *                  ADFL_SLQ_ALIGN_ELEMS-aligned bucket); d_scales one fp32 per tensor
+ *   d_q, d_chunks  a bucketed payload, any tensor offsets (offsets that are multiples of 4 elements, e.g. an
+ *                  ADFL_SLQ_ALIGN_ELEMS-aligned bucket, take 16-byte accesses; others, e.g. a compact
+ *                  bucket, are decoded element-wise with the same result); d_scales one fp32 per tensor
  *   d_targets      DEVICE array of ntargets * ntensors device pointers, d_targets[k * ntensors + t] = the
  *                  fp32 storage of tensor t of model k (contiguous, 16-byte aligned, sizes as the table) */
 int adfl_slq_dequantize_add_batched(const int8_t* d_q, const adfl_slq_chunk* d_chunks, int64_t nchunks,

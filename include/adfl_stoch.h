@@ -98,7 +98,8 @@ int adfl_cnat_dequantize_batched(const int8_t* d_exps, const int8_t* d_signs, co
  * ADFL_SLQ_RESIDENT_CHUNKS chunks: d_work / nwork is the work list of adfl_slq_build_encode_work (the first
  * chunk of every tensor; nwork == 0 when some tensor is larger). A 1024-thread block holds one whole tensor
  * in registers, reduces its norm and quantizes it: x read once, no workspace, no fix-up launch. With
- * nwork == 0 these run the multi-launch encodes above (which need the workspace). */
+ * nwork == 0 these run the multi-launch encodes above (which need the workspace). A work list entry naming a
+ * tensor with more than ADFL_SLQ_RESIDENT_CHUNKS chunks gets a NaN norm and no payload. */
 int adfl_qsgd_encode_batched_work(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks,
                                   const int32_t* d_work, int64_t nwork, int bits, const float* d_uniforms,
                                   uint64_t seed, uint64_t counter, void* d_workspace, int64_t workspace_bytes,

@@ -69,6 +69,8 @@ def test_argument_errors_return_codes_without_launching():
     assert lib.adfl_slq_absmax(20, 10, 16, 1 << 20, None) == -3                  # misaligned x
     assert lib.adfl_slq_absmax(16, 10, 16, 16, None) == -4                       # workspace too small
     assert lib.adfl_slq_absmax(16, 0, 16, 1 << 20, None) == -1                   # empty
+    assert lib.adfl_slq_absmax_value(None, 16, None) == -1
+    assert lib.adfl_slq_absmax_value(20, 16, None) == -3                          # misaligned workspace
     assert lib.adfl_slq_dequantize(16, 10, 16, 20, None) == -3
     assert lib.adfl_slq_dequantize_mean(16, 8, 2, 10, 16, 1, 16, None) == -1    # row stride < n
     assert lib.adfl_slq_dequantize_mean(16, 24, 2, 10, 16, 1, 16, None) == -3   # row stride % 16

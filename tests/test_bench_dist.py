@@ -84,3 +84,34 @@ def test_bench_failing_rank_fails_launch():
     """A rank that dies makes the launcher exit non-zero instead of hanging at the barrier."""
     r, lines = _run_bench(["--gpus", "3", "--plumbing-check"], {"ADFL_PLUMBING_FAIL_RANK": "1"})
     assert r.returncode == 3 and not lines
+
+
+def test_cpu_sweep_points_cover_the_physical_core_counts():
+    """The CPU baseline sweep (bench.cpu_sweep_points): the default point unpinned, then 1 thread and the
+    physical cores of one socket (and of every socket when there are several), pinned, each CPU list inside
+    this process's affinity mask and one hardware thread per core."""
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, repo)
+    import bench
+    pts = bench.cpu_sweep_points()
+    labels = [p[0] for p in pts]
+    assert labels[0] == "default" and pts[0][1] is None
+    assert labels[1] == "1 thread" and pts[1][2] == 1
+    assert any("physical cores" in lbl for lbl in labels)
+    allowed = os.sched_getaffinity(0)
+    for label, cpus, threads in pts[1:]:
+        assert set(cpus) <= allowed and len(cpus) == threads, label
+
+
+def test_cpu_child_times_the_reference_ops_pinned(tmp_path):
+    """One sweep point in its own process: pinned to the given CPUs, reads the input file, prints its
+    best-of round trip as the one JSON line."""
+    import numpy as np
+    path = tmp_path / "x.f32"
+    (np.random.default_rng(0).standard_normal(1 << 16, dtype=np.float32) * np.float32(1e-3)).tofile(path)
+    cpu = sorted(os.sched_getaffinity(0))[0]
+    r, lines = _run_bench(["--cpu-child", "--cpu-input", str(path), "--cpu-list", str(cpu), "--cpu-seconds", "0.05"],
+                          {"OMP_NUM_THREADS": "1"})
+    assert r.returncode == 0, r.stderr
+    assert len(lines) == 1 and lines[0]["affinity"] == 1 and lines[0]["threads"] == 1
+    assert lines[0]["runs"] >= 3 and lines[0]["best_s"] > 0

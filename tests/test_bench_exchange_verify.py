@@ -1,0 +1,96 @@
+"""CPU, world_size 2 (gloo): bench.py's self-check of the N > 1 exchange leg (exchange_verify) — the
+fingerprints of every gathered row against its sender's, the own row byte for byte, and the
+exact_self=False mean bit-identical on every rank (Examples/ray_ad.py:188) — driven with the oracle codec
+in place of the HIP codec, plus a rank whose received row is corrupted: every rank must then report
+parity false."""
+
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _worker(rank, world, port, corrupt, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import bench
+        from adfl_amd.exchange import PeerExchange
+        from test_exchange_gloo import OracleCodec
+
+        results = []
+        for numel, bits, packed, chunks in [(4099, 8, False, 1), (12345, 4, True, 3)]:
+            ex = PeerExchange(numel, bits=bits, packed=packed, chunks=chunks, device=torch.device("cpu"),
+                              codec=OracleCodec())
+            rng = np.random.default_rng(50 + rank)
+            x = torch.from_numpy(rng.standard_normal(numel, dtype=np.float32) * np.float32(1e-3))
+            if corrupt:
+                # the transport "loses" a byte of rank 0's row on rank 1 only: wrap the gather's wait
+                orig = ex.encode_and_gather
+
+                def tampered(flat, orig=orig, ex=ex):
+                    works = orig(flat)
+                    for w in works:
+                        w.wait()
+                    if rank == 1:
+                        ex.gathered[-1][0, 3] ^= 0x40
+                    return [None] * len(works)
+
+                ex.encode_and_gather = tampered
+            results.append(bench.exchange_verify(ex, x, world))
+        q.put((rank, results))
+        dist.destroy_process_group()
+    except Exception as e:  # surfaced in the parent
+        import traceback
+        q.put((rank, f"error {e!r}\n{traceback.format_exc()}"))
+
+
+def _run(corrupt):
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, corrupt, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for r, v in res.items():
+        assert not isinstance(v, str), v
+    return res
+
+
+def test_exchange_verify_passes_on_a_clean_exchange():
+    res = _run(corrupt=False)
+    for rank, checks in res.items():
+        for c in checks:
+            assert c["parity"] and c["own_row_equal"] and c["mean_identical_on_all_ranks"], (rank, c)
+            assert c["rows_mismatched"] == []
+    # both ranks hold the identical exact_self=False mean
+    assert [c["mean_fingerprint"] for c in res[0]] == [c["mean_fingerprint"] for c in res[1]]
+
+
+def test_exchange_verify_flags_a_corrupted_row_on_every_rank():
+    res = _run(corrupt=True)
+    for rank, checks in res.items():
+        for c in checks:
+            assert c["parity"] is False, (rank, c)       # the verdict is agreed over ranks
+    assert all(c["rows_mismatched"] for c in res[1])      # rank 1 names rank 0's row it received
+    assert all(not c["rows_mismatched"] for c in res[0])
+
+
+def test_fingerprint_is_position_sensitive():
+    import bench
+    a = torch.arange(1000, dtype=torch.int32)
+    b = a.clone()
+    b[[10, 11]] = b[[11, 10]]
+    assert bench.fingerprint(a) == bench.fingerprint(a.clone())
+    assert bench.fingerprint(a) != bench.fingerprint(b)
+    c = a.clone().view(torch.uint8)
+    c[7] ^= 1
+    assert bench.fingerprint(a) != bench.fingerprint(c)

@@ -18,10 +18,14 @@ from adfl_amd.Channel import SLQChannel  # noqa: E402
 DEV = torch.device("cuda", 0)
 
 
-@pytest.mark.parametrize("sizes,k", [([1, 3, 5, 8192, 8193, 70001], 3), ([1 << 20], 1), ([64] * 300, 8)])
-def test_dequantize_add_matches_oracle(sizes, k):
+@pytest.mark.parametrize("align", [64, 1, 2])
+@pytest.mark.parametrize("sizes,k", [([1, 3, 5, 8192, 8193, 70001], 3), ([1 << 20], 1), ([64] * 300, 8),
+                                     ([7, 1, 8191, 8195, 13, 40000, 2], 2)])
+def test_dequantize_add_matches_oracle(sizes, k, align):
+    """Aligned buckets (offsets multiples of 64: 16-byte path) and compact ones (align 1 / 2: offsets with every
+    residue mod 4, the element-wise path; include/adfl_slq.h no longer requires 4-element offsets)."""
     rng = np.random.default_rng(len(sizes) * 10 + k)
-    lay = ops.BucketLayout(sizes)  # aligned: offsets are multiples of 64
+    lay = ops.BucketLayout(sizes, align=align)
     flat = np.zeros(lay.total, np.float32)
     xs = []
     for off, n in zip(lay.offsets, sizes):
@@ -50,8 +54,6 @@ def test_dequantize_add_rejects_bad_targets():
         ops.dequantize_add_batched(q, s, lay, [[good[0], torch.zeros(21, device=DEV)]])
     with pytest.raises(ValueError, match="16-byte aligned fp32"):
         ops.dequantize_add_batched(q, s, lay, [[good[0], torch.zeros(21, device=DEV)[1:]]])
-    with pytest.raises(ValueError, match="multiples of 4"):
-        ops.dequantize_add_batched(q, s, ops.BucketLayout([10, 20], align=1), [good])
 
 
 def _model(seed, device):

@@ -35,3 +35,21 @@ def test_bench_emits_one_contract_line():
     assert 0.0 < rf["frac"] < 1.0 and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
     assert rf["alg_bytes_per_launch"] > 0 and rf["avg_launch_ms"] > 0
     assert d["cpu_baseline"] is None  # --no-cpu-baseline
+    # the receiver-side round trip: absmax + quantize + a decode whose payload is not in the Infinity Cache
+    cr = d["cold_round_trip"]
+    assert abs(cr["kernel_ms"] - (d["kernels_ms"]["absmax"] + d["kernels_ms"]["quantize"] + d["decode_cold_ms"])) < 2e-4
+    assert 0.0 < cr["frac"] < 1.0 and cr["GiB_per_s"] > 0
+
+
+def test_bench_exchange_leg_checks_itself():
+    """The C4 exchange leg at world 1 over RCCL (--exchange on): after its timed steps it verifies the
+    gathered rows against the sent rows and the exact_self=False mean across ranks, and says so."""
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2", "--warmup", "1",
+                        "--no-cpu-baseline", "--pmc", "off", "--exchange", "on"],
+                       cwd=REPO, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])
+    ex = d["exchange"]
+    assert "error" not in ex, ex
+    assert ex["parity"] is True, ex
+    assert ex["check"]["own_row_equal"] and ex["check"]["rows_checked"] == 1 and ex["backend"] == "nccl"

@@ -1,0 +1,174 @@
+"""GPU: the torch.ops.adfl.* custom ops (SURVEY.md §8b's surface) called through the op registry, each
+against the oracle bit for bit, each through torch.library.opcheck (schema, fake implementation, AOT
+dispatch), and a codec pipeline under torch.compile (aot_eager, fullgraph) equal to eager.
+
+Reference loops: Src/ADFL/Channel/quant.py:74-94 (per-tensor encode of a state dict) and :97-112,
+Src/ADFL/compression.py:35-66 (pack_4bit / unpack_4bit), Examples/ray_ad.py:188 (peer mean)."""
+
+import numpy as np
+import pytest
+import torch
+
+import slq_oracle as oracle
+
+pytestmark = pytest.mark.gpu
+
+import adfl_amd  # noqa: E402,F401  registers torch.ops.adfl.*
+
+DEV = torch.device("cuda", 0)
+A = torch.ops.adfl
+
+
+def _bucket(seed, sizes, gap=0, order=None):
+    """Flat fp32 buffer with tensors at offsets separated by `gap` elements, in `order` (a permutation)."""
+    rng = np.random.default_rng(seed)
+    order = list(range(len(sizes))) if order is None else order
+    offsets = [0] * len(sizes)
+    pos = 0
+    for t in order:
+        offsets[t] = pos
+        pos += sizes[t] + gap
+    flat = np.zeros(pos, np.float32)
+    for t, n in enumerate(sizes):
+        flat[offsets[t]:offsets[t] + n] = rng.standard_normal(n, dtype=np.float32) * np.float32(10.0 ** -(t % 4))
+    return flat, torch.tensor(offsets, dtype=torch.int64), torch.tensor(sizes, dtype=torch.int64)
+
+
+def _bits(a):
+    return np.ascontiguousarray(a).view(np.uint32 if a.dtype == np.float32 else np.uint8)
+
+
+def test_slq_absmax_matches_torch_max_abs():
+    for seed, n in [(0, 1), (1, 1027), (2, 1 << 20)]:
+        x = torch.from_numpy(np.random.default_rng(seed).standard_normal(n, dtype=np.float32))
+        got = A.slq_absmax(x.to(DEV))
+        assert got.shape == () and got.dtype == torch.float32
+        assert got.item() == torch.max(torch.abs(x)).item()
+    x = torch.ones(4099, device=DEV)
+    x[17] = float("nan")
+    assert torch.isnan(A.slq_absmax(x)).item()
+
+
+@pytest.mark.parametrize("bits", [8, 4, 2])
+@pytest.mark.parametrize("gap,order", [(0, None), (5, None), (3, [2, 0, 3, 1, 4])])
+def test_encode_decode_batched_match_oracle(bits, gap, order):
+    sizes = [1, 4097, 8192, 70001, 33]
+    flat, off, siz = _bucket(bits + gap, sizes, gap, order)
+    q, s = A.slq_encode_batched(torch.from_numpy(flat).to(DEV), off, siz, bits)
+    d = A.slq_decode_batched(q, s, off, siz)
+    qo, so = oracle.encode_batched(flat, off.numpy(), siz.numpy(), bits)
+    assert q.shape == (flat.size,) and s.shape == (len(sizes),)
+    assert np.array_equal(q.cpu().numpy(), qo)                   # gaps are zero on both sides
+    assert np.array_equal(_bits(s.cpu().numpy()), _bits(so))
+    want = np.zeros(flat.size, np.float32)
+    for t, (o, n) in enumerate(zip(off.tolist(), sizes)):
+        want[o:o + n] = oracle.decode(qo[o:o + n], so[t])
+    assert np.array_equal(_bits(d.cpu().numpy()), _bits(want))
+
+
+@pytest.mark.parametrize("gap", [0, 6])
+def test_encode_decode_batched_int4_match_oracle(gap):
+    """int4 buckets need even tensor offsets: each slot is the tensor rounded up to even, plus `gap`."""
+    sizes = [2, 4097, 8192, 70001, 31]
+    offsets, pos = [], 0
+    for n in sizes:
+        offsets.append(pos)
+        pos += n + n % 2 + gap
+    rng = np.random.default_rng(40 + gap)
+    flat = np.zeros(pos, np.float32)
+    for o, n in zip(offsets, sizes):
+        flat[o:o + n] = rng.standard_normal(n, dtype=np.float32) * np.float32(1e-2)
+    off, siz = torch.tensor(offsets), torch.tensor(sizes)
+    p, s = A.slq_encode_batched_int4(torch.from_numpy(flat).to(DEV), off, siz, 4)
+    d = A.slq_decode_batched_int4(p, s, off, siz, flat.size)
+    ph, sh, dh = p.cpu().numpy(), s.cpu().numpy(), d.cpu().numpy()
+    assert ph.size == (flat.size + 1) // 2 and dh.size == flat.size
+    for t, (o, n) in enumerate(zip(offsets, sizes)):
+        qo, so = oracle.encode(flat[o:o + n], 4)
+        packed = oracle.pack_int4(qo)   # an odd tensor's last byte pairs its last element with pack_4bit's pad
+        assert _bits(np.float32(so)) == _bits(sh[t:t + 1])[0], t
+        assert np.array_equal(ph[o // 2:o // 2 + packed.size], packed), t
+        assert np.array_equal(_bits(dh[o:o + n]), _bits(oracle.decode_int4(packed, n, so))), t
+
+
+def test_pack_unpack_int4_match_oracle():
+    rng = np.random.default_rng(3)
+    for n in (1, 2, 7, 4096, 100003):
+        q = rng.integers(-8, 8, n, dtype=np.int8)
+        p = A.pack_int4(torch.from_numpy(q).to(DEV))
+        assert np.array_equal(p.cpu().numpy(), oracle.pack_int4(q)), n
+        u = A.unpack_int4(p, [n])
+        assert np.array_equal(u.cpu().numpy(), oracle.unpack_int4(oracle.pack_int4(q), n)), n
+    u = A.unpack_int4(A.pack_int4(torch.from_numpy(q[:12]).to(DEV)), [3, 4])
+    assert u.shape == (3, 4)
+
+
+@pytest.mark.parametrize("self_row", [-1, 0, 2])
+def test_dequantize_mean_matches_oracle(self_row):
+    k, n = 4, 10007
+    rng = np.random.default_rng(11 + self_row)
+    xs = [rng.standard_normal(n, dtype=np.float32) * np.float32(10.0 ** -r) for r in range(k)]
+    encs = [oracle.encode(x, 8) for x in xs]
+    row = (n + 15) // 16 * 16
+    rows = np.zeros((k, row), np.int8)
+    for r, (q, _) in enumerate(encs):
+        rows[r, :n] = q
+    scales = np.array([s for _, s in encs], np.float32)
+    self_x = torch.from_numpy(xs[self_row]).to(DEV) if self_row >= 0 else None
+    got = A.slq_dequantize_mean(torch.from_numpy(rows).to(DEV), torch.from_numpy(scales).to(DEV), n, self_row,
+                                self_x).cpu().numpy()
+    want = (oracle.dequantize_mean_self([r for r in rows[:, :n]], scales, n, self_row, xs[self_row])
+            if self_row >= 0 else oracle.dequantize_mean([r for r in rows[:, :n]], scales))
+    assert np.array_equal(_bits(got), _bits(want))
+
+
+def _opcheck_cases():
+    flat, off, siz = _bucket(5, [3, 4097, 900], 2)
+    x = torch.from_numpy(flat).to(DEV)
+    q, s = A.slq_encode_batched(x, off, siz, 8)
+    p4, s4 = A.slq_encode_batched_int4(torch.zeros(6000, device=DEV).normal_(), torch.tensor([0, 4000]),
+                                       torch.tensor([3999, 1000]), 4)
+    rows = torch.randint(-128, 128, (3, 1024), dtype=torch.int8, device=DEV)
+    return [
+        (A.slq_absmax, (x,)),
+        (A.slq_encode, (x.reshape(1, -1), 8)),
+        (A.slq_decode, (q.reshape(1, -1), s[:1])),
+        (A.slq_encode_int4, (x, 4)),
+        (A.slq_decode_int4, (A.pack_int4(q), q.numel(), s[:1])),
+        (A.slq_encode_batched, (x, off, siz, 8)),
+        (A.slq_decode_batched, (q, s, off, siz)),
+        (A.slq_encode_batched_int4, (torch.zeros(6000, device=DEV).normal_(), torch.tensor([0, 4000]),
+                                     torch.tensor([3999, 1000]), 4)),
+        (A.slq_decode_batched_int4, (p4, s4, torch.tensor([0, 4000]), torch.tensor([3999, 1000]), 6000)),
+        (A.pack_int4, (q,)),
+        (A.unpack_int4, (A.pack_int4(q), [q.numel()])),
+        (A.slq_dequantize_mean, (rows, torch.rand(3, device=DEV), 1000, -1, None)),
+        (A.slq_dequantize_mean, (rows, torch.rand(3, device=DEV), 1000, 1, torch.randn(1000, device=DEV))),
+    ]
+
+
+@pytest.mark.parametrize("case", range(13))
+def test_opcheck(case):
+    op, args = _opcheck_cases()[case]
+    torch.library.opcheck(op, args)
+
+
+def test_codec_pipeline_under_torch_compile():
+    """encode -> decode -> mean of a bucketed update traced by torch.compile (fullgraph: every op goes through
+    its fake implementation at trace time, the HIP kernels at run time) equals eager bit for bit."""
+    flat, off, siz = _bucket(9, [4096, 80, 8192], 0)   # 12,368 elements: a 16-byte multiple row
+    x = torch.from_numpy(flat).to(DEV)
+
+    def pipeline(x):
+        q, s = torch.ops.adfl.slq_encode_batched(x, off, siz, 8)
+        d = torch.ops.adfl.slq_decode_batched(q, s, off, siz)
+        p, sc = torch.ops.adfl.slq_encode_int4(x, 4)
+        d4 = torch.ops.adfl.slq_decode_int4(p, x.numel(), sc)
+        rows = torch.stack([q, q]).contiguous()
+        m = torch.ops.adfl.slq_dequantize_mean(rows, torch.cat([s[:1], s[:1]]), x.numel(), -1, None)
+        return d, d4, m, torch.ops.adfl.slq_absmax(x)
+
+    eager = pipeline(x)
+    compiled = torch.compile(pipeline, backend="aot_eager", fullgraph=True)(x)
+    for e, c in zip(eager, compiled):
+        assert torch.equal(e.view(torch.int32), c.view(torch.int32))
