@@ -49,8 +49,6 @@ SIGNATURES = {
     "adfl_slq_encode_batched": (INT, [P, P, I64, INT, P, P, P, P]),
     "adfl_slq_build_encode_work": (I64, [P, I64, P, I64]),
     "adfl_slq_encode_batched_work": (INT, [P, P, I64, P, I64, INT, P, P, P, P]),
-    "adfl_slq_coop_capacity": (I64, []),
-    "adfl_slq_encode_batched_coop": (INT, [P, P, I64, INT, P, P, P, P, P]),
     "adfl_slq_dequantize_batched": (INT, [P, P, I64, P, P, P]),
     "adfl_slq_qerror_batched": (INT, [P, P, P, I64, P, P, P]),
     "adfl_slq_qerror_batched_int4": (INT, [P, P, P, I64, P, P, P]),

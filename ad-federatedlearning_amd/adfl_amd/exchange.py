@@ -22,10 +22,15 @@ Transport: RCCL (``nccl`` backend) all-gathers device rows directly over xGMI. W
 (``Examples/ray_ad.py:29``), which RCCL cannot form because it needs distinct devices per rank — each row
 is staged through pinned host memory: D2H, gloo all-gather, H2D.
 
-With ``chunks > 1`` (the C5 4 GiB/client int4 variant) the absmax pass runs over the whole update first
-(the scale needs the global max), then chunk c is quantized while chunk c-1's all-gather is in flight:
-each all-gather is issued ``async_op=True`` right after its chunk's quantize, so RCCL's stream runs it
-concurrently with the next quantize on the compute stream.
+Streams (device ranks). The absmax pass runs over the whole update on the caller's stream (the scale needs
+the global max). Every chunk's quantize is then enqueued at once on a side HIP stream, one event recorded
+after each; chunk c's all-gather is issued from a gather stream that waits on event c only, so RCCL's
+stream starts chunk c as soon as its quantize retires, while chunk c+1's quantize runs on the side stream.
+Enqueuing all the quantizes before any collective keeps the side stream busy back to back: issuing one
+all-gather costs the host about as long as quantizing a C5 chunk (tools/exchange_trace.py measured
+~100 us host gaps between the chunk quantizes when each quantize waited for the previous chunk's
+all_gather call to return). The caller's stream waits for the side stream before encode_and_gather
+returns, so later work there (the mean, or a write to x) is ordered after the quantizes.
 
 The codec backend is injectable so the exchange protocol can be exercised by gloo on CPU in tests; the
 product backend is the HIP codec (``HipCodec``) and there is no other.
@@ -125,6 +130,9 @@ class PeerExchange:
             self.local_host = [torch.empty(rb, dtype=torch.uint8, pin_memory=True) for rb in self.row_bytes]
             self.gathered_host = [torch.empty(self.world, rb, dtype=torch.uint8, pin_memory=True)
                                   for rb in self.row_bytes]
+        if device.type == "cuda":
+            self.quant_stream = torch.cuda.Stream(device)    # the chunk quantizes
+            self.gather_stream = torch.cuda.Stream(device)   # issues each all-gather behind its chunk's event
 
     def _payload_bytes(self, n: int) -> int:
         return (n + 1) // 2 if self.packed else n
@@ -145,17 +153,41 @@ class PeerExchange:
         x = x.reshape(-1)
         self._x = x
         self.codec.absmax(x)
+        if self.device.type != "cuda":   # host tensors (the protocol tests' codec): one sequence, no streams
+            works = []
+            for c in range(len(self.bounds)):
+                self.codec.quantize(self._chunk(x, c), self.bits, self.packed, self.local[c], self.payload[c])
+                works.append(self._gather(c))
+            return works
+        main, qs, gs = torch.cuda.current_stream(self.device), self.quant_stream, self.gather_stream
+        qs.wait_stream(main)             # the absmax partials (and x itself) are made on the caller's stream
+        x.record_stream(qs)
+        done = []
+        with torch.cuda.stream(qs):
+            for c in range(len(self.bounds)):
+                self.codec.quantize(self._chunk(x, c), self.bits, self.packed, self.local[c], self.payload[c])
+                done.append(qs.record_event())
         works = []
-        for c, ((c0, c1), row, out, pb) in enumerate(zip(self.bounds, self.local, self.gathered, self.payload)):
-            self.codec.quantize(x[c0:c1], self.bits, self.packed, row, pb)
-            if self.host_staged:
-                lh, gh = self.local_host[c], self.gathered_host[c]
-                lh.copy_(row)  # blocking D2H: also orders after the previous step's H2D from gh
-                w = dist.all_gather_into_tensor(gh.view(-1), lh, group=self.group, async_op=True)
-                works.append(_StagedGather(w, gh, out))
-            else:
-                works.append(dist.all_gather_into_tensor(out.view(-1), row, group=self.group, async_op=True))
+        with torch.cuda.stream(gs):      # RCCL (or the staging copy) syncs with this stream: chunk c only
+            for c, ev in enumerate(done):
+                gs.wait_event(ev)
+                works.append(self._gather(c))
+        main.wait_stream(qs)
         return works
+
+    def _chunk(self, x: torch.Tensor, c: int) -> torch.Tensor:
+        c0, c1 = self.bounds[c]
+        return x[c0:c1]
+
+    def _gather(self, c: int):
+        """Issue chunk c's all-gather (async) from the current stream's position."""
+        row, out = self.local[c], self.gathered[c]
+        if self.host_staged:
+            lh, gh = self.local_host[c], self.gathered_host[c]
+            lh.copy_(row)  # blocking D2H: also orders after the previous step's H2D from gh
+            w = dist.all_gather_into_tensor(gh.view(-1), lh, group=self.group, async_op=True)
+            return _StagedGather(w, gh, out)
+        return dist.all_gather_into_tensor(out.view(-1), row, group=self.group, async_op=True)
 
     def mean(self, works: List, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Wait for each chunk's all-gather and decode the K payloads into their fp32 mean (a `None` work

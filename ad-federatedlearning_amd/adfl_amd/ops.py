@@ -225,7 +225,6 @@ class BucketLayout:
         self.max_tensor_chunks = int(max(c.nchunks for c in self.chunks))
         self._device_chunks = {}
         self._device_work = {}
-        self._device_sync = {}
 
     def device_chunks(self, device: torch.device) -> torch.Tensor:
         key = (device.type, device.index)
@@ -245,23 +244,10 @@ class BucketLayout:
         return t
 
 
-    def device_sync(self, device: torch.device, stream: int) -> torch.Tensor:
-        """The cooperative encode's sync words (adfl_slq_encode_batched_coop): 2 * nchunks + 1 uint32, zeroed
-        once; every launch leaves them zero. One buffer per (device, stream), so encodes of this layout on
-        two streams never share one."""
-        key = (device.type, device.index, stream)
-        t = self._device_sync.get(key)
-        if t is None:
-            t = torch.zeros(2 * self.nchunks + 1, dtype=torch.int32, device=device)
-            self._device_sync[key] = t
-        return t
-
-
 # Bucketed SLQ encode: "resident" (one 1024-thread block per tensor; every tensor <= 8 chunks), "twopass"
-# (absmax launch + quantize launch), "coop" (one cooperative launch of chunk blocks that meet per tensor, any
-# layout; opt-in: the cooperative launch measured ~20 us slower than the two passes on C3, DESIGN.md §4).
-# "auto" (the product): resident when the layout allows it, else the two passes.
-_ENCODE_MODES = ("auto", "resident", "coop", "twopass")
+# (absmax launch + quantize launch). "auto" (the product): resident when the layout allows it, else the two
+# passes.
+_ENCODE_MODES = ("auto", "resident", "twopass")
 
 
 def _encode_mode() -> str:
@@ -285,13 +271,7 @@ def encode_batched(flat: torch.Tensor, layout: BucketLayout, bits: int, *, q: Op
     scales = torch.empty(layout.ntensors, dtype=torch.float32, device=dev) if scales is None else scales
     partials = torch.empty(layout.nchunks, dtype=torch.int32, device=dev) if partials is None else partials
     lib, st = _lib.load(), _stream(dev)
-    mode = _encode_mode()
-    if mode == "coop":
-        check(lib.adfl_slq_encode_batched_coop(flat.data_ptr(), layout.device_chunks(dev).data_ptr(), layout.nchunks,
-                                               bits, q.data_ptr(), scales.data_ptr(), partials.data_ptr(),
-                                               layout.device_sync(dev, st).data_ptr(), st))
-        return q, scales
-    nwork = 0 if mode == "twopass" else layout.nwork
+    nwork = 0 if _encode_mode() == "twopass" else layout.nwork
     check(lib.adfl_slq_encode_batched_work(flat.data_ptr(), layout.device_chunks(dev).data_ptr(),
                                            layout.nchunks, layout.device_work(dev).data_ptr(),
                                            nwork, bits, q.data_ptr(),

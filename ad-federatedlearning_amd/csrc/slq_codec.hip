@@ -30,7 +30,6 @@
 
 #include <hip/hip_runtime.h>
 
-#include <atomic>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -656,87 +655,9 @@ __global__ __launch_bounds__(kBlock) void k_quantize_batched(const float* __rest
   chunk_store(c, r, si.inv, q, lds[wave], lane, wave);
 }
 
-// ---- one-launch encode of a bucket with tensors of any size (x read once; opt-in, measured slower) -------
-// One 256-thread block per chunk, every block co-resident (cooperative launch: the runtime refuses a
-// grid that cannot be resident at once, and the host then runs the two passes). A block loads its chunk
-// into VGPRs, reduces max|x|, and — when its tensor spans several chunks — publishes it to the tensor's
-// sync words and waits until every chunk of the tensor has: sync[2f] counts arrivals then departures
-// (0 .. 2*nchunks), sync[2f+1] holds the running max (f = the tensor's first chunk). The block that makes
-// the last departure zeroes both words, so the buffer is zero again when the launch ends (it must be zero
-// before the first one). A bounded wait (kCoopSpinLimit polls) sets sync[2*nchunks] and gives the tensor
-// a NaN scale instead of hanging; with the whole grid resident it is never reached.
-// The scale and payload are those of the two-pass encode: max is order-independent, same make_scale.
-// Measured on C3 (profiles/r02/coop/): the cooperative launch costs about 20 us more than an ordinary one
-// (log-uniform encode 43 us vs 24.7 us for the two passes; equal layout 38 vs 17 us resident). An ordinary
-// launch of the same grid took 23.6 us — 1 us under the two passes — but its progress would rest on every
-// block being resident, which nothing guarantees beside other streams' kernels, so it is not offered.
-// Poll back-off (s_sleep 1 .. 127) changed nothing (+-1 us). The product keeps resident / two-pass.
-constexpr uint32_t kCoopSpinLimit = 1u << 22;
-
-__device__ __forceinline__ uint32_t chunk_absmax(const adfl_slq_chunk& c, const ChunkRegs& r, int wave) {
-  const int head = chunk_head(c.start, c.len, 16);
-  const int ntiles = (c.len - head) / kTile;
-  uint32_t m = abs_bits(r.head);  // head/tail lanes past the chunk hold 0
-#pragma unroll
-  for (int k = 0; k < kChunkTailPerThread; ++k) m = max(m, abs_bits(r.tail[k]));
-#pragma unroll
-  for (int k = 0; k < kChunkTilesPerWave; ++k)
-    if (wave + k * kWaves < ntiles)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) m = max(m, abs_bits4(r.v[k][j]));
-  return m;
-}
-
-__global__ __launch_bounds__(kBlock) void k_encode_coop(const float* __restrict__ x,
-                                                        const adfl_slq_chunk* __restrict__ chunks, int32_t nchunks,
-                                                        float qmax, uint32_t* __restrict__ sync,
-                                                        int8_t* __restrict__ q, float* __restrict__ scales) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[kWaves][kTile / 4];
-  __shared__ uint32_t s_max;
-  const int64_t ci = blockIdx.x;
-  const adfl_slq_chunk c = chunks[ci];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  ChunkRegs r;
-  chunk_load(x, c, r, lane, wave);
-  uint32_t m = block_max(chunk_absmax(c, r, wave));
-  if (c.nchunks > 1) {
-    if (threadIdx.x == 0) {
-      uint32_t* cnt = sync + 2 * (int64_t)c.first_chunk;
-      uint32_t* mx = cnt + 1;
-      const uint32_t need = (uint32_t)c.nchunks;
-      // Only device-scope atomics (performed at the memory side) publish, and relaxed sc1 loads poll, so
-      // no L2 write-back / invalidate fence is needed: the max is in before the arrival is counted (the
-      // returning umax completes first), and read back by a returning umax after the count is complete.
-      m = max(m, __hip_atomic_fetch_max(mx, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));  // returning
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      uint32_t spins = 0;
-      bool ok = true;
-      while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-        if (++spins > kCoopSpinLimit) {
-          ok = false;
-          __hip_atomic_exchange(sync + 2 * (int64_t)nchunks, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(8);
-      }
-      m = max(m, __hip_atomic_fetch_max(mx, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (!ok) m = 0x7FC00000u;
-      // departure: the last one (count 2*need - 1 -> 2*need) zeroes the tensor's words
-      if (__hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 2 * need - 1) {
-        __hip_atomic_exchange(mx, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_exchange(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      s_max = m;
-    }
-    __syncthreads();
-    m = s_max;
-  }
-  const ScaleInv si = make_scale(m, qmax);
-  if (ci == c.first_chunk && threadIdx.x == 0) scales[c.tensor] = si.scale;
-  chunk_store(c, r, si.inv, q, lds[wave], lane, wave);
-}
+// A one-launch encode for tensors of any size (chunk blocks meeting per tensor in a cooperative launch) was
+// measured in round 2 and removed in round 3: the cooperative launch cost ~20 us more than an ordinary
+// one on C3 (log-uniform 43 vs 24.7 us two-pass; equal 38 vs 17 us resident; profiles/r02/coop/).
 
 
 // ---- one-launch encode of a bucket of small tensors (a whole tensor per block, x read once) -------
@@ -1187,48 +1108,6 @@ int adfl_slq_encode_batched(const float* d_x, const adfl_slq_chunk* d_chunks, in
   hipLaunchKernelGGL(k_quantize_batched, dim3((unsigned)nchunks), dim3(kBlock), 0, st, d_x, d_chunks, qmax_f(bits),
                      (const uint32_t*)d_partials, d_q, d_scales);
   return launch_status();
-}
-
-// Co-resident block capacity of k_encode_coop on the current device (occupancy x CUs), cached per device
-// (the stream passed to adfl_slq_encode_batched_coop must belong to the current device, as for every
-// launch here). Concurrent first calls compute the same value.
-static int64_t coop_capacity() {
-  static std::atomic<int64_t> cap[64];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  if (cap[dev].load(std::memory_order_relaxed) == 0) {
-    int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k_encode_coop), kBlock,
-                                                     0) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return 0;
-    cap[dev].store((int64_t)per_cu * cus, std::memory_order_relaxed);
-  }
-  return cap[dev].load(std::memory_order_relaxed);
-}
-
-int64_t adfl_slq_coop_capacity(void) { return coop_capacity(); }
-
-int adfl_slq_encode_batched_coop(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, int bits,
-                                 int8_t* d_q, float* d_scales, uint32_t* d_partials, uint32_t* d_sync,
-                                 void* stream) {
-  if (!d_x || !d_chunks || !d_q || !d_scales || !d_partials || !d_sync || nchunks < 1 || nchunks > INT32_MAX)
-    return ADFL_E_ARG;
-  if (int s = check_bits(bits)) return s;
-  if (!aligned16(d_x) || !aligned16(d_q)) return ADFL_E_ALIGN;
-  hipStream_t st = (hipStream_t)stream;
-  if (nchunks <= coop_capacity()) {
-    const float qmax = qmax_f(bits);
-    const int32_t n32 = (int32_t)nchunks;
-    const void* kern = reinterpret_cast<const void*>(k_encode_coop);
-    void* args[] = {(void*)&d_x, (void*)&d_chunks, (void*)&n32, (void*)&qmax, (void*)&d_sync, (void*)&d_q,
-                    (void*)&d_scales};
-    const hipError_t e = hipLaunchCooperativeKernel(kern, dim3((unsigned)nchunks), dim3(kBlock), args, 0, st);
-    if (e == hipSuccess) return ADFL_OK;
-    if (e != hipErrorCooperativeLaunchTooLarge) return (int)e;
-    (void)hipGetLastError();  // too large for one resident grid after all: the two passes
-  }
-  return adfl_slq_encode_batched(d_x, d_chunks, nchunks, bits, d_q, d_scales, d_partials, stream);
 }
 
 int64_t adfl_slq_build_encode_work(const adfl_slq_chunk* chunks, int64_t nchunks, int32_t* work, int64_t capacity) {

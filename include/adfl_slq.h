@@ -112,20 +112,6 @@ int64_t adfl_slq_build_encode_work(const adfl_slq_chunk* chunks, int64_t nchunks
 int adfl_slq_encode_batched_work(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks,
                                  const int32_t* d_work, int64_t nwork, int bits, int8_t* d_q, float* d_scales,
                                  uint32_t* d_partials, void* stream);
-/* One-launch encode (same output) for ANY bucket layout, tensors larger than one block included: one
- * block per chunk holds its chunk in registers; a tensor's blocks meet through d_sync (an arrival count and
- * a running max per tensor), so x is read once. The grid is launched cooperatively (every block resident
- * at once); when the chunk table exceeds adfl_slq_coop_capacity() the call runs adfl_slq_encode_batched
- * with d_partials instead. d_sync: 2 * nchunks + 1 uint32 of device memory, ZERO before the first call;
- * each call leaves it zero (the last block of a tensor clears its words). d_sync[2 * nchunks] != 0 after a
- * call means a block gave up waiting (never expected: that tensor's scale is NaN; zero the buffer again).
- * One call per d_sync at a time (stream-ordered reuse is fine). Replaces the same loop as
- * adfl_slq_encode_batched (Src/ADFL/Channel/quant.py:74-94 over quant.py:97-104). Opt-in: on MI355X the
- * cooperative launch costs more than the launch gap it removes. */
-int64_t adfl_slq_coop_capacity(void);
-int adfl_slq_encode_batched_coop(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, int bits,
-                                 int8_t* d_q, float* d_scales, uint32_t* d_partials, uint32_t* d_sync,
-                                 void* stream);
 int adfl_slq_dequantize_batched(const int8_t* d_q, const adfl_slq_chunk* d_chunks, int64_t nchunks,
                                 const float* d_scales, float* d_out, void* stream);
 

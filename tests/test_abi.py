@@ -75,10 +75,6 @@ def test_argument_errors_return_codes_without_launching():
     assert lib.adfl_slq_dequantize_mean(16, 8, 2, 10, 16, 1, 16, None) == -1    # row stride < n
     assert lib.adfl_slq_dequantize_mean(16, 24, 2, 10, 16, 1, 16, None) == -3   # row stride % 16
     assert lib.adfl_slq_encode_batched(16, 16, 0, 8, 16, 16, 16, None) == -1
-    assert lib.adfl_slq_encode_batched_coop(16, 16, 0, 8, 16, 16, 16, 16, None) == -1     # no chunks
-    assert lib.adfl_slq_encode_batched_coop(16, 16, 1, 8, 16, 16, 16, None, None) == -1   # no sync words
-    assert lib.adfl_slq_encode_batched_coop(16, 16, 1, 17, 16, 16, 16, 16, None) == -2    # bits
-    assert lib.adfl_slq_encode_batched_coop(20, 16, 1, 8, 16, 16, 16, 16, None) == -3     # x misaligned
     with pytest.raises(_lib.AdflError, match="bits"):
         _lib.check(-2)
 

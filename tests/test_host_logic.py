@@ -146,9 +146,13 @@ def test_encode_mode_selection(monkeypatch):
     bad value fails loudly instead of silently choosing one."""
     monkeypatch.delenv("ADFL_SLQ_ENCODE", raising=False)
     assert ops._encode_mode() == "auto"
-    for m in ("auto", "resident", "coop", "twopass"):
+    for m in ("auto", "resident", "twopass"):
         monkeypatch.setenv("ADFL_SLQ_ENCODE", m)
         assert ops._encode_mode() == m
+    for bad in ("fastest", "coop"):   # the cooperative encode was removed in round 3
+        monkeypatch.setenv("ADFL_SLQ_ENCODE", bad)
+        with pytest.raises(ValueError, match="ADFL_SLQ_ENCODE"):
+            ops._encode_mode()
     monkeypatch.setenv("ADFL_SLQ_ENCODE", "fastest")
     with pytest.raises(ValueError, match="ADFL_SLQ_ENCODE"):
         ops._encode_mode()

@@ -65,7 +65,7 @@ def c3_round_trip(lay, packed, args, world, rank, dev, lib, sh, junk, mode="auto
     """Device-resident encode + decode of one bucket (per-tensor scales), Infinity Cache warm and
     flushed. packed: the int4 nibble layout (PackedSLQChannel's kernels, 13 B/element). mode: the int8
     encode as ops.encode_batched picks it ("auto": resident when every tensor fits a block, else the
-    two passes) or forced ("coop", "twopass")."""
+    two passes) or forced ("twopass")."""
     from adfl_amd import _lib
     g = torch.Generator(device=dev).manual_seed(rank)
     x = torch.randn(lay.total, device=dev, generator=g) * 1e-3
@@ -77,19 +77,13 @@ def c3_round_trip(lay, packed, args, world, rank, dev, lib, sh, junk, mode="auto
     work = lay.device_work(dev)
     bits = 4 if packed else 8
     n = int(lay.sizes.sum())
-    coop = mode == "coop"
     nwork = 0 if mode == "twopass" else lay.nwork
-    sync = lay.device_sync(dev, sh)
 
     def enc():
         if packed:
             _lib.check(lib.adfl_slq_encode_batched_int4_work(x.data_ptr(), chunks.data_ptr(), lay.nchunks,
                                                              work.data_ptr(), lay.nwork, bits, q.data_ptr(),
                                                              scales.data_ptr(), partials.data_ptr(), sh))
-        elif coop:  # the opt-in cooperative one-launch encode (ADFL_SLQ_ENCODE=coop)
-            _lib.check(lib.adfl_slq_encode_batched_coop(x.data_ptr(), chunks.data_ptr(), lay.nchunks, bits,
-                                                        q.data_ptr(), scales.data_ptr(), partials.data_ptr(),
-                                                        sync.data_ptr(), sh))
         else:  # resident one-launch encode when every tensor fits a block (nwork > 0), else the two passes
             _lib.check(lib.adfl_slq_encode_batched_work(x.data_ptr(), chunks.data_ptr(), lay.nchunks, work.data_ptr(),
                                                         nwork, bits, q.data_ptr(), scales.data_ptr(),
@@ -100,8 +94,7 @@ def c3_round_trip(lay, packed, args, world, rank, dev, lib, sh, junk, mode="auto
     def dec():
         _lib.check(dec_fn(q.data_ptr(), chunks.data_ptr(), lay.nchunks, scales.data_ptr(), out.data_ptr(), sh))
 
-    res = {"encode": "coop" if coop else ("resident" if nwork else "twopass"),
-           "encode_launches": 1 if (coop or nwork) else 2}
+    res = {"encode": "resident" if nwork else "twopass", "encode_launches": 1 if nwork else 2}
     for flush in (False, True):
         def flush_cache():
             if flush:
@@ -156,12 +149,7 @@ def mode_c3(args, world, rank, dev):
             "value": res["flushed"]["GiB_per_s"], "chunks": lay.nchunks, **res,
             "loguniform_layout": {"chunks": lay_log.nchunks,
                                   **c3_round_trip(lay_log, False, args, world, rank, dev, lib, sh, junk)},
-            "int4_packed": c3_round_trip(lay, True, args, world, rank, dev, lib, sh, junk),
-            # A/B of the bucketed int8 encodes (--coop-ab): the opt-in cooperative one-launch encode on both
-            # layouts (a cooperative launch does not run under rocprofv3 here, so it is not in the default run)
-            **({"loguniform_coop": c3_round_trip(lay_log, False, args, world, rank, dev, lib, sh, junk, "coop"),
-                "equal_coop": c3_round_trip(lay, False, args, world, rank, dev, lib, sh, junk, "coop")}
-               if args.coop_ab else {})}
+            "int4_packed": c3_round_trip(lay, True, args, world, rank, dev, lib, sh, junk)}
 
 
 def mode_c5_int4(args, world, rank, dev):
@@ -622,7 +610,6 @@ def main():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--elems", type=int, default=0)
     p.add_argument("--packed", action="store_true")
-    p.add_argument("--coop-ab", action="store_true", help="c3: add the opt-in cooperative encode A/B")
     p.add_argument("--chunks", type=int, default=1)
     p.add_argument("--no-cpu", action="store_true", help="stoch: skip the host reference timing")
     args = p.parse_args()

@@ -6,11 +6,12 @@
 // in the profiler's teardown, not in the cooperative launch or in libadfl_slq.
 //
 //   hipcc --offload-arch=gfx950 -O2 -o tools/coop_repro tools/coop_repro.hip
-//   ./tools/coop_repro [reps]
+//   ./tools/coop_repro [reps] [plain]      (plain: the control, ordinary launches only)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #define CHECK(x)                                                                        \
@@ -33,6 +34,7 @@ __global__ void k_coop(int* out, unsigned* counter) {
 
 int main(int argc, char** argv) {
   const int reps = argc > 1 ? std::atoi(argv[1]) : 3;
+  const bool coop_launch = !(argc > 2 && std::strcmp(argv[2], "plain") == 0);
   int dev = 0, coop = 0, per_cu = 0;
   hipDeviceProp_t prop;
   CHECK(hipGetDevice(&dev));
@@ -55,7 +57,12 @@ int main(int argc, char** argv) {
     CHECK(hipGetLastError());
     CHECK(hipMemsetAsync(d_cnt, 0, sizeof(unsigned), s));
     void* args[] = {&d_out, &d_cnt};
-    CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_coop), dim3(grid), dim3(block), args, 0, s));
+    if (coop_launch) {
+      CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_coop), dim3(grid), dim3(block), args, 0, s));
+    } else {
+      hipLaunchKernelGGL(k_coop, dim3(grid), dim3(block), 0, s, d_out, d_cnt);
+      CHECK(hipGetLastError());
+    }
     CHECK(hipStreamSynchronize(s));
     unsigned cnt = 0;
     CHECK(hipMemcpy(&cnt, d_cnt, sizeof(cnt), hipMemcpyDeviceToHost));
@@ -74,7 +81,7 @@ int main(int argc, char** argv) {
   CHECK(hipStreamDestroy(s));
   CHECK(hipFree(d_out));
   CHECK(hipFree(d_cnt));
-  std::printf("ok: %d reps of plain + cooperative launches\n", reps);
+  std::printf("ok: %d reps of plain + %s launches\n", reps, coop_launch ? "cooperative" : "plain (control)");
   std::fflush(stdout);
   return 0;
 }
