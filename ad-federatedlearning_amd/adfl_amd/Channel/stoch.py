@@ -17,7 +17,7 @@ the GPU and encoded / decoded by a few HIP launches for all tensors together (in
 
 Randomness: the reference draws ``torch.rand_like`` from torch's CPU generator. Here each encode draws a
 fresh 62-bit seed from that same generator (so ``torch.manual_seed`` reproduces a run) and the kernels
-generate their uniforms from a Philox4x32-10 stream keyed by it. The uniforms are not the reference's
+generate their uniforms from a Philox4x32-7 stream keyed by it. The uniforms are not the reference's
 mt19937 draws, so individual rounding decisions differ from a reference run; their distribution is the
 same (and with injected uniforms the codec is bit-identical: tests/test_gpu_stoch.py).
 

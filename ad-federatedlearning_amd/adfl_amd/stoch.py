@@ -11,7 +11,7 @@ Every function takes and returns CUDA (HIP) tensors over a bucketed flat buffer 
   given norms (what the parity tests use to inject the reference's own norm)
 
 Randomness: pass ``uniforms`` (fp32 plane indexed like x, values in [0, 1)) to inject the reference's
-``torch.rand_like`` draws, or leave it None to draw from the Philox4x32-10 stream ``(seed, counter)``.
+``torch.rand_like`` draws, or leave it None to draw from the Philox4x32-7 stream ``(seed, counter)``.
 ``RngStream`` hands out (seed, counter) pairs seeded from torch's default CPU generator, so
 ``torch.manual_seed`` makes a run reproducible the way it does for the reference.
 """

@@ -14,8 +14,13 @@
 // once (exponents + norm partials in the same pass) and a per-chunk fix-up rewrites the (rare) all-zero
 // tensors the way the reference's norm == 0 branch returns them.
 //
-// Uniforms come from an in-register Philox4x32-10 stream (4 uniforms per 128-bit block, one block per
-// float4 group: no uniform ever touches HBM) or from an injected plane (parity tests).
+// Uniforms come from an in-register Philox4x32-7 stream (4 uniforms per 128-bit block, one block per
+// float4 group: no uniform ever touches HBM) or from an injected plane (parity tests). Seven rounds is
+// Random123's crush-resistant minimum for Philox4x32 (Salmon et al., SC'11: passes TestU01 BigCrush);
+// the ten of curand's default buy margin, not quality these codecs can observe (their draws are compared
+// with a threshold at 24-bit resolution), and each round is two quarter-rate 32x32->64 multiplies: 7 rounds
+// cut the stream's VALU issue by 30%. Round function, constants and key schedule are
+// Philox4x32's (pinned by the 10-round known-answer vectors in tests/test_stoch_golden.py).
 //
 // Numerics: no fast-math, -ffp-contract=off, IEEE fp32 denormals; divisions are correctly rounded
 // (__fdiv_rn) because the reference divides element by element in fp32; CNAT's floor/ceil(log2) is the
@@ -37,11 +42,16 @@ constexpr int64_t kPartialBytes = 16;  // per chunk: fp64 sum of squares, or {ma
 // ------------------------------------------------------------------------------------------------
 // uniforms
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint4 philox4x32_10(uint64_t ctr, uint64_t seed) {
+#ifndef ADFL_PHILOX_ROUNDS
+#define ADFL_PHILOX_ROUNDS 7
+#endif
+constexpr int kPhiloxRounds = ADFL_PHILOX_ROUNDS;
+
+__device__ __forceinline__ uint4 philox4x32(uint64_t ctr, uint64_t seed) {
   uint32_t c0 = (uint32_t)ctr, c1 = (uint32_t)(ctr >> 32), c2 = 0, c3 = 0;
   uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
 #pragma unroll
-  for (int r = 0; r < 10; ++r) {
+  for (int r = 0; r < kPhiloxRounds; ++r) {
     // full 32x32 -> 64 products: one v_mad_u64_u32 each instead of a v_mul_hi_u32 + v_mul_lo_u32 pair
     const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
     c0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
@@ -56,12 +66,12 @@ __device__ __forceinline__ uint4 philox4x32_10(uint64_t ctr, uint64_t seed) {
 
 __device__ __forceinline__ float u24(uint32_t w) { return (float)(w >> 8) * 0x1p-24f; }
 
-// B independent Philox4x32-10 blocks with their rounds interleaved: a single block is a chain of 10
-// dependent 64-bit multiply rounds, which with only 4-5 waves per SIMD leaves the VALU waiting on latency
+// B independent Philox4x32 blocks with their rounds interleaved: a single block is a chain of dependent
+// 64-bit multiply rounds, which with only 4-5 waves per SIMD leaves the VALU waiting on latency
 // (tools/microbench_stoch_res.hip: 9.3 us of C3's resident QSGD encode); B chains in lockstep give the
-// scheduler B independent instructions per step. Same words as philox4x32_10, bit for bit.
+// scheduler B independent instructions per step. Same words as philox4x32, bit for bit.
 template <int B>
-__device__ __forceinline__ void philox4x32_10_batch(const uint64_t (&ctr)[B], uint64_t seed, uint4 (&out)[B]) {
+__device__ __forceinline__ void philox4x32_batch(const uint64_t (&ctr)[B], uint64_t seed, uint4 (&out)[B]) {
   uint32_t c0[B], c1[B], c2[B], c3[B];
 #pragma unroll
   for (int i = 0; i < B; ++i) {
@@ -72,7 +82,7 @@ __device__ __forceinline__ void philox4x32_10_batch(const uint64_t (&ctr)[B], ui
   }
   uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
 #pragma unroll
-  for (int r = 0; r < 10; ++r) {
+  for (int r = 0; r < kPhiloxRounds; ++r) {
 #pragma unroll
     for (int i = 0; i < B; ++i) {
       const uint64_t p0 = (uint64_t)0xD2511F53u * c0[i], p1 = (uint64_t)0xCD9E8D57u * c2[i];
@@ -95,12 +105,12 @@ struct Uniforms {
   // u for elements g .. g+3, g % 4 == 0
   __device__ __forceinline__ float4 group(int64_t g) const {
     if (inj) return *reinterpret_cast<const float4*>(inj + g);
-    const uint4 w = philox4x32_10(counter + (uint64_t)(g >> 2), seed);
+    const uint4 w = philox4x32(counter + (uint64_t)(g >> 2), seed);
     return make_float4(u24(w.x), u24(w.y), u24(w.z), u24(w.w));
   }
   __device__ __forceinline__ float one(int64_t g) const {
     if (inj) return inj[g];
-    const uint4 w = philox4x32_10(counter + (uint64_t)(g >> 2), seed);
+    const uint4 w = philox4x32(counter + (uint64_t)(g >> 2), seed);
     const int k = (int)(g & 3);
     return u24(k == 0 ? w.x : k == 1 ? w.y : k == 2 ? w.z : w.w);
   }
@@ -593,7 +603,7 @@ __device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0ull; }
 // thread's index in its 256-thread group). Per group the level / exponent bytes (fast form; exact form for
 // the wave if any lane flagged its group) and the sign bytes, stored as one dword each (contiguous across
 // the wave). `all_exact` is uniform over the group.
-// Philox uniforms are generated PB groups at a time (philox4x32_10_batch); injected uniforms (a test path)
+// Philox uniforms are generated PB groups at a time (philox4x32_batch); injected uniforms (a test path)
 // are loaded group by group.
 // pre (LDS, or null): Philox words generated ahead of time, group j's at pre[j * pre_stride]. s4 null: the
 // caller stores the sign bytes itself.
@@ -614,7 +624,7 @@ __device__ __forceinline__ void quantize_regs(const float4 (&v)[kPer], int tg, i
       uint64_t ctr[PB];
 #pragma unroll
       for (int i = 0; i < PB; ++i) ctr[i] = U.counter + (uint64_t)((g0 >> 2) + tg + (jb + i) * kBlock);
-      philox4x32_10_batch(ctr, U.seed, w);
+      philox4x32_batch(ctr, U.seed, w);
     }
 #pragma unroll
     for (int i = 0; i < PB; ++i) {
@@ -661,7 +671,7 @@ __device__ __forceinline__ void quantize_chunk_vec(const float4* __restrict__ x4
   quantize_regs<PB>(v, threadIdx.x, n4, g0, U, l4, s4, fast, exact, all_exact, acc);
 }
 
-// PB: Philox blocks generated per batch (philox4x32_10_batch); the product's choice is kPbQuantize.
+// PB: Philox blocks generated per batch (philox4x32_batch); the product's choice is kPbQuantize.
 template <int PB>
 __global__ __launch_bounds__(kBlock) void k_qsgd_quantize(const float* __restrict__ x,
                                                           const adfl_slq_chunk* __restrict__ chunks, float s,
@@ -812,7 +822,7 @@ __global__ __launch_bounds__(kResBlock) void k_qsgd_encode_resident(
       uint4 w[PB];
 #pragma unroll
       for (int i = 0; i < PB; ++i) ctr[i] = U.counter + (uint64_t)(q0 + tg + (jb + i) * kBlock);
-      philox4x32_10_batch(ctr, U.seed, w);
+      philox4x32_batch(ctr, U.seed, w);
 #pragma unroll
       for (int i = 0; i < PB; ++i) pre[jb + i][threadIdx.x] = w[i];
     }

@@ -15,7 +15,7 @@
  * Both planes are indexed like x (byte g of a plane belongs to element g of the bucket).
  *
  * Uniforms. Stochastic rounding compares u in [0, 1) with a per-element probability. d_uniforms == NULL
- * draws u from the counter-based Philox4x32-10 stream keyed by `seed`: element g of the bucket uses word
+ * draws u from the counter-based Philox4x32-7 stream keyed by `seed`: element g of the bucket uses word
  * g % 4 of block (counter + g / 4), u = (word >> 8) * 2^-24. A caller that advances `counter` by
  * ceil(total / 4) per call never reuses a uniform. d_uniforms != NULL injects one fp32 uniform per
  * element (indexed like x) — with the reference's own uniforms the outputs are bit-identical to it.

@@ -37,7 +37,7 @@ the powers-of-two neighbourhoods. The HIP kernel uses the equivalent integer ban
 ad-federatedlearning_amd/csrc/cnat_log2_table.h (tools/gen_cnat_table.py --verify: 0 mismatches).
 
 Uniforms. The reference draws ``torch.rand_like`` from torch's CPU mt19937 stream. The HIP codec draws
-from a counter-based Philox4x32-10 stream instead (``philox_uniforms`` below restates it bit-exactly) or
+from a counter-based Philox4x32-7 stream instead (``philox_uniforms`` below restates it bit-exactly) or
 takes injected uniforms; with the same uniforms every output is bit-identical to the reference.
 """
 
@@ -203,27 +203,40 @@ def cnat_dequantize(e: np.ndarray, signs: np.ndarray, norm) -> np.ndarray:
 
 
 # ------------------------------------------------------------------------------------------------
-# Philox4x32-10 uniforms (the HIP codec's production stream)
+# Philox4x32-7 uniforms (the HIP codec's production stream, csrc/stoch_codec.hip kPhiloxRounds)
 # ------------------------------------------------------------------------------------------------
 PHILOX_M0, PHILOX_M1 = 0xD2511F53, 0xCD9E8D57
 PHILOX_W0, PHILOX_W1 = 0x9E3779B9, 0xBB67AE85
+PHILOX_ROUNDS = 7      # the codec's stream; 10 is Random123's / curand's default (known-answer vectors)
 MASK32 = 0xFFFFFFFF
 
 
-def philox4x32(ctr_lo: np.ndarray, ctr_hi: np.ndarray, seed: int, ctr2: int = 0, ctr3: int = 0):
-    """Philox4x32-10 (Salmon et al., SC'11) on counters (ctr_lo, ctr_hi, ctr2, ctr3), key = 64-bit seed
-    (the codec always uses ctr2 = ctr3 = 0). Returns the four uint32 output words (arrays)."""
-    c0 = np.asarray(ctr_lo, dtype=np.uint64) & MASK32
-    c1 = np.asarray(ctr_hi, dtype=np.uint64) & MASK32
-    c2 = np.full_like(c0, ctr2 & MASK32)
-    c3 = np.full_like(c0, ctr3 & MASK32)
-    k0, k1 = seed & MASK32, (seed >> 32) & MASK32
-    for _ in range(10):
-        p0 = c0 * np.uint64(PHILOX_M0)
-        p1 = c2 * np.uint64(PHILOX_M1)
-        hi0, lo0 = p0 >> np.uint64(32), p0 & np.uint64(MASK32)
-        hi1, lo1 = p1 >> np.uint64(32), p1 & np.uint64(MASK32)
-        c0, c1, c2, c3 = hi1 ^ c1 ^ np.uint64(k0), lo1, hi0 ^ c3 ^ np.uint64(k1), lo0
+def philox_round(c0, c1, c2, c3, k0: int, k1: int):
+    """One Philox4x32 round (S-box multiply + key xor) on uint64 arrays holding 32-bit words."""
+    p0 = c0 * np.uint64(PHILOX_M0)
+    p1 = c2 * np.uint64(PHILOX_M1)
+    hi0, lo0 = p0 >> np.uint64(32), p0 & np.uint64(MASK32)
+    hi1, lo1 = p1 >> np.uint64(32), p1 & np.uint64(MASK32)
+    return hi1 ^ c1 ^ np.uint64(k0), lo1, hi0 ^ c3 ^ np.uint64(k1), lo0
+
+
+def philox4x32(ctr_lo: np.ndarray, ctr_hi: np.ndarray, seed: int, ctr2: int = 0, ctr3: int = 0,
+               rounds: int = PHILOX_ROUNDS, first_round: int = 0, state=None):
+    """Philox4x32-R (Salmon et al., SC'11) on counters (ctr_lo, ctr_hi, ctr2, ctr3), key = 64-bit seed (the
+    codec always uses ctr2 = ctr3 = 0). Returns the four uint32 output words (arrays). `state` / `first_round`
+    continue a computation: rounds first_round .. rounds-1 applied to the words `state` (the key schedule
+    bumped first_round times), so philox4x32(..., 10) == 3 more rounds on philox4x32(..., 7)."""
+    if state is None:
+        c0 = np.asarray(ctr_lo, dtype=np.uint64) & MASK32
+        c1 = np.asarray(ctr_hi, dtype=np.uint64) & MASK32
+        c2 = np.full_like(c0, ctr2 & MASK32)
+        c3 = np.full_like(c0, ctr3 & MASK32)
+    else:
+        c0, c1, c2, c3 = (np.asarray(w, dtype=np.uint64) for w in state)
+    k0 = (seed + first_round * PHILOX_W0) & MASK32
+    k1 = ((seed >> 32) + first_round * PHILOX_W1) & MASK32
+    for _ in range(first_round, rounds):
+        c0, c1, c2, c3 = philox_round(c0, c1, c2, c3, k0, k1)
         k0 = (k0 + PHILOX_W0) & MASK32
         k1 = (k1 + PHILOX_W1) & MASK32
     return c0, c1, c2, c3

@@ -139,17 +139,54 @@ def test_cnat_band_table_matches_restatement():
     np.testing.assert_array_equal(c, np.ceil(lc))
 
 
+KAT10 = [((0, 0, 0, 0), (0, 0)), ((0xFFFFFFFF,) * 4, (0xFFFFFFFF, 0xFFFFFFFF)),
+         ((0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344), (0xA4093822, 0x299F31D0))]
+
+
 def test_philox_known_answer():
     """Philox4x32-10 known-answer vectors (Random123 kat_vectors, philox4x32 10 rounds): counter 0 / key 0,
-    counter all-ones / key all-ones, and the pi-digits counter / key."""
+    counter all-ones / key all-ones, and the pi-digits counter / key. They pin the round function, the
+    multipliers and the key schedule the codec's 7-round stream uses."""
     def words(c, k):
-        w = so.philox4x32(np.array([c[0]], np.uint64), np.array([c[1]], np.uint64), k[0] | (k[1] << 32), c[2], c[3])
+        w = so.philox4x32(np.array([c[0]], np.uint64), np.array([c[1]], np.uint64), k[0] | (k[1] << 32), c[2], c[3],
+                          rounds=10)
         return [int(a[0]) for a in w]
     assert words((0, 0, 0, 0), (0, 0)) == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
     ones = 0xFFFFFFFF
     assert words((ones,) * 4, (ones, ones)) == [0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD]
     assert words((0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344), (0xA4093822, 0x299F31D0)) == \
         [0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1]
+
+
+def test_philox_7_rounds_is_a_prefix_of_the_known_answer_computation():
+    """The codec's stream (PHILOX_ROUNDS = 7) is the first 7 rounds of the KAT-pinned Philox4x32-10: three
+    more rounds, key schedule continued, give the 10-round known answers."""
+    assert so.PHILOX_ROUNDS == 7
+    for c, k in KAT10:
+        key = k[0] | (k[1] << 32)
+        lo, hi = np.array([c[0]], np.uint64), np.array([c[1]], np.uint64)
+        w7 = so.philox4x32(lo, hi, key, c[2], c[3])
+        w10 = so.philox4x32(lo, hi, key, c[2], c[3], rounds=10)
+        cont = so.philox4x32(None, None, key, rounds=10, first_round=7, state=w7)
+        assert [int(a[0]) for a in cont] == [int(a[0]) for a in w10]
+        assert [int(a[0]) for a in w7] != [int(a[0]) for a in w10]
+
+
+def test_philox_7_round_stream_statistics():
+    """Uniformity and independence checks on 2^20 uniforms of the 7-round stream: bucket chi-square (256
+    buckets), lag-1 / lag-4 correlation, and every bit of the 24 used bits near 1/2."""
+    u = so.philox_uniforms(1 << 20, seed=2024, counter=0).astype(np.float64)
+    counts = np.bincount(np.minimum((u * 256).astype(np.int64), 255), minlength=256)
+    exp = u.size / 256
+    chi2 = float(((counts - exp) ** 2 / exp).sum())
+    assert chi2 < 350, chi2            # 255 dof: p(chi2 > 350) ~ 1e-4
+    for lag in (1, 4):
+        r = np.corrcoef(u[:-lag], u[lag:])[0, 1]
+        assert abs(r) < 0.005, (lag, r)   # ~5 sigma at n = 2^20
+    bits = (u * (1 << 24)).astype(np.int64)
+    for b in range(24):
+        f = float(((bits >> b) & 1).mean())
+        assert abs(f - 0.5) < 0.0025, (b, f)
 
 
 def test_philox_uniform_range_and_layout():

@@ -1,7 +1,7 @@
 // microbench_stoch_res.hip — the stochastic encodes on the C3 bucket (11,689,512 fp32 in 256 tensors, every
 // tensor resident) and the C2 tensor (2^28 fp32): the product encodes (one-launch resident and multi-launch;
 // QSGD, RQSGD, CNAT), their passes, the SLQ resident encode as the data-movement reference, and the quantize
-// kernels at Philox batch sizes PB = 1, 2, 4, 8 (philox4x32_10_batch). Not part of the product; it #includes
+// kernels at Philox batch sizes PB = 1, 2, 4, 8 (philox4x32_batch). Not part of the product; it #includes
 // the product source to reach its kernels.
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -Iinclude -o tools/microbench_stoch_res \
