@@ -694,6 +694,12 @@ __device__ __forceinline__ uint32_t block_max_seg(uint32_t v) {
 }
 
 // work[b] = the first chunk of tensor b (every tensor <= kSegChunks chunks).
+// ST_NT: non-temporal payload stores. The block's stores are the tail of a launch in which every CU loads,
+// reduces and stores in lockstep (tools/microbench_resident_timeline.hip: entry spread 0.6 us, block max
+// at 8.5 us, stores acknowledged at 11.5-12 us); streaming them past the L2 shortens the encode (15.7 vs
+// 16.6 us, profiles/r03/c3_resident/timeline.txt) but the decode that follows then reads the payload from
+// HBM: C3 round trip 30.3 vs 27.0 us (profiles/r03/c3_resident/c3_nt_stores.json). kResidentNtStores = false.
+template <bool ST_NT>
 __global__ __launch_bounds__(kSegBlock) void k_encode_resident(const float* __restrict__ x,
                                                                const adfl_slq_chunk* __restrict__ chunks,
                                                                const int32_t* __restrict__ work, float qmax,
@@ -738,11 +744,12 @@ __global__ __launch_bounds__(kSegBlock) void k_encode_resident(const float* __re
 #pragma unroll
   for (int k = 0; k < kSegTilesPerWave; ++k) {
     const int t = wave + k * kSegWaves;
-    if (t < ntiles) quantize_tile_regs(v[k], q16 + t * (kTile / 16), si.inv, lds[wave], lane);
+    if (t < ntiles) quantize_tile_regs<ST_NT>(v[k], q16 + t * (kTile / 16), si.inv, lds[wave], lane);
   }
   if ((int)threadIdx.x < head) qt[threadIdx.x] = (int8_t)quant1(hv, si.inv);
   if (ti < len) qt[ti] = (int8_t)quant1(tv, si.inv);
 }
+constexpr bool kResidentNtStores = false;
 
 // int4 variant (PackedSLQChannel's buckets: even tensor offsets, packed byte e/2 = flat elements e, e+1):
 // 2048-element int4 wave tiles, 2 per wave (16 float4 per lane); the < 32-element head and the < 2048-
@@ -1137,7 +1144,7 @@ int adfl_slq_encode_batched_work(const float* d_x, const adfl_slq_chunk* d_chunk
     return ADFL_E_ARG;
   if (int s = check_bits(bits)) return s;
   if (!aligned16(d_x) || !aligned16(d_q)) return ADFL_E_ALIGN;
-  hipLaunchKernelGGL(k_encode_resident, dim3((unsigned)nwork), dim3(kSegBlock), 0, (hipStream_t)stream, d_x,
+  hipLaunchKernelGGL(k_encode_resident<kResidentNtStores>, dim3((unsigned)nwork), dim3(kSegBlock), 0, (hipStream_t)stream, d_x,
                      d_chunks, d_work, qmax_f(bits), d_q, d_scales);
   return launch_status();
 }

@@ -730,12 +730,21 @@ __global__ __launch_bounds__(kBlock) void k_cnat_quantize(const float* __restric
 }
 
 // CNAT norm == 0 (an all-zero tensor): the reference returns u8 zeros and int8 ones (quant.py:513-514).
-__global__ __launch_bounds__(kBlock) void k_cnat_zero_fixup(const adfl_slq_chunk* __restrict__ chunks,
-                                                            const float* __restrict__ norms,
-                                                            int8_t* __restrict__ exps, int8_t* __restrict__ signs) {
+// One wave per chunk: nearly every launch only reads a norm and exits, and the launch is then bounded by
+// wave dispatch (a 256-thread block per chunk took 8.2 us at C2's 32,768 chunks, profiles/r02/rocprof_head/);
+// the rare all-zero tensor is rewritten 64 bytes per instruction.
+constexpr int kFixupBlock = 64;
+__global__ __launch_bounds__(kFixupBlock) void k_cnat_zero_fixup(const adfl_slq_chunk* __restrict__ chunks,
+                                                                 const float* __restrict__ norms,
+                                                                 int8_t* __restrict__ exps, int8_t* __restrict__ signs) {
   const adfl_slq_chunk c = chunks[blockIdx.x];
   if (norms[c.tensor] != 0.0f) return;
-  fill_zero_norm(reinterpret_cast<uint8_t*>(exps) + c.start, signs + c.start, c.len);
+  uint8_t* lv = reinterpret_cast<uint8_t*>(exps) + c.start;
+  int8_t* sg = signs + c.start;
+  for (int i = threadIdx.x; i < c.len; i += kFixupBlock) {
+    lv[i] = 0;
+    sg[i] = 1;
+  }
 }
 
 // ---- one-launch encodes of a bucket of small tensors (a whole tensor per 1024-thread block) -------------
@@ -1245,7 +1254,7 @@ int adfl_cnat_encode_batched(const float* d_x, const adfl_slq_chunk* d_chunks, i
                      d_exps, d_signs, (double*)d_workspace);
   if (int s = launch_status()) return s;
   if (int s = launch_finalize<ADFL_NORM_L2>(d_chunks, nchunks, d_workspace, d_norms, nullptr, st)) return s;
-  hipLaunchKernelGGL(k_cnat_zero_fixup, dim3((unsigned)nchunks), dim3(kBlock), 0, st, d_chunks,
+  hipLaunchKernelGGL(k_cnat_zero_fixup, dim3((unsigned)nchunks), dim3(kFixupBlock), 0, st, d_chunks,
                      (const float*)d_norms, d_exps, d_signs);
   return launch_status();
 }

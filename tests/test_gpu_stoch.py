@@ -403,3 +403,28 @@ def test_default_norm_deviation_is_bounded(c):
     rate = np.count_nonzero(diff) / x.size
     expect = levels * rel
     assert rate <= expect + 3 * np.sqrt(expect / x.size) + 1.0 / x.size, (rate, expect)
+
+
+@pytest.mark.parametrize("align", [1, 64])
+def test_cnat_multilaunch_zero_tensor_fixup(align):
+    """An all-zero tensor of several chunks beside non-zero ones, through the multi-launch CNAT encode (a
+    tensor above one block's 8 chunks forces it): the reference's norm == 0 branch (quant.py:513-514) gives
+    u8 zeros and int8 ones for exactly that tensor's bytes; the neighbours keep their exponents."""
+    sizes = [3 * 8192 + 77, 70001, 5]
+    lay = ops.BucketLayout(sizes, align=align)
+    assert lay.nwork == 0                                  # multi-launch: k_cnat_quantize + finalize + fixup
+    rng = np.random.default_rng(9)
+    flat = np.zeros(lay.total, np.float32)
+    flat[lay.offsets[1]:lay.offsets[1] + sizes[1]] = rng.standard_normal(sizes[1], dtype=np.float32)
+    flat[lay.offsets[2]:lay.offsets[2] + sizes[2]] = 1.5
+    u = rng.random(lay.total, dtype=np.float32)
+    e, s, nrm = stoch.cnat_encode_batched(d(flat), lay, 8, uniforms=d(u))
+    eh, sh, nh = h(e).view(np.uint8), h(s), h(nrm)
+    o0 = int(lay.offsets[0])
+    assert nh[0] == 0.0 and nh[1] > 0 and nh[2] > 0
+    assert (eh[o0:o0 + sizes[0]] == 0).all() and (sh[o0:o0 + sizes[0]] == 1).all()
+    for t in (1, 2):
+        o, n = int(lay.offsets[t]), sizes[t]
+        ce, cs = so.cnat_quantize(flat[o:o + n], 8, np.float32(nh[t]), u[o:o + n])
+        np.testing.assert_array_equal(eh[o:o + n], ce.view(np.uint8))
+        np.testing.assert_array_equal(sh[o:o + n], cs)

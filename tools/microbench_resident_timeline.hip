@@ -272,7 +272,7 @@ void run(const Layout& L, int reps) {
   const float qmax = 127.0f;
 
   auto product = [&]() {
-    hipLaunchKernelGGL(k_encode_resident, dim3((unsigned)nwork), dim3(kSegBlock), 0, 0, x, dch, dwork, qmax, q, sc);
+    hipLaunchKernelGGL(k_encode_resident<false>, dim3((unsigned)nwork), dim3(kSegBlock), 0, 0, x, dch, dwork, qmax, q, sc);
   };
   auto timeline = [&]() {
     hipLaunchKernelGGL(k_encode_resident_tl, dim3((unsigned)nwork), dim3(kSegBlock), 0, 0, x, dch, dwork, qmax, q2,
