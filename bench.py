@@ -64,6 +64,7 @@ def parse():
     p.add_argument("--cpu-child", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--cpu-input", help=argparse.SUPPRESS)
     p.add_argument("--cpu-list", help=argparse.SUPPRESS)
+    p.add_argument("--share-gpu", action="store_true", help=argparse.SUPPRESS)   # N ranks on cuda:0 over gloo (tests)
     p.add_argument("--plumbing-check", action="store_true",
                    help="CPU-only check of the rank launcher / barrier / max-over-ranks (gloo); no GPU, no bench")
     return p.parse_args()
@@ -144,13 +145,16 @@ def maybe_launch(n_gpus: int, script: str, argv) -> "int | None":
     return launch_ranks(n_gpus, script, argv)
 
 
-def dist_setup(args, backend: str = "nccl"):
+def dist_setup(args, backend: str = "nccl", share_gpu: bool = False):
     """One process per GPU (torchrun env: RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*). `backend` is
-    "nccl" (= RCCL) for the bench; tests drive the same code with "gloo" on CPU."""
+    "nccl" (= RCCL) for the bench; tests drive the same code with "gloo" on CPU. share_gpu (the hidden
+    --share-gpu): every rank on cuda:0 over gloo — the reference's two-clients-per-GPU packing
+    (Examples/ray_ad.py:29), which RCCL cannot form — so the N-rank path runs on a one-GPU box.
+    Returns (world, rank, device index)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if backend == "nccl":
+    local = 0 if share_gpu else int(os.environ.get("LOCAL_RANK", "0"))
+    if backend == "nccl" or share_gpu:
         torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
@@ -570,7 +574,7 @@ def main():
         return pmc_child(args)
     if args.cpu_child:
         return cpu_child(args)
-    world, rank, local = dist_setup(args)
+    world, rank, local = dist_setup(args, "gloo" if args.share_gpu else "nccl", args.share_gpu)
     assert world == args.gpus, (world, args.gpus)
     from adfl_amd import ops
     from adfl_amd import _lib

@@ -53,3 +53,22 @@ def test_bench_exchange_leg_checks_itself():
     assert "error" not in ex, ex
     assert ex["parity"] is True, ex
     assert ex["check"]["own_row_equal"] and ex["check"]["rows_checked"] == 1 and ex["backend"] == "nccl"
+
+
+def test_bench_two_ranks_share_one_gpu():
+    """bench.py --gpus 2 end to end on a one-GPU box (hidden --share-gpu: both ranks on cuda:0, gloo): the
+    launcher, both ranks' timed round trips, the max over ranks, rank 0's single line with n_gpus 2 and
+    value = 2 GiB per step, and the exchange leg (host-staged all-gather) verifying itself across ranks."""
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+                        "--no-cpu-baseline", "--pmc", "off", "--share-gpu"],
+                       cwd=REPO, capture_output=True, text=True, timeout=115)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "independent clients x2"
+    assert abs(d["value"] - 2.0 / (d["ms_per_step"] * 1e-3)) / d["value"] < 0.01
+    ex = d["exchange"]
+    assert "error" not in ex, ex
+    assert ex["parity"] is True and ex["backend"] == "gloo", ex
+    assert ex["check"]["rows_checked"] == 2 and ex["check"]["mean_identical_on_all_ranks"]
