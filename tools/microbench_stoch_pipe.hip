@@ -1,0 +1,214 @@
+// microbench_stoch_pipe.hip — software-pipelined (persistent, double-buffered) forms of the C2 stochastic
+// kernels against the product's one-block-per-chunk kernels. In the product's k_cnat_quantize every block
+// loads its chunk, then computes, then stores: a wave has loads in flight only before it computes, so at
+// C2 the VALU work (~45 issue slots per element) and the 6 B/element memory stream overlap only across
+// waves. Here a grid of G resident blocks walks chunks b, b+G, b+2G, ...: chunk i+1's loads are issued
+// into the second register buffer before chunk i is quantized, so every wave keeps 8 KiB of loads in
+// flight while it computes. Per-chunk arithmetic, partials and outputs are the product's: bit-identical
+// (checked). Not part of the product; it #includes the product source.
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -Iinclude -o tools/microbench_stoch_pipe \
+//         tools/microbench_stoch_pipe.hip ad-federatedlearning_amd/csrc/slq_codec.hip
+#include "../ad-federatedlearning_amd/csrc/stoch_codec.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <vector>
+
+#define CK(x)                                                                                \
+  do {                                                                                       \
+    hipError_t e_ = (hipError_t)(x);                                                         \
+    if (e_ != hipSuccess) {                                                                  \
+      fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+      exit(1);                                                                               \
+    }                                                                                        \
+  } while (0)
+
+namespace {
+__global__ void k_flush(const uint4* __restrict__ junk, int64_t n16, uint32_t* __restrict__ sink) {
+  uint32_t a = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x)
+    a ^= junk[i].x;
+  if (a == 0x12345678u) *sink = a;
+}
+
+__global__ void k_fill(float* p, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t h = (uint32_t)i * 2654435761u;
+    h ^= h >> 15;
+    h *= 2246822519u;
+    h ^= h >> 13;
+    p[i] = ((float)(h & 0xffffff) / 16777216.0f - 0.5f) * 4e-3f;
+  }
+}
+
+struct ChunkView {
+  int64_t start;
+  int len, head, n4;
+};
+
+__device__ __forceinline__ ChunkView chunk_view(const adfl_slq_chunk* __restrict__ chunks, int64_t ci) {
+  const adfl_slq_chunk c = chunks[ci];
+  ChunkView v;
+  v.start = c.start;
+  v.len = c.len;
+  v.head = chunk_head4(c.start, c.len);
+  v.n4 = (c.len - v.head) >> 2;
+  return v;
+}
+
+// k_cnat_quantize's per-chunk body on registers already loaded
+template <int PB>
+__device__ __forceinline__ void cnat_chunk(const float* __restrict__ x, const ChunkView& c, const float4 (&v)[kPer],
+                                           int min_e, int max_e, const Uniforms& U, int8_t* __restrict__ exps,
+                                           int8_t* __restrict__ signs, double* __restrict__ partials, int64_t ci) {
+  const float* xc = x + c.start;
+  int8_t* ex = exps + c.start;
+  int8_t* sg = signs + c.start;
+  const auto fast = [=](float xv, float uv, bool& bad) { return cnat_exp_fast(xv, uv, min_e, max_e, bad); };
+  const auto exact = [=](float xv, float uv) { return cnat_exp_exact(xv, uv, min_e, max_e); };
+  NormAcc<ADFL_NORM_L2> acc;
+  quantize_regs<PB>(v, threadIdx.x, c.n4, c.start + c.head, U, reinterpret_cast<uint32_t*>(ex + c.head),
+                    reinterpret_cast<uint32_t*>(sg + c.head), fast, exact, false, &acc);
+  const int i = edge_elem(c.head, c.head + (c.n4 << 2), c.len);
+  if (i >= 0) {
+    const float e = xc[i];
+    ex[i] = (int8_t)exact(e, U.one(c.start + i));
+    sg[i] = (int8_t)sign_byte(e);
+    acc.add(e);
+  }
+  acc.flush(partials, ci);
+}
+
+template <int PB, int WPE>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void k_cnat_quantize_pipe(
+    const float* __restrict__ x, const adfl_slq_chunk* __restrict__ chunks, int64_t nchunks, int min_e, int max_e,
+    Uniforms U, int8_t* __restrict__ exps, int8_t* __restrict__ signs, double* __restrict__ partials) {
+  const int64_t G = gridDim.x;
+  int64_t ci = blockIdx.x;
+  if (ci >= nchunks) return;
+  float4 v[kPer], vn[kPer];
+  ChunkView c = chunk_view(chunks, ci);
+  load_chunk_regs(reinterpret_cast<const float4*>(x + c.start + c.head), c.n4, threadIdx.x, v);
+  for (;;) {
+    const int64_t cn = ci + G;
+    const bool more = cn < nchunks;  // block-uniform
+    ChunkView n = c;
+    if (more) {
+      n = chunk_view(chunks, cn);
+      load_chunk_regs(reinterpret_cast<const float4*>(x + n.start + n.head), n.n4, threadIdx.x, vn);
+    }
+    cnat_chunk<PB>(x, c, v, min_e, max_e, U, exps, signs, partials, ci);
+    if (!more) break;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) v[j] = vn[j];
+    c = n;
+    ci = cn;
+  }
+}
+
+double median(std::vector<double> v) {
+  std::sort(v.begin(), v.end());
+  return v[v.size() / 2];
+}
+
+void run(int reps) {
+  const int64_t n = 1ll << 28;
+  int64_t off = 0;
+  const int64_t nch = adfl_slq_build_chunks(&off, &n, 1, nullptr, 0);
+  std::vector<adfl_slq_chunk> ch(nch);
+  adfl_slq_build_chunks(&off, &n, 1, ch.data(), nch);
+  float* x;
+  int8_t *e1, *s1, *e2, *s2;
+  double *p1, *p2;
+  adfl_slq_chunk* dch;
+  uint4* junk;
+  uint32_t* sink;
+  const int64_t junk_bytes = 512ll << 20;
+  CK(hipMalloc(&x, n * 4));
+  CK(hipMalloc(&e1, n));
+  CK(hipMalloc(&s1, n));
+  CK(hipMalloc(&e2, n));
+  CK(hipMalloc(&s2, n));
+  CK(hipMalloc(&p1, nch * 8));
+  CK(hipMalloc(&p2, nch * 8));
+  CK(hipMalloc(&dch, nch * sizeof(adfl_slq_chunk)));
+  CK(hipMalloc(&junk, junk_bytes));
+  CK(hipMalloc(&sink, 4));
+  CK(hipMemset(junk, 0, junk_bytes));
+  CK(hipMemcpy(dch, ch.data(), nch * sizeof(adfl_slq_chunk), hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, x, n);
+  const Uniforms U{nullptr, 1234, 0};
+  const int min_e = -128, max_e = 127;
+  auto product = [&]() {
+    hipLaunchKernelGGL(k_cnat_quantize<kPbQuantize>, dim3((unsigned)nch), dim3(kBlock), 0, 0, x, dch, min_e, max_e, U,
+                       e1, s1, p1);
+  };
+  std::vector<std::pair<std::string, std::function<void()>>> vars;
+  for (int g : {768, 1024, 2048}) {
+    vars.push_back({"pipe PB2 w3 grid " + std::to_string(g), [&, g]() {
+                      hipLaunchKernelGGL((k_cnat_quantize_pipe<2, 3>), dim3((unsigned)g), dim3(kBlock), 0, 0, x, dch,
+                                         nch, min_e, max_e, U, e2, s2, p2);
+                    }});
+    vars.push_back({"pipe PB2 w4 grid " + std::to_string(g), [&, g]() {
+                      hipLaunchKernelGGL((k_cnat_quantize_pipe<2, 4>), dim3((unsigned)g), dim3(kBlock), 0, 0, x, dch,
+                                         nch, min_e, max_e, U, e2, s2, p2);
+                    }});
+    vars.push_back({"pipe PB4 w4 grid " + std::to_string(g), [&, g]() {
+                      hipLaunchKernelGGL((k_cnat_quantize_pipe<4, 4>), dim3((unsigned)g), dim3(kBlock), 0, 0, x, dch,
+                                         nch, min_e, max_e, U, e2, s2, p2);
+                    }});
+  }
+  product();
+  CK(hipDeviceSynchronize());
+  std::vector<int8_t> ha(n), hb(n);
+  std::vector<double> pa(nch), pb(nch);
+  CK(hipMemcpy(ha.data(), e1, n, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(pa.data(), p1, nch * 8, hipMemcpyDeviceToHost));
+  std::vector<int8_t> sa(n), sb(n);
+  CK(hipMemcpy(sa.data(), s1, n, hipMemcpyDeviceToHost));
+  for (auto& v : vars) {
+    CK(hipMemset(e2, 0x55, n));
+    CK(hipMemset(s2, 0x55, n));
+    CK(hipMemset(p2, 0, nch * 8));
+    v.second();
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(hb.data(), e2, n, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(sb.data(), s2, n, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(pb.data(), p2, nch * 8, hipMemcpyDeviceToHost));
+    const bool ok = ha == hb && sa == sb && std::memcmp(pa.data(), pb.data(), nch * 8) == 0;
+    printf("  %-22s output == product: %s\n", v.first.c_str(), ok ? "yes" : "NO");
+  }
+  hipEvent_t a0, a1;
+  CK(hipEventCreate(&a0));
+  CK(hipEventCreate(&a1));
+  std::vector<std::vector<double>> t(vars.size() + 1);
+  for (int rep = 0; rep < reps; ++rep)
+    for (size_t k = 0; k <= vars.size(); ++k) {
+      hipLaunchKernelGGL(k_flush, dim3(4096), dim3(256), 0, 0, junk, junk_bytes / 16, sink);
+      CK(hipEventRecord(a0, 0));
+      if (k == 0)
+        product();
+      else
+        vars[k - 1].second();
+      CK(hipEventRecord(a1, 0));
+      CK(hipEventSynchronize(a1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, a0, a1));
+      if (rep >= 3) t[k].push_back(ms * 1e3);
+    }
+  for (size_t k = 0; k <= vars.size(); ++k) {
+    const double m = median(t[k]);
+    printf("  %-28s C2 CNAT quantize %8.1f us  (6 B/elem: %.3f of 8 TB/s)\n",
+           k == 0 ? "product k_cnat_quantize<4>" : vars[k - 1].first.c_str(), m, 6.0 * n / (m * 1e-6) / 8e12);
+  }
+}
+}  // namespace
+
+int main(int argc, char** argv) {
+  run(argc > 1 ? atoi(argv[1]) : 15);
+  return 0;
+}
