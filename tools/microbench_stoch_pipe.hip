@@ -110,6 +110,38 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
   }
 }
 
+// Two-body form: the loop body holds chunk i (buffer a) and chunk i+1 (buffer b) as separate code, so the
+// register buffers never move and every inner loop unrolls (the single-body form above does not unroll).
+template <int PB, int WPE>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void k_cnat_quantize_pipe2(
+    const float* __restrict__ x, const adfl_slq_chunk* __restrict__ chunks, int64_t nchunks, int min_e, int max_e,
+    Uniforms U, int8_t* __restrict__ exps, int8_t* __restrict__ signs, double* __restrict__ partials) {
+  const int64_t G = gridDim.x;
+  int64_t ci = blockIdx.x;
+  if (ci >= nchunks) return;
+  float4 va[kPer], vb[kPer];
+  ChunkView ca = chunk_view(chunks, ci), cb;
+  load_chunk_regs(reinterpret_cast<const float4*>(x + ca.start + ca.head), ca.n4, threadIdx.x, va);
+  while (true) {
+    const int64_t nb = ci + G;
+    if (nb < nchunks) {
+      cb = chunk_view(chunks, nb);
+      load_chunk_regs(reinterpret_cast<const float4*>(x + cb.start + cb.head), cb.n4, threadIdx.x, vb);
+    }
+    cnat_chunk<PB>(x, ca, va, min_e, max_e, U, exps, signs, partials, ci);
+    if (nb >= nchunks) break;
+    ci = nb;
+    const int64_t na = ci + G;
+    if (na < nchunks) {
+      ca = chunk_view(chunks, na);
+      load_chunk_regs(reinterpret_cast<const float4*>(x + ca.start + ca.head), ca.n4, threadIdx.x, va);
+    }
+    cnat_chunk<PB>(x, cb, vb, min_e, max_e, U, exps, signs, partials, ci);
+    if (na >= nchunks) break;
+    ci = na;
+  }
+}
+
 double median(std::vector<double> v) {
   std::sort(v.begin(), v.end());
   return v[v.size() / 2];
@@ -148,17 +180,17 @@ void run(int reps) {
                        e1, s1, p1);
   };
   std::vector<std::pair<std::string, std::function<void()>>> vars;
-  for (int g : {768, 1024, 2048}) {
-    vars.push_back({"pipe PB2 w3 grid " + std::to_string(g), [&, g]() {
-                      hipLaunchKernelGGL((k_cnat_quantize_pipe<2, 3>), dim3((unsigned)g), dim3(kBlock), 0, 0, x, dch,
-                                         nch, min_e, max_e, U, e2, s2, p2);
-                    }});
-    vars.push_back({"pipe PB2 w4 grid " + std::to_string(g), [&, g]() {
+  for (int g : {1024, 1536, 2048}) {
+    vars.push_back({"pipe1 PB2 w4 grid " + std::to_string(g), [&, g]() {
                       hipLaunchKernelGGL((k_cnat_quantize_pipe<2, 4>), dim3((unsigned)g), dim3(kBlock), 0, 0, x, dch,
                                          nch, min_e, max_e, U, e2, s2, p2);
                     }});
-    vars.push_back({"pipe PB4 w4 grid " + std::to_string(g), [&, g]() {
-                      hipLaunchKernelGGL((k_cnat_quantize_pipe<4, 4>), dim3((unsigned)g), dim3(kBlock), 0, 0, x, dch,
+    vars.push_back({"pipe2 PB2 w2 grid " + std::to_string(g), [&, g]() {
+                      hipLaunchKernelGGL((k_cnat_quantize_pipe2<2, 2>), dim3((unsigned)g), dim3(kBlock), 0, 0, x, dch,
+                                         nch, min_e, max_e, U, e2, s2, p2);
+                    }});
+    vars.push_back({"pipe2 PB2 w3 grid " + std::to_string(g), [&, g]() {
+                      hipLaunchKernelGGL((k_cnat_quantize_pipe2<2, 3>), dim3((unsigned)g), dim3(kBlock), 0, 0, x, dch,
                                          nch, min_e, max_e, U, e2, s2, p2);
                     }});
   }
