@@ -730,20 +730,27 @@ __global__ __launch_bounds__(kBlock) void k_cnat_quantize(const float* __restric
 }
 
 // CNAT norm == 0 (an all-zero tensor): the reference returns u8 zeros and int8 ones (quant.py:513-514).
-// One wave per chunk: nearly every launch only reads a norm and exits, and the launch is then bounded by
-// wave dispatch (a 256-thread block per chunk took 8.2 us at C2's 32,768 chunks, profiles/r02/rocprof_head/);
-// the rare all-zero tensor is rewritten 64 bytes per instruction.
-constexpr int kFixupBlock = 64;
-__global__ __launch_bounds__(kFixupBlock) void k_cnat_zero_fixup(const adfl_slq_chunk* __restrict__ chunks,
-                                                                 const float* __restrict__ norms,
-                                                                 int8_t* __restrict__ exps, int8_t* __restrict__ signs) {
-  const adfl_slq_chunk c = chunks[blockIdx.x];
-  if (norms[c.tensor] != 0.0f) return;
-  uint8_t* lv = reinterpret_cast<uint8_t*>(exps) + c.start;
-  int8_t* sg = signs + c.start;
-  for (int i = threadIdx.x; i < c.len; i += kFixupBlock) {
-    lv[i] = 0;
-    sg[i] = 1;
+// One THREAD per chunk checks its tensor's norm; a wave then fills its zero-norm chunks one at a time, all
+// 64 lanes on each. Nearly every launch only reads a norm per chunk and exits: one block per chunk made it
+// a launch of 32,768 tiny dependent read chains at C2 (7.8-8.2 us at 256 or 64 threads per block,
+// profiles/r03/rocprof_head/stoch_kernel_stats.csv); here it is 128 blocks.
+__global__ __launch_bounds__(kBlock) void k_cnat_zero_fixup(const adfl_slq_chunk* __restrict__ chunks,
+                                                            int64_t nchunks, const float* __restrict__ norms,
+                                                            int8_t* __restrict__ exps, int8_t* __restrict__ signs) {
+  const int64_t wave0 = (int64_t)blockIdx.x * kBlock + (threadIdx.x & ~63);
+  const int64_t ci = wave0 + (threadIdx.x & 63);
+  const bool zero = ci < nchunks && norms[chunks[ci].tensor] == 0.0f;
+  uint64_t m = __ballot(zero);
+  while (m) {  // wave-uniform: the wave's zero-norm chunks, lowest lane first
+    const int l = __builtin_ctzll(m);
+    m &= m - 1;
+    const adfl_slq_chunk c = chunks[wave0 + l];
+    uint8_t* lv = reinterpret_cast<uint8_t*>(exps) + c.start;
+    int8_t* sg = signs + c.start;
+    for (int i = threadIdx.x & 63; i < c.len; i += 64) {
+      lv[i] = 0;
+      sg[i] = 1;
+    }
   }
 }
 
@@ -1254,8 +1261,8 @@ int adfl_cnat_encode_batched(const float* d_x, const adfl_slq_chunk* d_chunks, i
                      d_exps, d_signs, (double*)d_workspace);
   if (int s = launch_status()) return s;
   if (int s = launch_finalize<ADFL_NORM_L2>(d_chunks, nchunks, d_workspace, d_norms, nullptr, st)) return s;
-  hipLaunchKernelGGL(k_cnat_zero_fixup, dim3((unsigned)nchunks), dim3(kFixupBlock), 0, st, d_chunks,
-                     (const float*)d_norms, d_exps, d_signs);
+  hipLaunchKernelGGL(k_cnat_zero_fixup, dim3((unsigned)((nchunks + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
+                     d_chunks, nchunks, (const float*)d_norms, d_exps, d_signs);
   return launch_status();
 }
 
