@@ -9,7 +9,9 @@ fp32 tensors pickled through Ray's object store. Here each rank is one client on
                                       ->  fused decode + mean of the K payloads (one HIP launch)
 
 Message layout (one row per chunk per rank, 16-byte aligned): ``payload | pad to 16 | fp32 scale | pad``.
-The scale rides in the row, so one all-gather moves payloads and scales together.
+The scale rides in the row, so one all-gather moves payloads and scales together. With a bucket layout (a
+whole state dict, SLQChannel's per-tensor scales) the row is ``bucket payload | pad | T fp32 scales | pad``
+and the mean is taken per tensor with each row's scale for that tensor.
 
 The mean (``exact_self=True``, the default) is the reference's: the peers' decoded updates in rank order,
 then the rank's OWN update exactly as it is (fp32, not quantized: async_peer.py:170-174 and
@@ -57,6 +59,7 @@ class HipCodec:
         self.device = device
         self.lib = _lib.load()
         self.ws = torch.empty(_lib.workspace_bytes(), dtype=torch.uint8, device=device)
+        self._partials = None
 
     def _stream(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream
@@ -68,6 +71,26 @@ class HipCodec:
         scale_ptr = row.data_ptr() + _pad16(payload_bytes)
         fn = self.lib.adfl_slq_quantize_int4 if packed else self.lib.adfl_slq_quantize
         check(fn(x.data_ptr(), x.numel(), bits, self.ws.data_ptr(), row.data_ptr(), scale_ptr, self._stream()))
+
+    def encode_bucket(self, x: torch.Tensor, layout, bits: int, row: torch.Tensor) -> None:
+        """A whole bucketed state dict into one message row: per-tensor SLQ payload (the layout's offsets) |
+        pad | one fp32 scale per tensor (ops.encode_batched: one launch when every tensor fits a block)."""
+        from . import ops
+        total = layout.total
+        soff = _pad16(total)
+        if self._partials is None or self._partials.numel() < layout.nchunks:
+            self._partials = torch.empty(layout.nchunks, dtype=torch.int32, device=self.device)
+        ops.encode_batched(x, layout, bits, q=row[:total].view(torch.int8),
+                           scales=row[soff:soff + 4 * layout.ntensors].view(torch.float32), partials=self._partials)
+
+    def mean_bucket(self, rows: torch.Tensor, layout, out: torch.Tensor, self_row: int = -1,
+                    self_x: Optional[torch.Tensor] = None) -> None:
+        k, row_bytes = rows.shape
+        xp = self_x.data_ptr() if self_row >= 0 else None
+        check(self.lib.adfl_slq_dequantize_mean_batched(rows.data_ptr(), row_bytes, k,
+                                                        layout.device_chunks(self.device).data_ptr(), layout.nchunks,
+                                                        rows.data_ptr() + _pad16(layout.total), row_bytes // 4,
+                                                        self_row, xp, out.data_ptr(), self._stream()))
 
     def mean(self, rows: torch.Tensor, n: int, packed: bool, payload_bytes: int, out: torch.Tensor,
              self_row: int = -1, self_x: Optional[torch.Tensor] = None) -> None:
@@ -98,13 +121,20 @@ class PeerExchange:
     numel   elements of each rank's update (same on every rank)
     bits    SLQ bit width (8: int8 payload; with packed=True the int4 nibble layout, compression.py:35-66)
     chunks  >1 splits quantize + all-gather into a pipeline (C5)
+    layout  an ops.BucketLayout: the update is a bucketed state dict (numel = layout.total) encoded as
+            SLQChannel encodes a state dict, one scale per tensor (quant.py:74-94), and averaged per tensor
+            (ray_ad.py:164-190 averages every tensor). int8, one chunk. Without it the whole update has one
+            scale (BASELINE's C4 / C5: one flat gradient per client).
     """
 
     def __init__(self, numel: int, bits: int = 8, packed: bool = False, chunks: int = 1,
                  group: Optional[dist.ProcessGroup] = None, device: Optional[torch.device] = None, codec=None,
-                 exact_self: bool = True):
+                 exact_self: bool = True, layout=None):
         if numel < 1 or chunks < 1:
             raise ValueError("PeerExchange: numel and chunks must be >= 1")
+        if layout is not None and (packed or chunks != 1 or numel != layout.total):
+            raise ValueError("PeerExchange: a bucket layout takes int8 payloads in one chunk, numel = layout.total")
+        self.layout = layout
         self.numel, self.bits, self.packed, self.group = numel, bits, packed, group
         self.exact_self = exact_self
         self._x: Optional[torch.Tensor] = None
@@ -119,7 +149,8 @@ class PeerExchange:
         step = (step + 31) // 32 * 32
         self.bounds = [(c0, min(numel, c0 + step)) for c0 in range(0, numel, step)]
         self.payload = [self._payload_bytes(c1 - c0) for c0, c1 in self.bounds]
-        self.row_bytes = [_pad16(p) + 16 for p in self.payload]
+        trailer = 16 if layout is None else _pad16(4 * layout.ntensors)   # the scale(s) after the payload
+        self.row_bytes = [_pad16(p) + trailer for p in self.payload]
         self.local = [torch.empty(rb, dtype=torch.uint8, device=device) for rb in self.row_bytes]
         self.gathered = [torch.empty(self.world, rb, dtype=torch.uint8, device=device) for rb in self.row_bytes]
         # device rows over a host-only backend (gloo): stage each row through pinned host memory. A group
@@ -152,11 +183,12 @@ class PeerExchange:
             raise ValueError(f"PeerExchange: expected {self.numel} fp32 elements, got {x.numel()} {x.dtype}")
         x = x.reshape(-1)
         self._x = x
-        self.codec.absmax(x)
+        if self.layout is None:
+            self.codec.absmax(x)
         if self.device.type != "cuda":   # host tensors (the protocol tests' codec): one sequence, no streams
             works = []
             for c in range(len(self.bounds)):
-                self.codec.quantize(self._chunk(x, c), self.bits, self.packed, self.local[c], self.payload[c])
+                self._encode(x, c)
                 works.append(self._gather(c))
             return works
         main, qs, gs = torch.cuda.current_stream(self.device), self.quant_stream, self.gather_stream
@@ -165,7 +197,7 @@ class PeerExchange:
         done = []
         with torch.cuda.stream(qs):
             for c in range(len(self.bounds)):
-                self.codec.quantize(self._chunk(x, c), self.bits, self.packed, self.local[c], self.payload[c])
+                self._encode(x, c)
                 done.append(qs.record_event())
         works = []
         with torch.cuda.stream(gs):      # RCCL (or the staging copy) syncs with this stream: chunk c only
@@ -178,6 +210,12 @@ class PeerExchange:
     def _chunk(self, x: torch.Tensor, c: int) -> torch.Tensor:
         c0, c1 = self.bounds[c]
         return x[c0:c1]
+
+    def _encode(self, x: torch.Tensor, c: int) -> None:
+        if self.layout is not None:
+            self.codec.encode_bucket(x, self.layout, self.bits, self.local[c])
+        else:
+            self.codec.quantize(self._chunk(x, c), self.bits, self.packed, self.local[c], self.payload[c])
 
     def _gather(self, c: int):
         """Issue chunk c's all-gather (async) from the current stream's position."""
@@ -192,13 +230,18 @@ class PeerExchange:
     def mean(self, works: List, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Wait for each chunk's all-gather and decode the K payloads into their fp32 mean (a `None` work
         is a chunk whose collective the caller has already waited on)."""
-        out = torch.empty(self.numel, dtype=torch.float32, device=self.device) if out is None else out
+        if out is None:   # a bucket's gaps (alignment padding) are zero
+            out = (torch.empty if self.layout is None else torch.zeros)(self.numel, dtype=torch.float32,
+                                                                         device=self.device)
         self_row = self.rank if self.exact_self else -1
         if self_row >= 0 and self._x is None:
             raise RuntimeError("PeerExchange.mean: no pending encode_and_gather (exact_self needs its update)")
         for (c0, c1), rows, pb, w in zip(self.bounds, self.gathered, self.payload, works):
             if w is not None:
                 w.wait()
+            if self.layout is not None:
+                self.codec.mean_bucket(rows, self.layout, out, self_row, self._x if self_row >= 0 else None)
+                continue
             self.codec.mean(rows, c1 - c0, self.packed, pb, out[c0:c1], self_row,
                             self._x[c0:c1] if self_row >= 0 else None)
         self._x = None   # the caller's update is not kept alive past the exchange (1-4 GiB at C4/C5)

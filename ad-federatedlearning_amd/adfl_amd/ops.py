@@ -8,7 +8,8 @@ synchronises. Semantics are the reference's, bit for bit:
 * ``encode_batched`` / ``decode_batched`` — the per-tensor loop of ``_quantize_params`` / ``_receive``
   (quant.py:67-94) as one launch per pass over a whole bucketed state dict
 * ``encode_int4`` / ``decode_int4`` / ``pack_int4`` / ``unpack_int4`` — Src/ADFL/compression.py:35-66
-* ``dequantize_mean`` — the peer mean after the exchange (Examples/ray_ad.py:188)
+* ``dequantize_mean`` — the peer mean after the exchange (Examples/ray_ad.py:188); ``dequantize_mean_batched``
+  the same over bucketed payloads with per-tensor scales
 
 The same ops are registered as PyTorch custom ops ``torch.ops.adfl.*`` (with fake implementations, so
 they trace under torch.compile) at the bottom of this file: slq_absmax, slq_encode / slq_decode,
@@ -342,6 +343,37 @@ def dequantize_add_batched(q: torch.Tensor, scales: torch.Tensor, layout: Bucket
                                                       table.data_ptr(), layout.ntensors, len(targets),
                                                       _stream(dev)))
     # `table` may be freed on return: the caching allocator only reuses it for later work on this stream
+
+
+def dequantize_mean_batched(q_rows: torch.Tensor, scales: torch.Tensor, layout: BucketLayout, *,
+                            out: Optional[torch.Tensor] = None, self_row: int = -1,
+                            self_x: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Peer mean of K bucketed int8 payloads with per-tensor scales (SLQChannel's per-tensor codec over a
+    whole state dict, averaged as Examples/ray_ad.py:164-190 averages every tensor). q_rows: [K, row_bytes]
+    int8 (row_bytes >= layout.total, a 16-byte multiple), payload r in the layout; scales: [K, >= T] fp32
+    (column t = tensor t). With self_row >= 0 that row is replaced by the receiver's own fp32 bucket self_x,
+    added last and exactly (async_peer.py:170-174). Returns the flat fp32 bucket; positions outside every
+    tensor are zero when `out` is None (left untouched otherwise)."""
+    if q_rows.dim() != 2 or q_rows.dtype != torch.int8 or not q_rows.is_contiguous():
+        raise ValueError("dequantize_mean_batched: q_rows must be a contiguous [K, row_bytes] int8 tensor")
+    k, row = q_rows.shape
+    if row < layout.total:
+        raise ValueError("dequantize_mean_batched: rows shorter than the bucket layout")
+    sc = scales.reshape(k, -1)
+    if sc.shape[1] < layout.ntensors or sc.dtype != torch.float32:
+        raise ValueError("dequantize_mean_batched: scales must be fp32 [K, >= ntensors]")
+    dev = q_rows.device
+    xp = None
+    if self_row >= 0:
+        self_x = _dev(self_x, "self_x")
+        if self_x.dtype != torch.float32 or self_x.numel() < layout.total:
+            raise ValueError("dequantize_mean_batched: self_x must be an fp32 bucket of the layout")
+        xp = self_x.data_ptr()
+    out = torch.zeros(layout.total, dtype=torch.float32, device=dev) if out is None else out
+    check(_lib.load().adfl_slq_dequantize_mean_batched(q_rows.data_ptr(), row, k, layout.device_chunks(dev).data_ptr(),
+                                                       layout.nchunks, sc.data_ptr(), sc.stride(0), self_row, xp,
+                                                       out.data_ptr(), _stream(dev)))
+    return out
 
 
 def _require_even_offsets(layout: BucketLayout) -> None:

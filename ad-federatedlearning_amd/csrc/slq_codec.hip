@@ -834,6 +834,77 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_batched(const int8_t* __r
   for (int i = head + ntiles * kTile + threadIdx.x; i < c.len; i += kBlock) oc[i] = s * (float)qc[i];
 }
 
+// Peer mean of K bucketed payloads with per-tensor scales — the decentralized exchange of a whole state dict
+// under SLQChannel's per-tensor codec (ray_ad.py:164-190 averaging every tensor; quant.py:74-94 giving each
+// tensor its own scale): for tensor t and element i of the bucket,
+//   out[i] = fp32(sum over rows r != self_row, in r order, of fp32(scale_r[t] * q_r[i]), then + self_x[i]) / K
+// with the division correctly rounded, exactly k_dequantize_mean's arithmetic per tensor. Row r's payload is
+// q + r * row_stride (one bucket payload each, the same layout), its scales scales + r * scale_stride.
+// One block per chunk: the < 16 head elements and the tail element-wise, wave tiles in between.
+__device__ __forceinline__ float mean_elem(const int8_t* __restrict__ q, int64_t row_stride, int k,
+                                           const float* __restrict__ scales, int64_t scale_stride, int tensor,
+                                           int self_row, const float* __restrict__ self_x, int64_t e, double dk) {
+  float acc = 0.0f;
+  bool first = true;
+  for (int r = 0; r < k; ++r) {
+    if (r == self_row) continue;
+    const float d = scales[r * scale_stride + tensor] * (float)q[r * row_stride + e];
+    acc = first ? d : acc + d;
+    first = false;
+  }
+  if (self_row >= 0) acc = first ? self_x[e] : acc + self_x[e];
+  return (float)((double)acc / dk);
+}
+
+__global__ __launch_bounds__(kBlock) void k_dequantize_mean_batched(const int8_t* __restrict__ q, int64_t row_stride,
+                                                                    int k, const adfl_slq_chunk* __restrict__ chunks,
+                                                                    const float* __restrict__ scales,
+                                                                    int64_t scale_stride, int self_row,
+                                                                    const float* __restrict__ self_x,
+                                                                    float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kWaves][kTile / 4];
+  const adfl_slq_chunk c = chunks[blockIdx.x];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const double dk = (double)k;
+  const int head = chunk_head(c.start, c.len, 16);
+  if ((int)threadIdx.x < head)
+    out[c.start + threadIdx.x] =
+        mean_elem(q, row_stride, k, scales, scale_stride, c.tensor, self_row, self_x, c.start + threadIdx.x, dk);
+  const int ntiles = (c.len - head) / kTile;
+  for (int t = wave; t < ntiles; t += kWaves) {
+    const int64_t base = c.start + head + (int64_t)t * kTile;  // 16-element aligned
+    float4 acc[4];
+    bool first = true;
+    for (int r = 0; r < k; ++r) {
+      if (r == self_row) continue;
+      const uint4* q16 = reinterpret_cast<const uint4*>(q + r * row_stride + base);
+      const float s = scales[r * scale_stride + c.tensor];
+      reinterpret_cast<uint4*>(lds[wave])[lane] = q16[lane];
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float4 v = dequant4(lds[wave][j * 64 + lane], s);
+        acc[j] = first ? v : add4(acc[j], v);
+      }
+      __builtin_amdgcn_wave_barrier();
+      first = false;
+    }
+    if (self_row >= 0) {
+      const float4* xs = reinterpret_cast<const float4*>(self_x + base);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float4 v = xs[j * 64 + lane];
+        acc[j] = first ? v : add4(acc[j], v);
+      }
+    }
+    float4* o4 = reinterpret_cast<float4*>(out + base);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) store4_nt(o4 + j * 64 + lane, div4(acc[j], dk));
+  }
+  for (int i = head + ntiles * kTile + threadIdx.x; i < c.len; i += kBlock)
+    out[c.start + i] = mean_elem(q, row_stride, k, scales, scale_stride, c.tensor, self_row, self_x, c.start + i, dk);
+}
+
 // Decode + accumulate into K models (pool.py:62-75, qafel.py:176-179 via model.py:337-347): the chunk's
 // payload is decoded once into registers (8 float4 per thread), then every model's slice is read, added
 // (fp32(a + d), what mul_(1).add_(d, alpha=1) computes) and written back with 16-byte accesses when the
@@ -1267,6 +1338,21 @@ int adfl_slq_dequantize_mean_self(const int8_t* d_q, int64_t row_stride_bytes, i
   if (self_row >= 0 && !aligned16(d_self_x)) return ADFL_E_ALIGN;
   hipLaunchKernelGGL(k_dequantize_mean, dim3(tile_grid(n / kTile)), dim3(kBlock), 0, (hipStream_t)stream, d_q,
                      row_stride_bytes, (int)k, n, d_scales, scale_stride, (int)self_row, d_self_x, d_out);
+  return launch_status();
+}
+
+int adfl_slq_dequantize_mean_batched(const int8_t* d_q, int64_t row_stride_bytes, int32_t k,
+                                     const adfl_slq_chunk* d_chunks, int64_t nchunks, const float* d_scales,
+                                     int64_t scale_stride, int32_t self_row, const float* d_self_x, float* d_out,
+                                     void* stream) {
+  if (!d_q || !d_chunks || !d_scales || !d_out || k < 1 || nchunks < 1 || nchunks > INT32_MAX || scale_stride < 1 ||
+      row_stride_bytes < 1)
+    return ADFL_E_ARG;
+  if (self_row >= k || self_row < -1 || (self_row >= 0 && !d_self_x)) return ADFL_E_ARG;
+  if (!aligned16(d_q) || !aligned16(d_out) || (row_stride_bytes & 15) != 0) return ADFL_E_ALIGN;
+  if (self_row >= 0 && !aligned16(d_self_x)) return ADFL_E_ALIGN;
+  hipLaunchKernelGGL(k_dequantize_mean_batched, dim3((unsigned)nchunks), dim3(kBlock), 0, (hipStream_t)stream, d_q,
+                     row_stride_bytes, (int)k, d_chunks, d_scales, scale_stride, (int)self_row, d_self_x, d_out);
   return launch_status();
 }
 

@@ -175,6 +175,19 @@ int adfl_slq_dequantize_mean_self_int4(const uint8_t* d_packed, int64_t row_stri
                                        const float* d_scales, int64_t scale_stride, int32_t self_row,
                                        const float* d_self_x, float* d_out, void* stream);
 
+/* The same mean over K BUCKETED payloads with per-tensor scales: the decentralized exchange of a whole
+ * state dict under SLQChannel's per-tensor codec (Examples/ray_ad.py:164-190 averages every tensor;
+ * Src/ADFL/Channel/quant.py:74-94 gives each its own scale). Row r: payload d_q + r * row_stride_bytes in the
+ * layout of d_chunks (an adfl_slq_encode_batched* payload), scales d_scales + r * scale_stride (one fp32 per
+ * tensor). For tensor t, element i: (sum over r != self_row in r order of fp32(scale_r[t] * q_r[i]), then
+ * + d_self_x[i] if self_row >= 0) / k, fp32 adds, correctly rounded division — adfl_slq_dequantize_mean_self
+ * per tensor. d_out and d_self_x are flat buckets in the same layout; positions outside every tensor are
+ * not written. row_stride_bytes: a multiple of 16, at least the bucket's extent. */
+int adfl_slq_dequantize_mean_batched(const int8_t* d_q, int64_t row_stride_bytes, int32_t k,
+                                     const adfl_slq_chunk* d_chunks, int64_t nchunks, const float* d_scales,
+                                     int64_t scale_stride, int32_t self_row, const float* d_self_x, float* d_out,
+                                     void* stream);
+
 /* Fused decode + in-place accumulate into K models: for every model k and tensor t,
  *   model_k[t][i] = fp32(model_k[t][i] + fp32(scale_t * q[i]))
  * which is the receiver's on_client_receive followed by add_parameters_inpace(model, decoded, 1, 1)

@@ -33,6 +33,22 @@ class OracleCodec:
         off = (payload_bytes + 15) // 16 * 16
         r[off:off + 4] = np.array([scale], np.float32).view(np.uint8)
 
+    def encode_bucket(self, x, layout, bits, row):
+        q, scales = oracle.encode_batched(np.ascontiguousarray(x.numpy()), layout.offsets, layout.sizes, bits)
+        r = row.numpy()
+        r[:layout.total] = q.view(np.uint8)[:layout.total]
+        off = (layout.total + 15) // 16 * 16
+        r[off:off + 4 * layout.ntensors] = scales.view(np.uint8)
+
+    def mean_bucket(self, rows, layout, out, self_row=-1, self_x=None):
+        r = rows.numpy()
+        off = (layout.total + 15) // 16 * 16
+        scales = [np.ascontiguousarray(r[k, off:off + 4 * layout.ntensors]).view(np.float32) for k in range(r.shape[0])]
+        res = oracle.dequantize_mean_batched([r[k, :layout.total] for k in range(r.shape[0])], scales, layout.offsets,
+                                             layout.sizes, layout.total, self_row,
+                                             self_x.numpy() if self_x is not None else None)
+        out.copy_(torch.from_numpy(res))
+
     def mean(self, rows, n, packed, payload_bytes, out, self_row=-1, self_x=None):
         r = rows.numpy()
         off = (payload_bytes + 15) // 16 * 16
@@ -119,6 +135,72 @@ def test_peer_exchange_gloo(world):
     errors = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, cases, errors)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=180)
+    msgs = []
+    while not errors.empty():
+        msgs.append(errors.get())
+    assert not msgs, "\n".join(msgs)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+def _bucket_update(rank, layout):
+    rng = np.random.default_rng(2000 + rank)
+    flat = np.zeros(layout.total, np.float32)
+    for t, (o, n) in enumerate(zip(layout.offsets, layout.sizes)):
+        flat[o:o + n] = rng.standard_normal(int(n), dtype=np.float32) * np.float32(10.0 ** -(t % 3 + rank))
+    return flat
+
+
+def _bucket_worker(rank, world, port, cases, errors):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import sys
+        here = os.path.dirname(os.path.abspath(__file__))
+        sys.path.insert(0, os.path.join(os.path.dirname(here), "ad-federatedlearning_amd"))
+        from adfl_amd.exchange import PeerExchange
+        from adfl_amd.ops import BucketLayout
+        for sizes, align, exact_self in cases:
+            lay = BucketLayout(sizes, align=align)
+            ex = PeerExchange(lay.total, bits=8, device=torch.device("cpu"), codec=OracleCodec(),
+                              exact_self=exact_self, layout=lay)
+            assert ex.row_bytes == [(lay.total + 15) // 16 * 16 + (4 * lay.ntensors + 15) // 16 * 16]
+            got = ex.exchange_mean(torch.from_numpy(_bucket_update(rank, lay))).numpy()
+            # per tensor, the reference's mean: every rank's update SLQ-encoded with its own per-tensor
+            # scales (quant.py:74-94) and decoded; with exact_self this rank's own update enters exact, last
+            for t, (o, n) in enumerate(zip(lay.offsets.tolist(), lay.sizes.tolist())):
+                dec = []
+                for r in range(world):
+                    x = _bucket_update(r, lay)[o:o + n]
+                    if exact_self and r == rank:
+                        continue
+                    q, sc = oracle.encode(x, 8)
+                    dec.append(oracle.decode(q, sc))
+                if exact_self:
+                    dec.append(_bucket_update(rank, lay)[o:o + n])
+                ref = torch.stack([torch.from_numpy(d) for d in dec]).mean(0).numpy()
+                np.testing.assert_allclose(got[o:o + n], ref, rtol=1e-6, atol=1e-30, err_msg=str((sizes, t)))
+            gaps = np.ones(lay.total, bool)
+            for o, n in zip(lay.offsets.tolist(), lay.sizes.tolist()):
+                gaps[o:o + n] = False
+            assert (got[gaps] == 0).all()
+        dist.destroy_process_group()
+    except Exception as e:  # surfaced to the parent
+        import traceback
+        errors.put(f"rank {rank}: {e!r}\n{traceback.format_exc()}")
+
+
+def test_peer_exchange_bucket_gloo():
+    """A whole state dict per rank (BucketLayout: SLQChannel's per-tensor scales) through the exchange
+    protocol: the row carries the bucket payload and one scale per tensor, the mean is per tensor."""
+    cases = [([1000, 7, 4097, 33], 1, True), ([1000, 7, 4097, 33], 64, False), ([8193, 5, 64], 64, True)]
+    ctx = mp.get_context("spawn")
+    errors = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bucket_worker, args=(r, 2, port, cases, errors)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:

@@ -97,3 +97,33 @@ def test_exchange_k8_rows_mean(rccl_world1):
     got = ops.dequantize_mean(rows_d.view(torch.int8), scales.contiguous(), n).cpu().numpy()
     want = oracle.dequantize_mean([q for q, _ in enc], [s for _, s in enc])
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.parametrize("align", [1, 64])
+def test_bucket_exchange_world1_over_rccl(rccl_world1, align):
+    """PeerExchange(layout=...) through RCCL at world 1: one client's state dict with per-tensor scales
+    (quant.py:74-94) comes back as its own SLQ round trip per tensor (exact_self=False), the row carries
+    the bucket payload and the T scales, and the gaps between tensors stay zero."""
+    from adfl_amd import ops
+    from adfl_amd.exchange import PeerExchange
+    sizes = [3, 8193, 45662, 17, 70001]
+    lay = ops.BucketLayout(sizes, align=align)
+    rng = np.random.default_rng(align)
+    flat = np.zeros(lay.total, np.float32)
+    for t, (o, n) in enumerate(zip(lay.offsets.tolist(), sizes)):
+        flat[o:o + n] = rng.standard_normal(n, dtype=np.float32) * np.float32(10.0 ** -t)
+    ex = PeerExchange(lay.total, device=DEV, exact_self=False, layout=lay)
+    assert not ex.host_staged
+    got = ex.exchange_mean(torch.from_numpy(flat).to(DEV)).cpu().numpy()
+    q, s = oracle.encode_batched(flat, lay.offsets, lay.sizes, 8)
+    want = np.zeros(lay.total, np.float32)
+    for t, (o, n) in enumerate(zip(lay.offsets.tolist(), sizes)):
+        want[o:o + n] = oracle.decode(q[o:o + n], s[t])
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    row = ex.gathered[0].cpu().numpy()[0]
+    off = (lay.total + 15) // 16 * 16
+    assert np.array_equal(row[off:off + 4 * len(sizes)].view(np.float32).view(np.uint32), s.view(np.uint32))
+    # exact_self: one rank's mean is its own update
+    ex2 = PeerExchange(lay.total, device=DEV, layout=lay)
+    x = torch.from_numpy(flat).to(DEV)
+    assert torch.equal(ex2.exchange_mean(x), x)
