@@ -24,15 +24,16 @@ Transport: RCCL (``nccl`` backend) all-gathers device rows directly over xGMI. W
 (``Examples/ray_ad.py:29``), which RCCL cannot form because it needs distinct devices per rank — each row
 is staged through pinned host memory: D2H, gloo all-gather, H2D.
 
-Streams (device ranks). The absmax pass runs over the whole update on the caller's stream (the scale needs
-the global max). Every chunk's quantize is then enqueued at once on a side HIP stream, one event recorded
+Streams (device ranks, chunks > 1). The absmax pass runs over the whole update on the caller's stream (the
+scale needs the global max). Every chunk's quantize is then enqueued at once on a side HIP stream, one event recorded
 after each; chunk c's all-gather is issued from a gather stream that waits on event c only, so RCCL's
 stream starts chunk c as soon as its quantize retires, while chunk c+1's quantize runs on the side stream.
 Enqueuing all the quantizes before any collective keeps the side stream busy back to back: issuing one
 all-gather costs the host about as long as quantizing a C5 chunk (tools/exchange_trace.py measured
 ~100 us host gaps between the chunk quantizes when each quantize waited for the previous chunk's
 all_gather call to return). The caller's stream waits for the side stream before encode_and_gather
-returns, so later work there (the mean, or a write to x) is ordered after the quantizes.
+returns, so later work there (the mean, or a write to x) is ordered after the quantizes. With one chunk
+there is nothing to overlap, and the encode and the all-gather go on the caller's stream as issued.
 
 The codec backend is injectable so the exchange protocol can be exercised by gloo on CPU in tests; the
 product backend is the HIP codec (``HipCodec``) and there is no other.
@@ -121,6 +122,8 @@ class PeerExchange:
     numel   elements of each rank's update (same on every rank)
     bits    SLQ bit width (8: int8 payload; with packed=True the int4 nibble layout, compression.py:35-66)
     chunks  >1 splits quantize + all-gather into a pipeline (C5)
+    side_stream  chunk quantizes on a side stream, each all-gather behind its chunk's event (default: when
+            chunks > 1); False issues quantize and all-gather in order on the caller's stream
     layout  an ops.BucketLayout: the update is a bucketed state dict (numel = layout.total) encoded as
             SLQChannel encodes a state dict, one scale per tensor (quant.py:74-94), and averaged per tensor
             (ray_ad.py:164-190 averages every tensor). int8, one chunk. Without it the whole update has one
@@ -129,12 +132,13 @@ class PeerExchange:
 
     def __init__(self, numel: int, bits: int = 8, packed: bool = False, chunks: int = 1,
                  group: Optional[dist.ProcessGroup] = None, device: Optional[torch.device] = None, codec=None,
-                 exact_self: bool = True, layout=None):
+                 exact_self: bool = True, layout=None, side_stream: Optional[bool] = None):
         if numel < 1 or chunks < 1:
             raise ValueError("PeerExchange: numel and chunks must be >= 1")
         if layout is not None and (packed or chunks != 1 or numel != layout.total):
             raise ValueError("PeerExchange: a bucket layout takes int8 payloads in one chunk, numel = layout.total")
         self.layout = layout
+        self.side_stream = chunks > 1 if side_stream is None else side_stream
         self.numel, self.bits, self.packed, self.group = numel, bits, packed, group
         self.exact_self = exact_self
         self._x: Optional[torch.Tensor] = None
@@ -185,7 +189,9 @@ class PeerExchange:
         self._x = x
         if self.layout is None:
             self.codec.absmax(x)
-        if self.device.type != "cuda":   # host tensors (the protocol tests' codec): one sequence, no streams
+        if self.device.type != "cuda" or not self.side_stream:
+            # one chunk (nothing to overlap inside the exchange) or host tensors (the protocol tests' codec):
+            # everything in order on the caller's stream, no stream or event traffic per step
             works = []
             for c in range(len(self.bounds)):
                 self._encode(x, c)

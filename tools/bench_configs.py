@@ -191,9 +191,19 @@ def mode_exchange(args, world, rank, dev):
     if world == 1 and not dist.is_initialized():
         dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{free_port()}", rank=0, world_size=1,
                                 device_id=dev)
-    n = args.elems or (1 << 28)
     bits = 4 if args.packed else 8
-    ex = PeerExchange(n, bits=bits, packed=args.packed, chunks=args.chunks, device=dev)
+    layout = None
+    if args.layout != "flat":   # a whole C3 state dict per client, SLQChannel's per-tensor scales
+        sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
+        import recipes
+        from adfl_amd import ops
+        name = args.layout.split("_", 1)[1]
+        layout = ops.BucketLayout(recipes.bucket_sizes(name) if name == "equal" else recipes.bucket_sizes(name, 0))
+        n = layout.total
+    else:
+        n = args.elems or (1 << 28)
+    ex = PeerExchange(n, bits=bits, packed=args.packed, chunks=args.chunks, device=dev, layout=layout,
+                      side_stream=False if args.serial else None)
     g = torch.Generator(device=dev).manual_seed(rank)
     x = torch.randn(n, device=dev, generator=g) * 1e-3
     out = torch.empty(n, device=dev)
@@ -203,8 +213,10 @@ def mode_exchange(args, world, rank, dev):
     elapsed, _ = timed(step, args.steps, args.warmup, world, 1)
     t = elapsed / args.steps
     moved = ex.bytes_per_rank * (world - 1)  # bytes each rank receives over xGMI
-    return {"metric": f"C4/C5 peer exchange: SLQ encode + RCCL all-gather + fused decode-mean, bits={bits}"
-                      f"{' packed' if args.packed else ''}, chunks={args.chunks}", "unit": "GiB/s",
+    what = (f"bucketed {args.layout} state dict, per-tensor scales" if layout is not None else
+            f"bits={bits}{' packed' if args.packed else ''}, chunks={args.chunks}"
+            f"{', side stream' if ex.side_stream else ', in order'}")
+    return {"metric": f"peer exchange: SLQ encode + RCCL all-gather + fused decode-mean, {what}", "unit": "GiB/s",
             "value": round(world * n * 4 / GIB / t, 2), "n_gpus": world, "ms_per_step": round(t * 1e3, 4),
             "elements_per_rank": n, "bytes_per_rank_on_wire": ex.bytes_per_rank,
             "allgather_algbw_GBs": round(moved / t / 1e9, 1) if world > 1 else None}
@@ -603,6 +615,9 @@ def mode_stoch(args, world, rank, dev):
 
 def main():
     p = argparse.ArgumentParser()
+    p.add_argument("--serial", action="store_true", help="exchange: no side stream (quantize + all-gather in order)")
+    p.add_argument("--layout", choices=["flat", "c3_equal", "c3_loguniform"], default="flat",
+                   help="exchange: one flat update per rank, or a C3 state dict with per-tensor scales")
     p.add_argument("--mode", choices=["c3", "c5_int4", "exchange", "pcie", "channel", "channel_stoch", "stoch"],
                    required=True)
     p.add_argument("--gpus", type=int, default=1)
