@@ -14,7 +14,8 @@ synchronises. Semantics are the reference's, bit for bit:
 The same ops are registered as PyTorch custom ops ``torch.ops.adfl.*`` (with fake implementations, so
 they trace under torch.compile) at the bottom of this file: slq_absmax, slq_encode / slq_decode,
 slq_encode_int4 / slq_decode_int4, slq_encode_batched / slq_decode_batched and their _int4 variants over
-caller-placed tensors (host offsets / sizes), pack_int4 / unpack_int4 and slq_dequantize_mean.
+caller-placed tensors (host offsets / sizes), pack_int4 / unpack_int4, slq_dequantize_mean and
+slq_dequantize_mean_batched.
 """
 
 import os
@@ -590,4 +591,20 @@ def slq_dequantize_mean_op(q_rows: torch.Tensor, scales: torch.Tensor, n: int, s
 
 @slq_dequantize_mean_op.register_fake
 def _(q_rows, scales, n, self_row=-1, self_x=None):
+    return q_rows.new_empty((n,), dtype=torch.float32)
+
+
+@torch.library.custom_op("adfl::slq_dequantize_mean_batched", mutates_args=())
+def slq_dequantize_mean_batched_op(q_rows: torch.Tensor, scales: torch.Tensor, offsets: torch.Tensor,
+                                   sizes: torch.Tensor, n: int, self_row: int = -1,
+                                   self_x: Optional[torch.Tensor] = None) -> torch.Tensor:
+    lay = layout_for(offsets, sizes)
+    if n < lay.total:
+        raise ValueError("slq_dequantize_mean_batched: n smaller than the layout")
+    out = torch.zeros(n, dtype=torch.float32, device=q_rows.device)
+    return dequantize_mean_batched(q_rows, scales, lay, out=out, self_row=self_row, self_x=self_x)
+
+
+@slq_dequantize_mean_batched_op.register_fake
+def _(q_rows, scales, offsets, sizes, n, self_row=-1, self_x=None):
     return q_rows.new_empty((n,), dtype=torch.float32)

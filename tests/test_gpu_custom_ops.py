@@ -122,6 +122,30 @@ def test_dequantize_mean_matches_oracle(self_row):
     assert np.array_equal(_bits(got), _bits(want))
 
 
+def test_dequantize_mean_batched_op_matches_oracle():
+    """torch.ops.adfl.slq_dequantize_mean_batched: K bucketed payloads with per-tensor scales averaged per
+    tensor (ray_ad.py:164-190 under quant.py:74-94), caller-placed tensors, own row exact."""
+    sizes, offsets = [5000, 3, 9000], [9100, 0, 16]
+    n = 14208   # a 16-byte multiple row
+    k = 3
+    rng = np.random.default_rng(77)
+    rows = np.zeros((k, n), np.int8)
+    scales = np.zeros((k, 3), np.float32)
+    flats = []
+    for r in range(k):
+        f = np.zeros(n, np.float32)
+        for o, m in zip(offsets, sizes):
+            f[o:o + m] = rng.standard_normal(m, dtype=np.float32) * np.float32(1e-3)
+        q, s = oracle.encode_batched(f, offsets, sizes, 8)
+        rows[r], scales[r] = q, s
+        flats.append(f)
+    got = A.slq_dequantize_mean_batched(torch.from_numpy(rows).to(DEV), torch.from_numpy(scales).to(DEV),
+                                        torch.tensor(offsets), torch.tensor(sizes), n, 1,
+                                        torch.from_numpy(flats[1]).to(DEV)).cpu().numpy()
+    want = oracle.dequantize_mean_batched(list(rows), list(scales), offsets, sizes, n, 1, flats[1])
+    assert np.array_equal(_bits(got), _bits(want))
+
+
 def _opcheck_cases():
     flat, off, siz = _bucket(5, [3, 4097, 900], 2)
     x = torch.from_numpy(flat).to(DEV)
@@ -144,10 +168,14 @@ def _opcheck_cases():
         (A.unpack_int4, (A.pack_int4(q), [q.numel()])),
         (A.slq_dequantize_mean, (rows, torch.rand(3, device=DEV), 1000, -1, None)),
         (A.slq_dequantize_mean, (rows, torch.rand(3, device=DEV), 1000, 1, torch.randn(1000, device=DEV))),
+        (A.slq_dequantize_mean_batched, (rows, torch.rand(3, 2, device=DEV), torch.tensor([0, 500]),
+                                         torch.tensor([300, 500]), 1024, -1, None)),
+        (A.slq_dequantize_mean_batched, (rows, torch.rand(3, 2, device=DEV), torch.tensor([0, 500]),
+                                         torch.tensor([300, 500]), 1000, 2, torch.randn(1000, device=DEV))),
     ]
 
 
-@pytest.mark.parametrize("case", range(13))
+@pytest.mark.parametrize("case", range(15))
 def test_opcheck(case):
     op, args = _opcheck_cases()[case]
     torch.library.opcheck(op, args)
