@@ -66,6 +66,7 @@ SIGNATURES = {
     "adfl_slq_dequantize_mean_self_int4": (INT, [P, I64, I32, I64, P, I64, I32, P, P, P]),
     "adfl_slq_dequantize_add_batched": (INT, [P, P, I64, P, P, I32, I32, P]),
     "adfl_slq_dequantize_mean_batched": (INT, [P, I64, I32, P, I64, P, I64, I32, P, P, P]),
+    "adfl_slq_dequantize_mean_batched_int4": (INT, [P, I64, I32, P, I64, P, I64, I32, P, P, P]),
     # adfl_stoch.h
     "adfl_stoch_workspace_bytes": (I64, [I64]),
     "adfl_stoch_norms_batched": (INT, [P, P, I64, INT, P, I64, P, P, P]),

@@ -11,7 +11,8 @@ fp32 tensors pickled through Ray's object store. Here each rank is one client on
 Message layout (one row per chunk per rank, 16-byte aligned): ``payload | pad to 16 | fp32 scale | pad``.
 The scale rides in the row, so one all-gather moves payloads and scales together. With a bucket layout (a
 whole state dict, SLQChannel's per-tensor scales) the row is ``bucket payload | pad | T fp32 scales | pad``
-and the mean is taken per tensor with each row's scale for that tensor.
+and the mean is taken per tensor with each row's scale for that tensor; the bucket payload is int8, or
+int4-packed with ``packed=True`` (PackedSLQChannel per tensor, compression.py:35-66).
 
 The mean (``exact_self=True``, the default) is the reference's: the peers' decoded updates in rank order,
 then the rank's OWN update exactly as it is (fp32, not quantized: async_peer.py:170-174 and
@@ -73,25 +74,29 @@ class HipCodec:
         fn = self.lib.adfl_slq_quantize_int4 if packed else self.lib.adfl_slq_quantize
         check(fn(x.data_ptr(), x.numel(), bits, self.ws.data_ptr(), row.data_ptr(), scale_ptr, self._stream()))
 
-    def encode_bucket(self, x: torch.Tensor, layout, bits: int, row: torch.Tensor) -> None:
-        """A whole bucketed state dict into one message row: per-tensor SLQ payload (the layout's offsets) |
-        pad | one fp32 scale per tensor (ops.encode_batched: one launch when every tensor fits a block)."""
+    def encode_bucket(self, x: torch.Tensor, layout, bits: int, row: torch.Tensor, packed: bool = False) -> None:
+        """A whole bucketed state dict into one message row: per-tensor SLQ payload (the layout's offsets;
+        int4-packed with packed=True) | pad | one fp32 scale per tensor (ops.encode_batched[_int4]: one launch
+        when every tensor fits a block)."""
         from . import ops
-        total = layout.total
-        soff = _pad16(total)
+        pb = (layout.total + 1) // 2 if packed else layout.total
+        soff = _pad16(pb)
         if self._partials is None or self._partials.numel() < layout.nchunks:
             self._partials = torch.empty(layout.nchunks, dtype=torch.int32, device=self.device)
-        ops.encode_batched(x, layout, bits, q=row[:total].view(torch.int8),
-                           scales=row[soff:soff + 4 * layout.ntensors].view(torch.float32), partials=self._partials)
+        scales = row[soff:soff + 4 * layout.ntensors].view(torch.float32)
+        if packed:
+            ops.encode_batched_int4(x, layout, bits, packed=row[:pb], scales=scales, partials=self._partials)
+        else:
+            ops.encode_batched(x, layout, bits, q=row[:pb].view(torch.int8), scales=scales, partials=self._partials)
 
     def mean_bucket(self, rows: torch.Tensor, layout, out: torch.Tensor, self_row: int = -1,
-                    self_x: Optional[torch.Tensor] = None) -> None:
+                    self_x: Optional[torch.Tensor] = None, packed: bool = False) -> None:
         k, row_bytes = rows.shape
         xp = self_x.data_ptr() if self_row >= 0 else None
-        check(self.lib.adfl_slq_dequantize_mean_batched(rows.data_ptr(), row_bytes, k,
-                                                        layout.device_chunks(self.device).data_ptr(), layout.nchunks,
-                                                        rows.data_ptr() + _pad16(layout.total), row_bytes // 4,
-                                                        self_row, xp, out.data_ptr(), self._stream()))
+        pb = (layout.total + 1) // 2 if packed else layout.total
+        fn = self.lib.adfl_slq_dequantize_mean_batched_int4 if packed else self.lib.adfl_slq_dequantize_mean_batched
+        check(fn(rows.data_ptr(), row_bytes, k, layout.device_chunks(self.device).data_ptr(), layout.nchunks,
+                 rows.data_ptr() + _pad16(pb), row_bytes // 4, self_row, xp, out.data_ptr(), self._stream()))
 
     def mean(self, rows: torch.Tensor, n: int, packed: bool, payload_bytes: int, out: torch.Tensor,
              self_row: int = -1, self_x: Optional[torch.Tensor] = None) -> None:
@@ -126,7 +131,8 @@ class PeerExchange:
             chunks > 1); False issues quantize and all-gather in order on the caller's stream
     layout  an ops.BucketLayout: the update is a bucketed state dict (numel = layout.total) encoded as
             SLQChannel encodes a state dict, one scale per tensor (quant.py:74-94), and averaged per tensor
-            (ray_ad.py:164-190 averages every tensor). int8, one chunk. Without it the whole update has one
+            (ray_ad.py:164-190 averages every tensor). One chunk; int8, or int4 with packed=True (even tensor
+            offsets, e.g. BucketLayout(align=2) or the default 64). Without it the whole update has one
             scale (BASELINE's C4 / C5: one flat gradient per client).
     """
 
@@ -135,8 +141,10 @@ class PeerExchange:
                  exact_self: bool = True, layout=None, side_stream: Optional[bool] = None):
         if numel < 1 or chunks < 1:
             raise ValueError("PeerExchange: numel and chunks must be >= 1")
-        if layout is not None and (packed or chunks != 1 or numel != layout.total):
-            raise ValueError("PeerExchange: a bucket layout takes int8 payloads in one chunk, numel = layout.total")
+        if layout is not None and (chunks != 1 or numel != layout.total):
+            raise ValueError("PeerExchange: a bucket layout is exchanged in one chunk, numel = layout.total")
+        if layout is not None and packed and (layout.align % 2 or (layout.offsets % 2).any()):
+            raise ValueError("PeerExchange: an int4 bucket needs even tensor offsets")
         self.layout = layout
         self.side_stream = chunks > 1 if side_stream is None else side_stream
         self.numel, self.bits, self.packed, self.group = numel, bits, packed, group
@@ -219,7 +227,7 @@ class PeerExchange:
 
     def _encode(self, x: torch.Tensor, c: int) -> None:
         if self.layout is not None:
-            self.codec.encode_bucket(x, self.layout, self.bits, self.local[c])
+            self.codec.encode_bucket(x, self.layout, self.bits, self.local[c], self.packed)
         else:
             self.codec.quantize(self._chunk(x, c), self.bits, self.packed, self.local[c], self.payload[c])
 
@@ -246,7 +254,8 @@ class PeerExchange:
             if w is not None:
                 w.wait()
             if self.layout is not None:
-                self.codec.mean_bucket(rows, self.layout, out, self_row, self._x if self_row >= 0 else None)
+                self.codec.mean_bucket(rows, self.layout, out, self_row, self._x if self_row >= 0 else None,
+                                       self.packed)
                 continue
             self.codec.mean(rows, c1 - c0, self.packed, pb, out[c0:c1], self_row,
                             self._x[c0:c1] if self_row >= 0 else None)

@@ -15,7 +15,7 @@ The same ops are registered as PyTorch custom ops ``torch.ops.adfl.*`` (with fak
 they trace under torch.compile) at the bottom of this file: slq_absmax, slq_encode / slq_decode,
 slq_encode_int4 / slq_decode_int4, slq_encode_batched / slq_decode_batched and their _int4 variants over
 caller-placed tensors (host offsets / sizes), pack_int4 / unpack_int4, slq_dequantize_mean and
-slq_dequantize_mean_batched.
+slq_dequantize_mean_batched (+ _int4).
 """
 
 import os
@@ -348,17 +348,22 @@ def dequantize_add_batched(q: torch.Tensor, scales: torch.Tensor, layout: Bucket
 
 def dequantize_mean_batched(q_rows: torch.Tensor, scales: torch.Tensor, layout: BucketLayout, *,
                             out: Optional[torch.Tensor] = None, self_row: int = -1,
-                            self_x: Optional[torch.Tensor] = None) -> torch.Tensor:
+                            self_x: Optional[torch.Tensor] = None, packed: bool = False) -> torch.Tensor:
     """Peer mean of K bucketed int8 payloads with per-tensor scales (SLQChannel's per-tensor codec over a
     whole state dict, averaged as Examples/ray_ad.py:164-190 averages every tensor). q_rows: [K, row_bytes]
     int8 (row_bytes >= layout.total, a 16-byte multiple), payload r in the layout; scales: [K, >= T] fp32
     (column t = tensor t). With self_row >= 0 that row is replaced by the receiver's own fp32 bucket self_x,
-    added last and exactly (async_peer.py:170-174). Returns the flat fp32 bucket; positions outside every
-    tensor are zero when `out` is None (left untouched otherwise)."""
-    if q_rows.dim() != 2 or q_rows.dtype != torch.int8 or not q_rows.is_contiguous():
-        raise ValueError("dequantize_mean_batched: q_rows must be a contiguous [K, row_bytes] int8 tensor")
+    added last and exactly (async_peer.py:170-174). packed=True: the rows are int4-packed bucket payloads
+    (encode_batched_int4's: uint8, row_bytes >= ceil(layout.total / 2), even tensor offsets) -- the
+    PackedSLQChannel exchange. Returns the flat fp32 bucket; positions outside every tensor are zero when
+    `out` is None (left untouched otherwise)."""
+    dt = torch.uint8 if packed else torch.int8
+    if q_rows.dim() != 2 or q_rows.dtype != dt or not q_rows.is_contiguous():
+        raise ValueError(f"dequantize_mean_batched: q_rows must be a contiguous [K, row_bytes] {dt} tensor")
     k, row = q_rows.shape
-    if row < layout.total:
+    if packed:
+        _require_even_offsets(layout)
+    if row < ((layout.total + 1) // 2 if packed else layout.total):
         raise ValueError("dequantize_mean_batched: rows shorter than the bucket layout")
     sc = scales.reshape(k, -1)
     if sc.shape[1] < layout.ntensors or sc.dtype != torch.float32:
@@ -371,9 +376,11 @@ def dequantize_mean_batched(q_rows: torch.Tensor, scales: torch.Tensor, layout: 
             raise ValueError("dequantize_mean_batched: self_x must be an fp32 bucket of the layout")
         xp = self_x.data_ptr()
     out = torch.zeros(layout.total, dtype=torch.float32, device=dev) if out is None else out
-    check(_lib.load().adfl_slq_dequantize_mean_batched(q_rows.data_ptr(), row, k, layout.device_chunks(dev).data_ptr(),
-                                                       layout.nchunks, sc.data_ptr(), sc.stride(0), self_row, xp,
-                                                       out.data_ptr(), _stream(dev)))
+    if out.dtype != torch.float32 or out.numel() < layout.total or not out.is_contiguous():
+        raise ValueError("dequantize_mean_batched: out must be a contiguous fp32 bucket of the layout")
+    fn = _lib.load().adfl_slq_dequantize_mean_batched_int4 if packed else _lib.load().adfl_slq_dequantize_mean_batched
+    check(fn(q_rows.data_ptr(), row, k, layout.device_chunks(dev).data_ptr(), layout.nchunks, sc.data_ptr(),
+             sc.stride(0), self_row, xp, out.data_ptr(), _stream(dev)))
     return out
 
 
@@ -386,15 +393,20 @@ def encode_batched_int4(flat: torch.Tensor, layout: BucketLayout, bits: int = 4,
                         packed: Optional[torch.Tensor] = None, scales: Optional[torch.Tensor] = None,
                         partials: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """Per-tensor SLQ encode fused with pack_4bit over a bucket: packed byte e/2 holds flat elements
-    e, e+1 (layout.total // 2 bytes); per-tensor fp32 scales."""
+    e, e+1 (ceil(layout.total / 2) bytes); per-tensor fp32 scales."""
     if flat.dtype != torch.float32:
         raise RuntimeError(f"Quantize only works on Float Tensor, got {_TORCH_TYPE_NAMES.get(flat.dtype, flat.dtype)}")
     _require_even_offsets(layout)
     flat = _dev(flat, "flat")
+    if flat.numel() < layout.total:
+        raise ValueError("encode_batched_int4: flat buffer smaller than the layout")
     dev = flat.device
-    packed = torch.empty(layout.total // 2, dtype=torch.uint8, device=dev) if packed is None else packed
+    packed = torch.empty((layout.total + 1) // 2, dtype=torch.uint8, device=dev) if packed is None else packed
     scales = torch.empty(layout.ntensors, dtype=torch.float32, device=dev) if scales is None else scales
     partials = torch.empty(layout.nchunks, dtype=torch.int32, device=dev) if partials is None else partials
+    if packed.numel() < (layout.total + 1) // 2 or scales.numel() < layout.ntensors or \
+            partials.numel() < layout.nchunks:
+        raise ValueError("encode_batched_int4: packed / scales / partials smaller than the layout needs")
     check(_lib.load().adfl_slq_encode_batched_int4_work(flat.data_ptr(), layout.device_chunks(dev).data_ptr(),
                                                         layout.nchunks, layout.device_work(dev).data_ptr(),
                                                         layout.nwork, bits, packed.data_ptr(), scales.data_ptr(),
@@ -409,6 +421,8 @@ def decode_batched_int4(packed: torch.Tensor, scales: torch.Tensor, layout: Buck
     packed = _dev(packed, "packed")
     dev = packed.device
     out = torch.empty(layout.total, dtype=torch.float32, device=dev) if out is None else out
+    if packed.numel() < (layout.total + 1) // 2 or out.numel() < layout.total or scales.numel() < layout.ntensors:
+        raise ValueError("decode_batched_int4: packed / scales / out smaller than the layout needs")
     check(_lib.load().adfl_slq_dequantize_batched_int4(packed.data_ptr(), layout.device_chunks(dev).data_ptr(),
                                                        layout.nchunks, scales.data_ptr(), out.data_ptr(),
                                                        _stream(dev)))
@@ -608,3 +622,20 @@ def slq_dequantize_mean_batched_op(q_rows: torch.Tensor, scales: torch.Tensor, o
 @slq_dequantize_mean_batched_op.register_fake
 def _(q_rows, scales, offsets, sizes, n, self_row=-1, self_x=None):
     return q_rows.new_empty((n,), dtype=torch.float32)
+
+
+@torch.library.custom_op("adfl::slq_dequantize_mean_batched_int4", mutates_args=())
+def slq_dequantize_mean_batched_int4_op(packed_rows: torch.Tensor, scales: torch.Tensor, offsets: torch.Tensor,
+                                        sizes: torch.Tensor, n: int, self_row: int = -1,
+                                        self_x: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """slq_dequantize_mean_batched over int4-packed rows (uint8 [K, row_bytes], even offsets)."""
+    lay = layout_for(offsets, sizes)
+    if n < lay.total:
+        raise ValueError("slq_dequantize_mean_batched_int4: n smaller than the layout")
+    out = torch.zeros(n, dtype=torch.float32, device=packed_rows.device)
+    return dequantize_mean_batched(packed_rows, scales, lay, out=out, self_row=self_row, self_x=self_x, packed=True)
+
+
+@slq_dequantize_mean_batched_int4_op.register_fake
+def _(packed_rows, scales, offsets, sizes, n, self_row=-1, self_x=None):
+    return packed_rows.new_empty((n,), dtype=torch.float32)

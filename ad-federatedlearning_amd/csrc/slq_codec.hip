@@ -905,6 +905,75 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_mean_batched(const int8_t
     out[c.start + i] = mean_elem(q, row_stride, k, scales, scale_stride, c.tensor, self_row, self_x, c.start + i, dk);
 }
 
+// The same mean over K int4-packed bucket payloads (PackedSLQChannel per tensor; encode_batched_int4's
+// layout: even tensor offsets, flat element e in byte e/2, high nibble for even e). Heads run to a 32-element
+// (16-byte) boundary, wave tiles are kTile4 = 2048 elements = 1 KiB of packed bytes per row.
+__device__ __forceinline__ float mean_elem_int4(const uint8_t* __restrict__ p, int64_t row_stride, int k,
+                                                const float* __restrict__ scales, int64_t scale_stride, int tensor,
+                                                int self_row, const float* __restrict__ self_x, int64_t e,
+                                                double dk) {
+  float acc = 0.0f;
+  bool first = true;
+  for (int r = 0; r < k; ++r) {
+    if (r == self_row) continue;
+    float e0, e1;
+    dequant_byte_int4(p[r * row_stride + (e >> 1)], scales[r * scale_stride + tensor], e0, e1);
+    const float d = (e & 1) ? e1 : e0;
+    acc = first ? d : acc + d;
+    first = false;
+  }
+  if (self_row >= 0) acc = first ? self_x[e] : acc + self_x[e];
+  return (float)((double)acc / dk);
+}
+
+__global__ __launch_bounds__(kBlock) void k_dequantize_mean_batched_int4(
+    const uint8_t* __restrict__ p, int64_t row_stride, int k, const adfl_slq_chunk* __restrict__ chunks,
+    const float* __restrict__ scales, int64_t scale_stride, int self_row, const float* __restrict__ self_x,
+    float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[kWaves][kTile4 / 4];
+  const adfl_slq_chunk c = chunks[blockIdx.x];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const double dk = (double)k;
+  const int head = chunk_head(c.start, c.len, 32);
+  if ((int)threadIdx.x < head)
+    out[c.start + threadIdx.x] = mean_elem_int4(p, row_stride, k, scales, scale_stride, c.tensor, self_row, self_x,
+                                                c.start + threadIdx.x, dk);
+  const int ntiles = (c.len - head) / kTile4;
+  for (int t = wave; t < ntiles; t += kWaves) {
+    const int64_t base = c.start + head + (int64_t)t * kTile4;  // 32-element aligned
+    float4 acc[8];
+    bool first = true;
+    for (int r = 0; r < k; ++r) {
+      if (r == self_row) continue;
+      const uint4* p16 = reinterpret_cast<const uint4*>(p + r * row_stride + (base >> 1));
+      const float s = scales[r * scale_stride + c.tensor];
+      reinterpret_cast<uint4*>(lds[wave])[lane] = p16[lane];
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float4 v = dequant2_int4(lds[wave][j * 64 + lane], s);
+        acc[j] = first ? v : add4(acc[j], v);
+      }
+      __builtin_amdgcn_wave_barrier();
+      first = false;
+    }
+    if (self_row >= 0) {
+      const float4* xs = reinterpret_cast<const float4*>(self_x + base);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float4 v = xs[j * 64 + lane];
+        acc[j] = first ? v : add4(acc[j], v);
+      }
+    }
+    float4* o4 = reinterpret_cast<float4*>(out + base);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) store4_nt(o4 + j * 64 + lane, div4(acc[j], dk));
+  }
+  for (int i = head + ntiles * kTile4 + threadIdx.x; i < c.len; i += kBlock)
+    out[c.start + i] = mean_elem_int4(p, row_stride, k, scales, scale_stride, c.tensor, self_row, self_x,
+                                      c.start + i, dk);
+}
+
 // Decode + accumulate into K models (pool.py:62-75, qafel.py:176-179 via model.py:337-347): the chunk's
 // payload is decoded once into registers (8 float4 per thread), then every model's slice is read, added
 // (fp32(a + d), what mul_(1).add_(d, alpha=1) computes) and written back with 16-byte accesses when the
@@ -1353,6 +1422,22 @@ int adfl_slq_dequantize_mean_batched(const int8_t* d_q, int64_t row_stride_bytes
   if (self_row >= 0 && !aligned16(d_self_x)) return ADFL_E_ALIGN;
   hipLaunchKernelGGL(k_dequantize_mean_batched, dim3((unsigned)nchunks), dim3(kBlock), 0, (hipStream_t)stream, d_q,
                      row_stride_bytes, (int)k, d_chunks, d_scales, scale_stride, (int)self_row, d_self_x, d_out);
+  return launch_status();
+}
+
+int adfl_slq_dequantize_mean_batched_int4(const uint8_t* d_packed, int64_t row_stride_bytes, int32_t k,
+                                          const adfl_slq_chunk* d_chunks, int64_t nchunks, const float* d_scales,
+                                          int64_t scale_stride, int32_t self_row, const float* d_self_x,
+                                          float* d_out, void* stream) {
+  if (!d_packed || !d_chunks || !d_scales || !d_out || k < 1 || nchunks < 1 || nchunks > INT32_MAX ||
+      scale_stride < 1 || row_stride_bytes < 1)
+    return ADFL_E_ARG;
+  if (self_row >= k || self_row < -1 || (self_row >= 0 && !d_self_x)) return ADFL_E_ARG;
+  if (!aligned16(d_packed) || !aligned16(d_out) || (row_stride_bytes & 15) != 0) return ADFL_E_ALIGN;
+  if (self_row >= 0 && !aligned16(d_self_x)) return ADFL_E_ALIGN;
+  hipLaunchKernelGGL(k_dequantize_mean_batched_int4, dim3((unsigned)nchunks), dim3(kBlock), 0, (hipStream_t)stream,
+                     d_packed, row_stride_bytes, (int)k, d_chunks, d_scales, scale_stride, (int)self_row, d_self_x,
+                     d_out);
   return launch_status();
 }
 

@@ -187,6 +187,14 @@ int adfl_slq_dequantize_mean_batched(const int8_t* d_q, int64_t row_stride_bytes
                                      const adfl_slq_chunk* d_chunks, int64_t nchunks, const float* d_scales,
                                      int64_t scale_stride, int32_t self_row, const float* d_self_x, float* d_out,
                                      void* stream);
+/* Same over K int4-packed bucket payloads (adfl_slq_encode_batched_int4's: every tensor offset in d_chunks
+ * EVEN, flat element e in byte e/2 of the row, high nibble for even e): PackedSLQChannel per tensor
+ * (Src/ADFL/compression.py:35-66 over quant.py:74-94). row_stride_bytes: a multiple of 16, at least
+ * ceil(extent / 2). */
+int adfl_slq_dequantize_mean_batched_int4(const uint8_t* d_packed, int64_t row_stride_bytes, int32_t k,
+                                          const adfl_slq_chunk* d_chunks, int64_t nchunks, const float* d_scales,
+                                          int64_t scale_stride, int32_t self_row, const float* d_self_x,
+                                          float* d_out, void* stream);
 
 /* Fused decode + in-place accumulate into K models: for every model k and tensor t,
  *   model_k[t][i] = fp32(model_k[t][i] + fp32(scale_t * q[i]))

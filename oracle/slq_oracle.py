@@ -146,18 +146,24 @@ def dequantize_mean_self(rows, scales, n: int, self_row: int, self_x, packed: bo
     return out
 
 
-def dequantize_mean_batched(rows, scales, offsets, sizes, total: int, self_row: int = -1, self_x=None) -> np.ndarray:
+def dequantize_mean_batched(rows, scales, offsets, sizes, total: int, self_row: int = -1, self_x=None,
+                            packed: bool = False) -> np.ndarray:
     """Peer mean of K bucketed int8 payloads with per-tensor scales: for each tensor t, dequantize_mean_self
     (self_row >= 0: the receiver's own fp32 values added last) or dequantize_mean over the rows' slices
     [offset_t, offset_t + size_t) with scales[r][t] (Examples/ray_ad.py:164-190 per tensor, quant.py:74-94).
-    Positions outside every tensor are 0."""
+    packed=True: int4-packed rows (even offsets; tensor t's bytes [offset_t / 2, ceil((offset_t + size_t) / 2)),
+    compression.py:35-66), through the int4 mean restatements. Positions outside every tensor are 0."""
     out = np.zeros(total, np.float32)
     for t, (o, n) in enumerate(zip(offsets, sizes)):
         o, n = int(o), int(n)
-        rs = [np.ascontiguousarray(np.asarray(r).view(np.uint8).reshape(-1)[o:o + n]) for r in rows]
+        lo, hi = (o // 2, (o + n + 1) // 2) if packed else (o, o + n)
+        rs = [np.ascontiguousarray(np.asarray(r).view(np.uint8).reshape(-1)[lo:hi]) for r in rows]
         sc = np.array([np.asarray(s, np.float32).reshape(-1)[t] for s in scales], np.float32)
         if self_row >= 0:
-            out[o:o + n] = dequantize_mean_self(rs, sc, n, self_row, np.asarray(self_x, np.float32).reshape(-1)[o:o + n])
+            out[o:o + n] = dequantize_mean_self(rs, sc, n, self_row, np.asarray(self_x, np.float32).reshape(-1)[o:o + n],
+                                                packed=packed)
+        elif packed:
+            out[o:o + n] = dequantize_mean_int4(rs, sc, n)
         else:
             out[o:o + n] = dequantize_mean([r.view(np.int8) for r in rs], sc)
     return out

@@ -13,7 +13,7 @@ from adfl_amd import ops
 A = torch.ops.adfl
 OPS = ["slq_absmax", "slq_encode", "slq_decode", "slq_encode_int4", "slq_decode_int4", "slq_encode_batched",
        "slq_decode_batched", "slq_encode_batched_int4", "slq_decode_batched_int4", "pack_int4", "unpack_int4",
-       "slq_dequantize_mean", "slq_dequantize_mean_batched"]
+       "slq_dequantize_mean", "slq_dequantize_mean_batched", "slq_dequantize_mean_batched_int4"]
 
 
 def test_every_op_is_registered():
@@ -48,6 +48,9 @@ def test_fake_shapes_and_dtypes():
         assert m.shape == (100,) and m.dtype == torch.float32
         mb = A.slq_dequantize_mean_batched(rows, mode.from_tensor(torch.empty(4, 3)), off, siz, 107, -1, None)
         assert mb.shape == (107,) and mb.dtype == torch.float32
+        prow = mode.from_tensor(torch.empty(4, 64, dtype=torch.uint8))
+        mb4 = A.slq_dequantize_mean_batched_int4(prow, mode.from_tensor(torch.empty(4, 3)), off, siz, 107, -1, None)
+        assert mb4.shape == (107,) and mb4.dtype == torch.float32
 
 
 def test_caller_placed_layout():

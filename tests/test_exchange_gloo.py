@@ -33,20 +33,22 @@ class OracleCodec:
         off = (payload_bytes + 15) // 16 * 16
         r[off:off + 4] = np.array([scale], np.float32).view(np.uint8)
 
-    def encode_bucket(self, x, layout, bits, row):
+    def encode_bucket(self, x, layout, bits, row, packed=False):
         q, scales = oracle.encode_batched(np.ascontiguousarray(x.numpy()), layout.offsets, layout.sizes, bits)
+        payload = oracle.pack_int4(q[:layout.total]) if packed else q.view(np.uint8)[:layout.total]
         r = row.numpy()
-        r[:layout.total] = q.view(np.uint8)[:layout.total]
-        off = (layout.total + 15) // 16 * 16
+        r[:payload.size] = payload
+        off = (payload.size + 15) // 16 * 16
         r[off:off + 4 * layout.ntensors] = scales.view(np.uint8)
 
-    def mean_bucket(self, rows, layout, out, self_row=-1, self_x=None):
+    def mean_bucket(self, rows, layout, out, self_row=-1, self_x=None, packed=False):
         r = rows.numpy()
-        off = (layout.total + 15) // 16 * 16
+        pb = (layout.total + 1) // 2 if packed else layout.total
+        off = (pb + 15) // 16 * 16
         scales = [np.ascontiguousarray(r[k, off:off + 4 * layout.ntensors]).view(np.float32) for k in range(r.shape[0])]
-        res = oracle.dequantize_mean_batched([r[k, :layout.total] for k in range(r.shape[0])], scales, layout.offsets,
+        res = oracle.dequantize_mean_batched([r[k, :pb] for k in range(r.shape[0])], scales, layout.offsets,
                                              layout.sizes, layout.total, self_row,
-                                             self_x.numpy() if self_x is not None else None)
+                                             self_x.numpy() if self_x is not None else None, packed=packed)
         out.copy_(torch.from_numpy(res))
 
     def mean(self, rows, n, packed, payload_bytes, out, self_row=-1, self_x=None):
@@ -163,11 +165,13 @@ def _bucket_worker(rank, world, port, cases, errors):
         sys.path.insert(0, os.path.join(os.path.dirname(here), "ad-federatedlearning_amd"))
         from adfl_amd.exchange import PeerExchange
         from adfl_amd.ops import BucketLayout
-        for sizes, align, exact_self in cases:
+        for sizes, align, exact_self, packed in cases:
             lay = BucketLayout(sizes, align=align)
-            ex = PeerExchange(lay.total, bits=8, device=torch.device("cpu"), codec=OracleCodec(),
+            bits = 4 if packed else 8
+            ex = PeerExchange(lay.total, bits=bits, packed=packed, device=torch.device("cpu"), codec=OracleCodec(),
                               exact_self=exact_self, layout=lay)
-            assert ex.row_bytes == [(lay.total + 15) // 16 * 16 + (4 * lay.ntensors + 15) // 16 * 16]
+            pb = (lay.total + 1) // 2 if packed else lay.total
+            assert ex.row_bytes == [(pb + 15) // 16 * 16 + (4 * lay.ntensors + 15) // 16 * 16]
             got = ex.exchange_mean(torch.from_numpy(_bucket_update(rank, lay))).numpy()
             # per tensor, the reference's mean: every rank's update SLQ-encoded with its own per-tensor
             # scales (quant.py:74-94) and decoded; with exact_self this rank's own update enters exact, last
@@ -177,8 +181,8 @@ def _bucket_worker(rank, world, port, cases, errors):
                     x = _bucket_update(r, lay)[o:o + n]
                     if exact_self and r == rank:
                         continue
-                    q, sc = oracle.encode(x, 8)
-                    dec.append(oracle.decode(q, sc))
+                    q, sc = oracle.encode(x, bits)
+                    dec.append(oracle.decode_int4(oracle.pack_int4(q), n, sc) if packed else oracle.decode(q, sc))
                 if exact_self:
                     dec.append(_bucket_update(rank, lay)[o:o + n])
                 ref = torch.stack([torch.from_numpy(d) for d in dec]).mean(0).numpy()
@@ -195,8 +199,11 @@ def _bucket_worker(rank, world, port, cases, errors):
 
 def test_peer_exchange_bucket_gloo():
     """A whole state dict per rank (BucketLayout: SLQChannel's per-tensor scales) through the exchange
-    protocol: the row carries the bucket payload and one scale per tensor, the mean is per tensor."""
-    cases = [([1000, 7, 4097, 33], 1, True), ([1000, 7, 4097, 33], 64, False), ([8193, 5, 64], 64, True)]
+    protocol: the row carries the bucket payload (int8, or int4-packed) and one scale per tensor, the mean
+    is per tensor."""
+    cases = [([1000, 7, 4097, 33], 1, True, False), ([1000, 7, 4097, 33], 64, False, False),
+             ([8193, 5, 64], 64, True, False), ([1000, 7, 4097, 33], 2, True, True),
+             ([8193, 5, 65], 64, False, True)]
     ctx = mp.get_context("spawn")
     errors = ctx.Queue()
     port = _free_port()

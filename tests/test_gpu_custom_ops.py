@@ -144,6 +144,16 @@ def test_dequantize_mean_batched_op_matches_oracle():
                                         torch.from_numpy(flats[1]).to(DEV)).cpu().numpy()
     want = oracle.dequantize_mean_batched(list(rows), list(scales), offsets, sizes, n, 1, flats[1])
     assert np.array_equal(_bits(got), _bits(want))
+    # the int4 exchange rows (PackedSLQChannel per tensor): even offsets, packed payload
+    offs4 = [9100, 0, 18]
+    prow = np.zeros((k, n // 2), np.uint8)
+    for r in range(k):
+        q4, s4 = oracle.encode_batched(np.roll(flats[r], 2), offs4, sizes, 4)
+        prow[r], scales[r] = oracle.pack_int4(q4), s4
+    got4 = A.slq_dequantize_mean_batched_int4(torch.from_numpy(prow).to(DEV), torch.from_numpy(scales).to(DEV),
+                                              torch.tensor(offs4), torch.tensor(sizes), n).cpu().numpy()
+    want4 = oracle.dequantize_mean_batched(list(prow), list(scales), offs4, sizes, n, -1, None, packed=True)
+    assert np.array_equal(_bits(got4), _bits(want4))
 
 
 def _opcheck_cases():
@@ -172,10 +182,13 @@ def _opcheck_cases():
                                          torch.tensor([300, 500]), 1024, -1, None)),
         (A.slq_dequantize_mean_batched, (rows, torch.rand(3, 2, device=DEV), torch.tensor([0, 500]),
                                          torch.tensor([300, 500]), 1000, 2, torch.randn(1000, device=DEV))),
+        (A.slq_dequantize_mean_batched_int4, (rows.view(torch.uint8)[:, :512].contiguous(),
+                                              torch.rand(3, 2, device=DEV), torch.tensor([0, 500]),
+                                              torch.tensor([300, 500]), 1000, 1, torch.randn(1000, device=DEV))),
     ]
 
 
-@pytest.mark.parametrize("case", range(15))
+@pytest.mark.parametrize("case", range(16))
 def test_opcheck(case):
     op, args = _opcheck_cases()[case]
     torch.library.opcheck(op, args)
