@@ -321,6 +321,55 @@ def _decode_add(c_params: QuantParameters, names: List[str], targets: List[Param
     torch.cuda.current_stream(dev).synchronize()
 
 
+def _stage_rows(clients: List[List[torch.Tensor]], lay: ops.BucketLayout, st: _DeviceStaging,
+                key: str) -> torch.Tensor:
+    """K clients' payload byte tensors (client k's tensor j at lay.offsets[j]) -> device rows
+    [K, pad16(lay.total)] uint8. All on the CPU: one native gather per client into its pinned row, that
+    row's H2D enqueued as soon as it is staged (the copy engine overlaps the next client's gather)."""
+    k = len(clients)
+    row = (lay.total + 15) // 16 * 16
+    dev = st.buf(key, k * row, torch.uint8).view(k, row)
+    if all(not t.is_cuda and t.is_contiguous() for c in clients for t in c):
+        host = st.buf(key + "_host", k * row, torch.uint8, pinned=True).view(k, row)
+        for r, c in enumerate(clients):
+            hostcopy.copy_pieces(*_range_copies(_ptrs(c), lay, host[r].data_ptr(), 1, 0, lay.total, to_bucket=True))
+            dev[r].copy_(host[r], non_blocking=True)
+    else:  # device (or mixed) payloads: per-tensor copies into the device rows
+        for r, c in enumerate(clients):
+            for t, off, n in zip(c, lay.offsets.tolist(), lay.sizes.tolist()):
+                dev[r, off:off + n].copy_(t.reshape(-1).to(st.device))
+    return dev
+
+
+@_serialized
+def _decode_mean(clients: List[List[torch.Tensor]], scales: List[List[float]], shapes: List[torch.Size],
+                 packed: bool) -> List[torch.Tensor]:
+    """The fp32 mean over K clients of their decoded tensors, tensor by tensor, in client order, in ONE
+    launch (ops.dequantize_mean_batched): clients[k][j] is client k's payload bytes for tensor j (a qint8
+    tensor's int8 view, or ceil(n/2) packed bytes with packed=True), scales[k][j] its scale. Returns one
+    owned tensor per entry (CPU when every client's payload is on the CPU)."""
+    st = _staging()
+    dev = st.device
+    sizes = tuple(int(torch.Size(s).numel()) for s in shapes)
+    if packed:   # element layout with even offsets; its bytes: every slot exactly ceil(n/2), back to back
+        lay = st.layout(sizes, align=2)
+        b_lay = st.layout(tuple((n + 1) // 2 for n in sizes), align=1)
+    else:
+        lay = b_lay = st.layout(sizes, align=1)
+    rows = _stage_rows([[t.view(torch.uint8) for t in c] for c in clients], b_lay, st, "mq")
+    s_dev = torch.tensor(scales, dtype=torch.float32).to(dev, non_blocking=True)
+    out_dev = ops.dequantize_mean_batched(rows if packed else rows.view(torch.int8), s_dev, lay,
+                                          out=st.buf("m_out", lay.total, torch.float32), packed=packed)
+    on_cpu = [not any(c[j].is_cuda for c in clients) for j in range(len(sizes))]
+    return _hand_out(out_dev, lay, [torch.Size(s) for s in shapes], on_cpu, st, "m_out")
+
+
+def _simple_aggregate(values: List[torch.Tensor]) -> torch.Tensor:
+    """One entry of simple_aggregate (Src/ADFL/model.py:221-234), as the reference computes it."""
+    with torch.no_grad():
+        return torch.sum(torch.stack(values, dim=0), dim=0) / len(values)
+
+
 @_serialized
 def _encode_dict_packed(params: Parameters, names: List[str], bits: int, stats: Optional[list] = None):
     """Packed int4 variant of _encode_dict: {name: (int8 tensor of ceil(n/2) packed bytes, scale)}; with
@@ -448,6 +497,48 @@ class SLQChannel(Channel):
                         t[n].mul_(1).add_(d.to(t[n].device), alpha=1)
         return time.perf_counter() - s_time
 
+    def receive_mean(self, all_c_params: List[CompressedParameters]) -> Tuple[Parameters, float]:
+        """``simple_aggregate([self.on_server_receive(c)[0] for c in all_c_params])`` — a synchronous
+        server decoding K client updates and averaging them (Src/ADFL/Strategy/simple.py:83-89 over
+        Src/ADFL/model.py:221-234; the peer mean of Examples/ray_ad.py:188). Returns (aggregate, seconds).
+
+        Tensors quantized in every update are decoded and averaged on the device in one launch: the K
+        payloads are read once and no decoded copy is materialised (ops.dequantize_mean_batched). Their
+        mean is the fp32 sum in client order, then / K: bit-identical to simple_aggregate for K <= 4;
+        for K >= 5 torch's CPU sum regroups the additions (multi-accumulator tails, cascade levels),
+        so the two agree to fp32 summation error. Everything else (biases, running statistics,
+        non-quantized payloads) is decoded and aggregated as the reference does, on the host."""
+        if not all_c_params:
+            raise AssertionError("receive_mean: no updates")   # simple_aggregate asserts len > 0
+        for c in all_c_params:
+            assert isinstance(c, QuantParameters)
+        s_time = time.perf_counter()
+        names = list(all_c_params[0].params.keys())
+        fused = [n for n in names if all(n in c.params and self._fusable(c.params[n]) for c in all_c_params)
+                 and len({tuple(c.params[n].shape) for c in all_c_params}) == 1]
+        out: Parameters = {}
+        if fused:
+            decoded = self._mean_payloads(all_c_params, fused)
+            out.update(zip(fused, decoded))
+        rest = [n for n in names if n not in out]
+        if rest:
+            parts = [self._receive(QuantParameters({n: c.params[n] for n in rest}, 0))[0] for c in all_c_params]
+            for n in rest:
+                out[n] = _simple_aggregate([p[n] for p in parts])
+        return {n: out[n] for n in names}, time.perf_counter() - s_time
+
+    @staticmethod
+    def _fusable(p: QuantParameter) -> bool:
+        d = p.data
+        return (d.ndim > 1 and d.is_quantized and d.numel() > 0 and d.dtype == torch.qint8
+                and d.qscheme() == torch.per_tensor_affine and d.q_zero_point() == 0)
+
+    def _mean_payloads(self, all_c_params: List[QuantParameters], names: List[str]) -> List[torch.Tensor]:
+        qs = [[c.params[n].data for n in names] for c in all_c_params]
+        # q_scale() is a double; fbgemm's dequantize uses it as fp32 (quant.py:110)
+        return _decode_mean([[_int8_view(q) for q in c] for c in qs], [[q.q_scale() for q in c] for c in qs],
+                            [q.shape for q in qs[0]], packed=False)
+
     def send_with_q_error(self, params: Parameters) -> Tuple[CompressedParameters, float, float, float]:
         """`on_client_send` fused with the worker's quantization-error metrics.
 
@@ -530,6 +621,14 @@ class PackedSLQChannel(SLQChannel):
         decoded = _decode_dict_packed(packed) if packed else {}
         params = {name: decoded[name] if name in decoded else p.data.data for name, p in c_params.params.items()}
         return params, time.perf_counter() - s_time
+
+    def _fusable(self, p: QuantParameter) -> bool:
+        return self._is_packed(p) and p.data.numel() == (torch.Size(p.shape).numel() + 1) // 2
+
+    def _mean_payloads(self, all_c_params: List[QuantParameters], names: List[str]) -> List[torch.Tensor]:
+        return _decode_mean([[c.params[n].data for n in names] for c in all_c_params],
+                            [[c.params[n].scale for n in names] for c in all_c_params],
+                            [torch.Size(all_c_params[0].params[n].shape) for n in names], packed=True)
 
     def _quantize_params(self, params: Parameters, bits: int, stats: Optional[list] = None) -> QuantParameters:
         names = [name for name, p in params.items() if p.ndim > 1]

@@ -1,0 +1,106 @@
+"""GPU: SLQChannel.receive_mean / PackedSLQChannel.receive_mean — a synchronous server decoding K client
+updates and averaging them, simple_aggregate([on_server_receive(c)[0] for c in updates])
+(Src/ADFL/Strategy/simple.py:83-89 over Src/ADFL/model.py:221-234), with the quantized tensors decoded and
+averaged in one HIP launch.
+
+* against simple_aggregate over the channel's own per-update decode (restated below: torch.stack, sum over
+  dim 0, / K — the reference function's three ops): bit-identical for K <= 4; for larger K (torch's CPU
+  sum regroups the additions there) within the bound two fp32 summation orders can differ by,
+  2 (K - 1) u sum|d_i| / K;
+* the quantized tensors bit for bit against the oracle's client-order mean of the decoded payloads
+  (oracle.dequantize_mean / dequantize_mean_int4) for every K;
+* passthrough entries (biases, 0-dim int64 counters) exactly as simple_aggregate computes them."""
+
+import numpy as np
+import pytest
+import torch
+
+import slq_oracle as oracle
+
+pytestmark = pytest.mark.gpu
+
+adfl_amd = pytest.importorskip("adfl_amd")
+from adfl_amd.Channel import PackedSLQChannel, SLQChannel  # noqa: E402
+
+SHAPES = {"conv1.weight": (64, 3, 7, 7), "fc.weight": (10, 513), "layer.weight": (257, 255), "tiny.weight": (1, 3),
+          "big.weight": (300, 1000)}
+
+
+def simple_aggregate(parameters):
+    """Src/ADFL/model.py:221-234."""
+    out = {}
+    with torch.no_grad():
+        for name in parameters[0].keys():
+            out[name] = torch.sum(torch.stack([p[name] for p in parameters], dim=0), dim=0) / len(parameters)
+    return out
+
+
+def _client(k):
+    g = torch.Generator().manual_seed(100 + k)
+    d = {n: torch.randn(s, generator=g) * (10.0 ** -(i % 3)) for i, (n, s) in enumerate(SHAPES.items())}
+    d["fc.bias"] = torch.randn(10, generator=g)
+    d["bn.num_batches_tracked"] = torch.tensor(7 + k, dtype=torch.int64)
+    return d
+
+
+def _same(a, b):
+    return a.dtype == b.dtype and a.shape == b.shape and np.array_equal(a.numpy().reshape(-1).view(np.uint8),
+                                                                         b.numpy().reshape(-1).view(np.uint8))
+
+
+@pytest.mark.parametrize("packed", [False, True])
+@pytest.mark.parametrize("k", [1, 2, 3, 4, 5, 8])
+def test_receive_mean_matches_simple_aggregate(k, packed):
+    ch = PackedSLQChannel(4) if packed else SLQChannel(8)
+    updates = [ch.on_client_send(_client(r))[0] for r in range(k)]
+    decoded = [ch.on_server_receive(u)[0] for u in updates]
+    want = simple_aggregate(decoded)
+    got, t = ch.receive_mean(updates)
+    assert t > 0 and list(got) == list(want)
+    for n in want:
+        assert got[n].device.type == "cpu" and got[n].shape == want[n].shape and got[n].dtype == want[n].dtype, n
+        if n in SHAPES:
+            # the oracle's client-order mean of the same payloads
+            numel = int(np.prod(SHAPES[n]))
+            if packed:
+                ref = oracle.dequantize_mean_int4([u.params[n].data.view(torch.uint8).numpy() for u in updates],
+                                                  [u.params[n].scale for u in updates], numel)
+            else:
+                ref = oracle.dequantize_mean([u.params[n].data.int_repr().numpy() for u in updates],
+                                             [u.params[n].data.q_scale() for u in updates])
+            assert np.array_equal(got[n].numpy().reshape(-1).view(np.uint32), ref.view(np.uint32)), n
+        if k <= 4 or n not in SHAPES:
+            assert _same(got[n], want[n]), n
+        else:
+            # two summation orders of K fp32 terms differ by at most 2 (K - 1) u sum|d_i| / K (u = 2^-24)
+            mag = torch.stack([d[n].abs() for d in decoded]).sum(0) / k
+            assert ((got[n] - want[n]).abs() <= 2 * (k - 1) * 2.0 ** -24 * mag).all(), n
+    got["fc.weight"].add_(1.0)   # owned and writable
+
+
+def test_receive_mean_device_updates_and_c3_layout():
+    """Device-resident updates stay on the device; a C3-sized dict (ResNet-18's 11.7 M parameters in 256
+    tensors, equal layout) from 4 clients is one launch and bit-identical to simple_aggregate."""
+    import recipes
+    sizes = recipes.bucket_sizes("equal")
+    ch = SLQChannel(8)
+    dev = torch.device("cuda", 0)
+    updates = []
+    for r in range(4):
+        g = torch.Generator(device=dev).manual_seed(r)
+        updates.append(ch.on_client_send({f"t{i}.weight": torch.randn(1, n, device=dev, generator=g) * 1e-3
+                                          for i, n in enumerate(sizes)})[0])
+    got, _ = ch.receive_mean(updates)
+    want = simple_aggregate([ch.on_server_receive(u)[0] for u in updates])
+    for n in want:
+        assert got[n].is_cuda and torch.equal(got[n], want[n]), n
+
+
+def test_receive_mean_errors():
+    ch = SLQChannel(8)
+    with pytest.raises(AssertionError):
+        ch.receive_mean([])
+    u1 = ch.on_client_send({"w": torch.randn(4, 4)})[0]
+    u2 = ch.on_client_send({"w": torch.randn(4, 5)})[0]
+    with pytest.raises(RuntimeError):   # torch.stack of unequal shapes, as simple_aggregate raises
+        ch.receive_mean([u1, u2])

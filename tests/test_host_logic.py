@@ -125,6 +125,23 @@ def test_passthrough_only_dict_needs_no_device():
     assert dec["b"].data_ptr() == b.data_ptr()  # `q_param.data.data`: a new view of the same storage
 
 
+def test_receive_mean_passthrough_entries_are_simple_aggregate():
+    """receive_mean over updates with nothing quantized: simple_aggregate's own arithmetic on the host
+    (Src/ADFL/model.py:221-234: stack, sum over dim 0, / K; an int64 counter becomes fp32), key order of
+    the first update, no device."""
+    ch = SLQChannel(8)
+    ups = [ch.on_client_send({"b": torch.randn(5) * (r + 1), "n": torch.tensor(3 + r)})[0] for r in range(6)]
+    got, t = ch.receive_mean(ups)
+    assert list(got) == ["b", "n"] and t >= 0
+    for name in ("b", "n"):
+        want = torch.sum(torch.stack([u.params[name].data for u in ups], dim=0), dim=0) / len(ups)
+        assert got[name].dtype == want.dtype and torch.equal(got[name], want)
+    with pytest.raises(AssertionError):
+        ch.receive_mean([])
+    with pytest.raises(AssertionError):
+        ch.receive_mean([{"b": torch.zeros(2)}])   # not QuantParameters (quant.py:68)
+
+
 def test_bucket_layout():
     lay = ops.BucketLayout([10, 8192, 8193, 64])
     assert lay.offsets.tolist() == [0, 64, 8256, 16512] and lay.total == 16576

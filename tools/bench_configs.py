@@ -213,7 +213,8 @@ def mode_exchange(args, world, rank, dev):
     elapsed, _ = timed(step, args.steps, args.warmup, world, 1)
     t = elapsed / args.steps
     moved = ex.bytes_per_rank * (world - 1)  # bytes each rank receives over xGMI
-    what = (f"bucketed {args.layout} state dict, per-tensor scales" if layout is not None else
+    what = (f"bucketed {args.layout} state dict, per-tensor scales, bits={bits}{' packed' if args.packed else ''}"
+            if layout is not None else
             f"bits={bits}{' packed' if args.packed else ''}, chunks={args.chunks}"
             f"{', side stream' if ex.side_stream else ', in order'}")
     return {"metric": f"peer exchange: SLQ encode + RCCL all-gather + fused decode-mean, {what}", "unit": "GiB/s",
@@ -427,12 +428,38 @@ def mode_channel(args, world, rank, dev):
                for k in params if params[k].ndim > 1)
     best = lambda xs, i: min(x[i] for x in xs) * 1e3  # noqa: E731
     gib = sum(t.numel() for t in params.values()) * 4 / GIB
+
+    # synchronous server aggregate of K = 4 client updates (Src/ADFL/Strategy/simple.py:83-89): ours
+    # receive_mean (one fused decode-mean launch) vs the reference's K decodes + simple_aggregate
+    # (Src/ADFL/model.py:221-234) on the host
+    ups = []
+    for ci in range(4):
+        gr = torch.Generator().manual_seed(10 + ci)
+        ups.append(ch.on_client_send({k: torch.randn(v.shape, generator=gr) * 1e-3 for k, v in params.items()})[0])
+
+    def ref_aggregate():
+        t0 = time.perf_counter()
+        dec = [{k: (p.data.dequantize() if p.data.ndim > 1 else p.data.data) for k, p in u.params.items()}
+               for u in ups]
+        agg = {k: torch.sum(torch.stack([d[k] for d in dec], dim=0), dim=0) / len(dec) for k in dec[0]}
+        return time.perf_counter() - t0, agg
+
+    for _ in range(args.warmup):
+        ch.receive_mean(ups)
+        ref_aggregate()
+    om = min(ch.receive_mean(ups)[1] for _ in range(args.steps))
+    rm = min(ref_aggregate()[0] for _ in range(max(3, args.steps // 4)))
+    mine, want = ch.receive_mean(ups)[0], ref_aggregate()[1]
+    agg_same = all(torch.equal(mine[k], want[k]) for k in want)
     return {"metric": "SLQChannel on a CPU ResNet-18-sized state dict (256 weights + 256 biases), host to host",
             "unit": "ms", "ours_encode_ms": round(best(o, 0), 3), "ours_decode_ms": round(best(o, 1), 3),
             "reference_encode_ms": round(best(r, 0), 3), "reference_decode_ms": round(best(r, 1), 3),
             "ours_GiB_s": round(gib / ((best(o, 0) + best(o, 1)) * 1e-3), 2),
             "reference_GiB_s": round(gib / ((best(r, 0) + best(r, 1)) * 1e-3), 2),
-            "reference_threads": torch.get_num_threads(), "identical_output": same}
+            "reference_threads": torch.get_num_threads(), "identical_output": same,
+            "aggregate_k4": {"ours_receive_mean_ms": round(om * 1e3, 3),
+                             "reference_decode_simple_aggregate_ms": round(rm * 1e3, 3),
+                             "identical_output": agg_same}}
 
 
 def _ref_stoch_cpu(codec, x, bits=8):
