@@ -1031,6 +1031,37 @@ __device__ __forceinline__ float decode_fast(uint32_t l, uint32_t sgn, float nor
   return cnat_value(l, sgn, norm);
 }
 
+// Four decoded values from one dword of levels and one of signs. The fast division path falls back to the
+// exact one for the whole wave if any live lane's quotient is in doubt (every lane must call this).
+template <int KIND>
+__device__ __forceinline__ float4 decode4(uint32_t l, uint32_t g, float norm, float mn, const Div& d, float s,
+                                          bool live) {
+  bool bad = KIND != 2 && !d.fast;
+  float4 r;
+  r.x = decode_fast<KIND>(l & 0xffu, g & 0xffu, norm, mn, d, bad);
+  r.y = decode_fast<KIND>((l >> 8) & 0xffu, (g >> 8) & 0xffu, norm, mn, d, bad);
+  r.z = decode_fast<KIND>((l >> 16) & 0xffu, (g >> 16) & 0xffu, norm, mn, d, bad);
+  r.w = decode_fast<KIND>(l >> 24, g >> 24, norm, mn, d, bad);
+  if (KIND != 2 && wave_any(bad && live)) {
+    r.x = decode_exact<KIND>(l & 0xffu, g & 0xffu, norm, mn, s);
+    r.y = decode_exact<KIND>((l >> 8) & 0xffu, (g >> 8) & 0xffu, norm, mn, s);
+    r.z = decode_exact<KIND>((l >> 16) & 0xffu, (g >> 16) & 0xffu, norm, mn, s);
+    r.w = decode_exact<KIND>(l >> 24, g >> 24, norm, mn, s);
+  }
+  return r;
+}
+
+// Decode in wave tiles of 1024 elements, the SLQ decode's shape (slq_codec.hip dequantize_tile): lane l
+// loads 16 level bytes and 16 sign bytes (16-byte accesses, 1 KiB per wave-instruction per plane), a 1 KiB
+// per-wave LDS transpose per plane hands lane l dwords j*64+l (j = 0..3), and the four float4 results are
+// 16-byte stores contiguous across the wave. A wave issues all its tiles' loads (at most 2 per chunk)
+// before consuming the first. The < 16 elements before the first 16-element boundary and the < 1024 after
+// the last whole tile go per dword / per element. Measured on C2 (2^28 elements): 4-byte plane loads per
+// lane, the previous shape, decoded QSGD in 0.303 ms and CNAT in 0.325 ms (0.66 / 0.62 of 8 TB/s at 6 B
+// per element).
+constexpr int kDecTile = 1024;
+constexpr int kDecTilesPerWave = ADFL_SLQ_CHUNK_ELEMS / kDecTile / kWaves;
+
 template <int KIND>
 __global__ __launch_bounds__(kBlock) void k_stoch_dequantize(const uint8_t* __restrict__ levels,
                                                              const int8_t* __restrict__ signs,
@@ -1038,6 +1069,7 @@ __global__ __launch_bounds__(kBlock) void k_stoch_dequantize(const uint8_t* __re
                                                              const float* __restrict__ norms,
                                                              const float* __restrict__ mins, float s,
                                                              float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kWaves][2][kDecTile / 4];
   const adfl_slq_chunk c = chunks[blockIdx.x];
   const float norm = norms[c.tensor];
   const float mn = KIND == 1 ? mins[c.tensor] : 0.0f;
@@ -1047,43 +1079,54 @@ __global__ __launch_bounds__(kBlock) void k_stoch_dequantize(const uint8_t* __re
     return;
   }
   const Div d = make_div(s);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint8_t* lv = levels + c.start;
   const uint8_t* sg = reinterpret_cast<const uint8_t*>(signs) + c.start;
-  const int head = chunk_head4(c.start, c.len);
-  const int n4 = (c.len - head) >> 2;
-  const uint32_t* l4 = reinterpret_cast<const uint32_t*>(lv + head);
-  const uint32_t* s4 = reinterpret_cast<const uint32_t*>(sg + head);
-  float4* o4 = reinterpret_cast<float4*>(oc + head);
-  uint32_t lw[kPer], gw[kPer];
+  const int h16 = (int)((16 - (c.start & 15)) & 15);
+  const int head = h16 < c.len ? h16 : c.len;
+  const int ntiles = (c.len - head) / kDecTile;
+  uint4 L[kDecTilesPerWave], G[kDecTilesPerWave];
 #pragma unroll
-  for (int j = 0; j < kPer; ++j) {
-    const int k = threadIdx.x + j * kBlock;
-    if (k < n4) {
-      lw[j] = l4[k];
-      gw[j] = s4[k];
+  for (int u = 0; u < kDecTilesPerWave; ++u) {
+    const int t = wave + u * kWaves;
+    if (t < ntiles) {
+      L[u] = reinterpret_cast<const uint4*>(lv + head + t * kDecTile)[lane];
+      G[u] = reinterpret_cast<const uint4*>(sg + head + t * kDecTile)[lane];
     }
   }
 #pragma unroll
-  for (int j = 0; j < kPer; ++j) {
-    const int k = threadIdx.x + j * kBlock;
-    if (j * kBlock >= n4) break;  // block-uniform
+  for (int u = 0; u < kDecTilesPerWave; ++u) {
+    const int t = wave + u * kWaves;
+    if (t >= ntiles) break;  // wave-uniform
+    reinterpret_cast<uint4*>(lds[wave][0])[lane] = L[u];
+    reinterpret_cast<uint4*>(lds[wave][1])[lane] = G[u];
+    __builtin_amdgcn_wave_barrier();
+    uint32_t lw[4], gw[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      lw[j] = lds[wave][0][j * 64 + lane];
+      gw[j] = lds[wave][1][j * 64 + lane];
+    }
+    __builtin_amdgcn_wave_barrier();
+    float4* o4 = reinterpret_cast<float4*>(oc + head + t * kDecTile);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) store4_nt(o4 + j * 64 + lane, decode4<KIND>(lw[j], gw[j], norm, mn, d, s, true));
+  }
+  // after the last whole tile: < 1024 elements, one dword of each plane per thread
+  const int rs = head + ntiles * kDecTile;
+  const int n4 = (c.len - rs) >> 2;
+  if (n4 > 0) {  // block-uniform
+    const int k = threadIdx.x;
     const bool live = k < n4;
-    const uint32_t l = lw[j], g = gw[j];
-    bool bad = KIND != 2 && !d.fast;
-    float4 r;
-    r.x = decode_fast<KIND>(l & 0xffu, g & 0xffu, norm, mn, d, bad);
-    r.y = decode_fast<KIND>((l >> 8) & 0xffu, (g >> 8) & 0xffu, norm, mn, d, bad);
-    r.z = decode_fast<KIND>((l >> 16) & 0xffu, (g >> 16) & 0xffu, norm, mn, d, bad);
-    r.w = decode_fast<KIND>(l >> 24, g >> 24, norm, mn, d, bad);
-    if (KIND != 2 && wave_any(bad && live)) {  // whole wave exact, as in quantize_regs
-      r.x = decode_exact<KIND>(l & 0xffu, g & 0xffu, norm, mn, s);
-      r.y = decode_exact<KIND>((l >> 8) & 0xffu, (g >> 8) & 0xffu, norm, mn, s);
-      r.z = decode_exact<KIND>((l >> 16) & 0xffu, (g >> 16) & 0xffu, norm, mn, s);
-      r.w = decode_exact<KIND>(l >> 24, g >> 24, norm, mn, s);
+    uint32_t l = 0u, g = 0u;
+    if (live) {
+      l = reinterpret_cast<const uint32_t*>(lv + rs)[k];
+      g = reinterpret_cast<const uint32_t*>(sg + rs)[k];
     }
-    if (live) store4_nt(o4 + k, r);
+    const float4 r = decode4<KIND>(l, g, norm, mn, d, s, live);
+    if (live) store4_nt(reinterpret_cast<float4*>(oc + rs) + k, r);
   }
-  const int i = edge_elem(head, head + (n4 << 2), c.len);
+  const int i = edge_elem(head, rs + (n4 << 2), c.len);
   if (i >= 0) oc[i] = decode_exact<KIND>(lv[i], sg[i], norm, mn, s);
 }
 
