@@ -1085,21 +1085,21 @@ __global__ __launch_bounds__(kBlock) void k_stoch_dequantize(const uint8_t* __re
   const int h16 = (int)((16 - (c.start & 15)) & 15);
   const int head = h16 < c.len ? h16 : c.len;
   const int ntiles = (c.len - head) / kDecTile;
-  uint4 L[kDecTilesPerWave], G[kDecTilesPerWave];
-#pragma unroll
-  for (int u = 0; u < kDecTilesPerWave; ++u) {
-    const int t = wave + u * kWaves;
-    if (t < ntiles) {
-      L[u] = reinterpret_cast<const uint4*>(lv + head + t * kDecTile)[lane];
-      G[u] = reinterpret_cast<const uint4*>(sg + head + t * kDecTile)[lane];
-    }
+  // two tiles per wave at most (named registers: an indexed array here was promoted to LDS by the compiler)
+  static_assert(kDecTilesPerWave == 2, "k_stoch_dequantize: one chunk is two tiles per wave");
+  const int t0 = wave, t1 = wave + kWaves;
+  uint4 L0, G0, L1, G1;
+  if (t0 < ntiles) {
+    L0 = reinterpret_cast<const uint4*>(lv + head + t0 * kDecTile)[lane];
+    G0 = reinterpret_cast<const uint4*>(sg + head + t0 * kDecTile)[lane];
   }
-#pragma unroll
-  for (int u = 0; u < kDecTilesPerWave; ++u) {
-    const int t = wave + u * kWaves;
-    if (t >= ntiles) break;  // wave-uniform
-    reinterpret_cast<uint4*>(lds[wave][0])[lane] = L[u];
-    reinterpret_cast<uint4*>(lds[wave][1])[lane] = G[u];
+  if (t1 < ntiles) {
+    L1 = reinterpret_cast<const uint4*>(lv + head + t1 * kDecTile)[lane];
+    G1 = reinterpret_cast<const uint4*>(sg + head + t1 * kDecTile)[lane];
+  }
+  auto tile = [&](int t, const uint4& L, const uint4& G) {
+    reinterpret_cast<uint4*>(lds[wave][0])[lane] = L;
+    reinterpret_cast<uint4*>(lds[wave][1])[lane] = G;
     __builtin_amdgcn_wave_barrier();
     uint32_t lw[4], gw[4];
 #pragma unroll
@@ -1111,7 +1111,9 @@ __global__ __launch_bounds__(kBlock) void k_stoch_dequantize(const uint8_t* __re
     float4* o4 = reinterpret_cast<float4*>(oc + head + t * kDecTile);
 #pragma unroll
     for (int j = 0; j < 4; ++j) store4_nt(o4 + j * 64 + lane, decode4<KIND>(lw[j], gw[j], norm, mn, d, s, true));
-  }
+  };
+  if (t0 < ntiles) tile(t0, L0, G0);  // wave-uniform
+  if (t1 < ntiles) tile(t1, L1, G1);
   // after the last whole tile: < 1024 elements, one dword of each plane per thread
   const int rs = head + ntiles * kDecTile;
   const int n4 = (c.len - rs) >> 2;
