@@ -323,13 +323,15 @@ def _decode_add(c_params: QuantParameters, names: List[str], targets: List[Param
 
 def _stage_rows(clients: List[List[torch.Tensor]], lay: ops.BucketLayout, st: _DeviceStaging,
                 key: str) -> torch.Tensor:
-    """K clients' payload byte tensors (client k's tensor j at lay.offsets[j]) -> device rows
-    [K, pad16(lay.total)] uint8. All on the CPU: one native gather per client into its pinned row, that
-    row's H2D enqueued as soon as it is staged (the copy engine overlaps the next client's gather)."""
+    """K clients' payload tensors of one byte per element (int8 / uint8 / qint8; client k's tensor j at
+    lay.offsets[j]) -> device rows [K, pad16(lay.total)] uint8. All on the CPU: one native gather per
+    client into its pinned row, that row's H2D enqueued as soon as it is staged (the copy engine overlaps
+    the next client's gather)."""
     k = len(clients)
     row = (lay.total + 15) // 16 * 16
     dev = st.buf(key, k * row, torch.uint8).view(k, row)
-    if all(not t.is_cuda and t.is_contiguous() for c in clients for t in c):
+    if all(not t.is_cuda and t.is_contiguous() and t.element_size() == 1 for c in clients for t in c):
+        # byte copies from the tensors' storages: qint8 payloads need no int8 view object here
         host = st.buf(key + "_host", k * row, torch.uint8, pinned=True).view(k, row)
         for r, c in enumerate(clients):
             hostcopy.copy_pieces(*_range_copies(_ptrs(c), lay, host[r].data_ptr(), 1, 0, lay.total, to_bucket=True))
@@ -337,16 +339,23 @@ def _stage_rows(clients: List[List[torch.Tensor]], lay: ops.BucketLayout, st: _D
     else:  # device (or mixed) payloads: per-tensor copies into the device rows
         for r, c in enumerate(clients):
             for t, off, n in zip(c, lay.offsets.tolist(), lay.sizes.tolist()):
-                dev[r, off:off + n].copy_(t.reshape(-1).to(st.device))
+                dev[r, off:off + n].copy_(_byte_view(t).reshape(-1).to(st.device))
     return dev
+
+
+def _byte_view(t: torch.Tensor) -> torch.Tensor:
+    """The bytes of an int8 / uint8 / qint8 tensor as a uint8 tensor over the same storage."""
+    if t.is_quantized:
+        t = _int8_view(t)
+    return t if t.dtype == torch.uint8 else t.view(torch.uint8)
 
 
 @_serialized
 def _decode_mean(clients: List[List[torch.Tensor]], scales: List[List[float]], shapes: List[torch.Size],
                  packed: bool) -> List[torch.Tensor]:
     """The fp32 mean over K clients of their decoded tensors, tensor by tensor, in client order, in ONE
-    launch (ops.dequantize_mean_batched): clients[k][j] is client k's payload bytes for tensor j (a qint8
-    tensor's int8 view, or ceil(n/2) packed bytes with packed=True), scales[k][j] its scale. Returns one
+    launch (ops.dequantize_mean_batched): clients[k][j] is client k's payload for tensor j (a qint8 tensor,
+    or ceil(n/2) packed int8 bytes with packed=True), scales[k][j] its scale. Returns one
     owned tensor per entry (CPU when every client's payload is on the CPU)."""
     st = _staging()
     dev = st.device
@@ -356,7 +365,7 @@ def _decode_mean(clients: List[List[torch.Tensor]], scales: List[List[float]], s
         b_lay = st.layout(tuple((n + 1) // 2 for n in sizes), align=1)
     else:
         lay = b_lay = st.layout(sizes, align=1)
-    rows = _stage_rows([[t.view(torch.uint8) for t in c] for c in clients], b_lay, st, "mq")
+    rows = _stage_rows(clients, b_lay, st, "mq")
     s_dev = torch.tensor(scales, dtype=torch.float32).to(dev, non_blocking=True)
     out_dev = ops.dequantize_mean_batched(rows if packed else rows.view(torch.int8), s_dev, lay,
                                           out=st.buf("m_out", lay.total, torch.float32), packed=packed)
@@ -368,6 +377,48 @@ def _simple_aggregate(values: List[torch.Tensor]) -> torch.Tensor:
     """One entry of simple_aggregate (Src/ADFL/model.py:221-234), as the reference computes it."""
     with torch.no_grad():
         return torch.sum(torch.stack(values, dim=0), dim=0) / len(values)
+
+
+_SUM_GRAIN = 32768  # torch's intra-op grain size: smaller reductions run on one thread
+
+
+def _aggregate_entries(names: List[str], parts: List[Parameters]) -> Dict[str, torch.Tensor]:
+    """simple_aggregate over the entries `names` of the K dicts `parts` (host tensors: biases, running
+    statistics, counters), with the per-entry call's values but not its per-entry dispatch cost (256
+    biases: about 3 ms of stack / sum / div). Entries of one dtype are concatenated and summed with K
+    elementwise adds from zero, then divided and split into owned tensors, where that provably equals each
+    entry's own torch.sum(torch.stack(...), 0): int64 (integer sums are exact in any order), and fp32 entries
+    below torch's grain size for K <= 4 (one thread, and torch's CPU sum over dim 0 adds up to 4 rows in row
+    order from zero at every column, vector body and scalar tail alike; from 5 rows it regroups the tail
+    columns, so there each entry is summed on its own). A single concatenated torch.sum is no substitute:
+    its order depends on the combined size (and [4, 17000] took 40 ms on 8 threads)."""
+    k = len(parts)
+    res: Dict[str, torch.Tensor] = {}
+    groups: Dict[torch.dtype, List[str]] = {}
+    for n in names:
+        vals = [p[n] for p in parts]
+        t0 = vals[0]
+        if not all(isinstance(v, torch.Tensor) and not v.is_cuda and v.is_contiguous() and v.dtype == t0.dtype
+                   and v.shape == t0.shape for v in vals):
+            continue
+        if t0.dtype == torch.int64 or (t0.dtype == torch.float32 and k <= 4 and t0.numel() < _SUM_GRAIN):
+            groups.setdefault(t0.dtype, []).append(n)
+    with torch.no_grad():
+        for ns in groups.values():
+            if len(ns) < 2:
+                continue
+            rows = [torch.cat([t if t.dim() == 1 else t.reshape(-1) for t in (p[n] for n in ns)]) for p in parts]
+            acc = torch.zeros_like(rows[0])
+            for r in rows:
+                acc = acc + r
+            agg = acc / k
+            for n, piece in zip(ns, torch.split(agg, [parts[0][n].numel() for n in ns])):
+                shape = parts[0][n].shape
+                res[n] = (piece if piece.shape == shape else piece.view(shape)).clone()
+    for n in names:
+        if n not in res:
+            res[n] = _simple_aggregate([p[n] for p in parts])
+    return res
 
 
 @_serialized
@@ -522,22 +573,34 @@ class SLQChannel(Channel):
             out.update(zip(fused, decoded))
         rest = [n for n in names if n not in out]
         if rest:
-            parts = [self._receive(QuantParameters({n: c.params[n] for n in rest}, 0))[0] for c in all_c_params]
-            for n in rest:
-                out[n] = _simple_aggregate([p[n] for p in parts])
+            # passthrough entries decode to their own payload tensor (quant.py:111-112): used as they are
+            # (the values _receive hands back, without its per-entry work); the rest through _receive
+            plain = [n for n in rest if all(self._passthrough(c.params[n]) for c in all_c_params)]
+            other = [n for n in rest if n not in set(plain)]
+            parts = []
+            for c in all_c_params:
+                part = {n: c.params[n].data for n in plain}
+                if other:
+                    part.update(self._receive(QuantParameters({n: c.params[n] for n in other}, 0))[0])
+                parts.append(part)
+            out.update(_aggregate_entries(rest, parts))
         return {n: out[n] for n in names}, time.perf_counter() - s_time
+
+    @staticmethod
+    def _passthrough(p: QuantParameter) -> bool:
+        """_receive hands this entry back as its own payload tensor (quant.py:111-112)."""
+        return isinstance(p.data, torch.Tensor) and p.data.ndim <= 1
 
     @staticmethod
     def _fusable(p: QuantParameter) -> bool:
         d = p.data
-        return (d.ndim > 1 and d.is_quantized and d.numel() > 0 and d.dtype == torch.qint8
+        return (d.dtype == torch.qint8 and d.ndim > 1 and d.numel() > 0
                 and d.qscheme() == torch.per_tensor_affine and d.q_zero_point() == 0)
 
     def _mean_payloads(self, all_c_params: List[QuantParameters], names: List[str]) -> List[torch.Tensor]:
         qs = [[c.params[n].data for n in names] for c in all_c_params]
         # q_scale() is a double; fbgemm's dequantize uses it as fp32 (quant.py:110)
-        return _decode_mean([[_int8_view(q) for q in c] for c in qs], [[q.q_scale() for q in c] for c in qs],
-                            [q.shape for q in qs[0]], packed=False)
+        return _decode_mean(qs, [[q.q_scale() for q in c] for c in qs], [q.shape for q in qs[0]], packed=False)
 
     def send_with_q_error(self, params: Parameters) -> Tuple[CompressedParameters, float, float, float]:
         """`on_client_send` fused with the worker's quantization-error metrics.
@@ -624,6 +687,9 @@ class PackedSLQChannel(SLQChannel):
 
     def _fusable(self, p: QuantParameter) -> bool:
         return self._is_packed(p) and p.data.numel() == (torch.Size(p.shape).numel() + 1) // 2
+
+    def _passthrough(self, p: QuantParameter) -> bool:
+        return isinstance(p.data, torch.Tensor) and p.data.ndim <= 1 and not self._is_packed(p)
 
     def _mean_payloads(self, all_c_params: List[QuantParameters], names: List[str]) -> List[torch.Tensor]:
         return _decode_mean([[c.params[n].data for n in names] for c in all_c_params],

@@ -125,17 +125,37 @@ def test_passthrough_only_dict_needs_no_device():
     assert dec["b"].data_ptr() == b.data_ptr()  # `q_param.data.data`: a new view of the same storage
 
 
-def test_receive_mean_passthrough_entries_are_simple_aggregate():
-    """receive_mean over updates with nothing quantized: simple_aggregate's own arithmetic on the host
+@pytest.mark.parametrize("k", [1, 2, 3, 4, 5, 8])
+def test_receive_mean_passthrough_entries_are_simple_aggregate(k):
+    """receive_mean over updates with nothing quantized: simple_aggregate's own values on the host
     (Src/ADFL/model.py:221-234: stack, sum over dim 0, / K; an int64 counter becomes fp32), key order of
-    the first update, no device."""
+    the first update, no device. The entries are summed batched (concatenated per dtype, K elementwise
+    adds from zero) where that equals the per-entry torch.sum — int64 always, fp32 for K <= 4 — and per
+    entry otherwise; every value, sign of zero included, must equal the per-entry call's."""
     ch = SLQChannel(8)
-    ups = [ch.on_client_send({"b": torch.randn(5) * (r + 1), "n": torch.tensor(3 + r)})[0] for r in range(6)]
+    g = torch.Generator().manual_seed(k)
+    ups = []
+    for r in range(k):
+        d = {f"b{i}": torch.randn(1 + (i * 37) % 300, generator=g) * 10.0 ** (i % 7 - 3) for i in range(40)}
+        d["zeros"] = torch.tensor([-0.0, 0.0, -0.0 if r % 2 else 0.0])
+        d["n"] = torch.tensor(3 + r)
+        d["big"] = torch.randn(40000, generator=g)    # above torch's grain size: always per entry
+        d["i64v"] = torch.arange(5, dtype=torch.int64) * (r + 1)
+        ups.append(ch.on_client_send(d)[0])
     got, t = ch.receive_mean(ups)
-    assert list(got) == ["b", "n"] and t >= 0
-    for name in ("b", "n"):
+    assert list(got) == list(ups[0].params) and t >= 0
+    for name in got:
         want = torch.sum(torch.stack([u.params[name].data for u in ups], dim=0), dim=0) / len(ups)
-        assert got[name].dtype == want.dtype and torch.equal(got[name], want)
+        assert got[name].dtype == want.dtype and got[name].shape == want.shape, name
+        assert torch.equal(got[name], want) and torch.equal(torch.signbit(got[name]), torch.signbit(want)), name
+    before = {n: v.clone() for n, v in got.items()}
+    got["b0"].add_(1.0)   # each entry owns its storage: writing one leaves the others as they were
+    assert all(torch.equal(got[n], before[n]) for n in got if n != "b0")
+    assert got["b0"].untyped_storage().nbytes() == got["b0"].numel() * 4
+
+
+def test_receive_mean_rejects_what_simple_aggregate_rejects():
+    ch = SLQChannel(8)
     with pytest.raises(AssertionError):
         ch.receive_mean([])
     with pytest.raises(AssertionError):
