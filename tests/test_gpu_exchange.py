@@ -127,3 +127,50 @@ def test_bucket_exchange_world1_over_rccl(rccl_world1, align):
     ex2 = PeerExchange(lay.total, device=DEV, layout=lay)
     x = torch.from_numpy(flat).to(DEV)
     assert torch.equal(ex2.exchange_mean(x), x)
+
+
+@pytest.mark.parametrize("case", ["flat_in_order", "flat_side_stream", "int4_chunks", "bucket", "bucket_int4"])
+def test_exchange_graph_replays_equal_eager(rccl_world1, case):
+    """PeerExchange.graph: the whole exchange (encode, RCCL all-gather, fused mean; the side-stream chunk
+    pipeline included) captured once as a HIP graph; every replay on new contents of x equals the eager
+    exchange and the oracle's decode (exact_self=False at world 1: the mean is the rank's own round trip)."""
+    from adfl_amd import ops
+    from adfl_amd.exchange import PeerExchange
+    lay = None
+    numel, bits, packed, chunks = {"flat_in_order": (1 << 20, 8, False, 1), "flat_side_stream": (1000003, 8, False, 3),
+                                   "int4_chunks": (1 << 21, 4, True, 4), "bucket": (None, 8, False, 1),
+                                   "bucket_int4": (None, 4, True, 1)}[case]
+    if numel is None:
+        lay = ops.BucketLayout([3, 8193, 45662, 17, 70001])
+        numel = lay.total
+    ex = PeerExchange(numel, bits=bits, packed=packed, chunks=chunks, device=DEV, exact_self=False, layout=lay)
+    x = torch.zeros(numel, device=DEV)
+    out = torch.empty(numel, device=DEV)
+    g = ex.graph(x, out)
+    for seed in (1, 2, 3):
+        xn = np.random.default_rng(seed).standard_normal(numel, dtype=np.float32) * np.float32(10.0 ** -seed)
+        if lay is not None:   # gaps stay zero, as the bucket's producer leaves them
+            mask = np.zeros(numel, bool)
+            for o, n in zip(lay.offsets.tolist(), lay.sizes.tolist()):
+                mask[o:o + n] = True
+            xn[~mask] = 0.0
+        x.copy_(torch.from_numpy(xn))
+        got = g.replay().cpu().numpy()
+        eager = ex.exchange_mean(torch.from_numpy(xn).to(DEV)).cpu().numpy()
+        assert np.array_equal(got.view(np.uint32), eager.view(np.uint32)), seed
+        if lay is None:
+            q, s = oracle.encode(xn, bits)
+            want = oracle.decode_int4(oracle.pack_int4(q), numel, s) if packed else oracle.decode(q, s)
+            assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), seed
+
+
+def test_exchange_graph_rejects_host_staging(rccl_world1):
+    """Rows staged through host memory over gloo cannot be captured: graph() refuses instead of capturing
+    a partial step."""
+    from adfl_amd.exchange import PeerExchange
+    gl = dist.new_group(backend="gloo")
+    ex = PeerExchange(4096, device=DEV, group=gl)
+    assert ex.host_staged
+    with pytest.raises(ValueError, match="RCCL"):
+        ex.graph(torch.zeros(4096, device=DEV), torch.empty(4096, device=DEV))
+    dist.destroy_process_group(gl)

@@ -208,15 +208,21 @@ def mode_exchange(args, world, rank, dev):
     x = torch.randn(n, device=dev, generator=g) * 1e-3
     out = torch.empty(n, device=dev)
 
-    def step(ev):
-        ex.exchange_mean(x, out)
+    if args.graph:   # the whole step captured once (PeerExchange.graph), replayed with one host call
+        gx = ex.graph(x, out)
+
+        def step(ev):
+            gx.replay()
+    else:
+        def step(ev):
+            ex.exchange_mean(x, out)
     elapsed, _ = timed(step, args.steps, args.warmup, world, 1)
     t = elapsed / args.steps
     moved = ex.bytes_per_rank * (world - 1)  # bytes each rank receives over xGMI
     what = (f"bucketed {args.layout} state dict, per-tensor scales, bits={bits}{' packed' if args.packed else ''}"
             if layout is not None else
             f"bits={bits}{' packed' if args.packed else ''}, chunks={args.chunks}"
-            f"{', side stream' if ex.side_stream else ', in order'}")
+            f"{', side stream' if ex.side_stream else ', in order'}") + (", HIP graph replay" if args.graph else "")
     return {"metric": f"peer exchange: SLQ encode + RCCL all-gather + fused decode-mean, {what}", "unit": "GiB/s",
             "value": round(world * n * 4 / GIB / t, 2), "n_gpus": world, "ms_per_step": round(t * 1e3, 4),
             "elements_per_rank": n, "bytes_per_rank_on_wire": ex.bytes_per_rank,
@@ -643,6 +649,7 @@ def mode_stoch(args, world, rank, dev):
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--serial", action="store_true", help="exchange: no side stream (quantize + all-gather in order)")
+    p.add_argument("--graph", action="store_true", help="exchange: time PeerExchange.graph replays")
     p.add_argument("--layout", choices=["flat", "c3_equal", "c3_loguniform"], default="flat",
                    help="exchange: one flat update per rank, or a C3 state dict with per-tensor scales")
     p.add_argument("--mode", choices=["c3", "c5_int4", "exchange", "pcie", "channel", "channel_stoch", "stoch"],
