@@ -23,6 +23,10 @@ same (and with injected uniforms the codec is bit-identical: tests/test_gpu_stoc
 
 Norms: L2 norms are the correctly rounded fp32 norm (fp64 accumulation of fp32 squares); torch's fp32
 accumulation is less accurate. There is no CPU fallback: without the HIP library these raise.
+
+fp16 / bf16 / fp64 tensors are encoded as the reference encodes them, in their own dtype's arithmetic (each
+op rounded to the dtype; uniforms on torch.rand's grid for the dtype): one bucket per dtype through the
+*_dt kernels (csrc/stoch_dtype.hip). Their payloads decode like fp32 ones (the reference decodes to fp32).
 """
 
 import time
@@ -39,9 +43,15 @@ from .quant import _PendingD2H, _hand_out, _serialized, _stage_in, _staging
 _CODECS = ("qsgd", "rqsgd", "cnat")
 
 
-def _require_fp32(name: str, t: torch.Tensor, cls: str) -> None:
-    if t.dtype != torch.float32:
-        raise ValueError(f"{cls}: '{name}' is {t.dtype}; the HIP stochastic codecs quantize fp32 tensors")
+def _require_codable(name: str, t: torch.Tensor, cls: str) -> None:
+    """fp32 / fp16 / bf16 / fp64 tensors are encoded (each in its own dtype's arithmetic, as the reference
+    computes them). Anything else fails as the reference's first op on it fails: torch.linalg.vector_norm
+    raises for integer and bool tensors (quant.py:226,367,512)."""
+    if t.dtype == torch.float32 or t.dtype in sops.DT_DTYPES:
+        return
+    if not (t.is_floating_point() or t.is_complex()):
+        torch.linalg.vector_norm(t.reshape(-1)[:0])   # raises the reference's RuntimeError
+    raise ValueError(f"{cls}: '{name}' is {t.dtype}; the HIP stochastic codecs take fp32 / fp16 / bf16 / fp64")
 
 
 def _owned(parts: List[torch.Tensor], shapes: List[torch.Size]) -> List[torch.Tensor]:
@@ -129,13 +139,53 @@ def _encode_stoch(params: Parameters, names: List[str], codec: str, bits: int, u
     return _payloads(names, datas, signs, nm, lay.ntensors, codec)
 
 
-def _payloads(names, datas, signs, nm, ntensors: int, codec: str):
+@_serialized
+def _encode_stoch_dt(params: Parameters, names: List[str], codec: str, bits: int, uniforms=None, seed=None):
+    """Encode the ndim > 1 tensors `names` (all of one dtype: fp16 / bf16 / fp64) in one bucketed pass, in
+    that dtype's arithmetic (adfl_stoch_encode_batched_dt). Same return as _encode_stoch; the norms are the
+    dtype's values as Python floats (norm.item() of the reference's 0-dim norm tensor)."""
+    st = _staging()
+    dev = st.device
+    tensors = [params[n] for n in names]
+    dtype = tensors[0].dtype
+    tag = str(dtype).replace("torch.", "")
+    lay = st.layout(tuple(int(t.numel()) for t in tensors))
+    x_dev = _stage_in(tensors, lay, st, "x_" + tag, dtype)
+    if seed is None:
+        seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+    ws = st.buf("stoch_ws", lay.nchunks * 16, torch.uint8)
+    u = uniforms if uniforms is not None and uniforms.dtype == dtype else None
+    lv, sg, norms, mins = sops.encode_batched_dt(codec, x_dev, lay, bits, uniforms=u, seed=seed, counter=0,
+                                                 levels=st.buf("s_levels", lay.total, torch.uint8).view(
+                                                     torch.int8 if codec == "cnat" else torch.uint8),
+                                                 signs=st.buf("s_signs", lay.total, torch.int8), ws=ws)
+    nm = torch.cat([norms, mins]) if mins is not None else norms
+    on_cpu = [not t.is_cuda for t in tensors]
+    shapes = [t.shape for t in tensors]
+    if any(on_cpu):
+        lv_h = st.buf("s_levels_host", lay.total, torch.uint8, pinned=True).view(lv.dtype)
+        sg_h = st.buf("s_signs_host", lay.total, torch.int8, pinned=True)
+        lv_h.copy_(lv, non_blocking=True)
+        sg_h.copy_(sg, non_blocking=True)
+    nm = nm.cpu().tolist()   # synchronises: the planes' D2H has landed too
+    sizes = lay.sizes.tolist()
+    split = lambda buf: [p[:n] for p, n in zip(torch.split(buf, lay.padded.tolist()), sizes)]  # noqa: E731
+    lv_parts = _owned_host(lv_h, lay.offsets, shapes) if any(on_cpu) else None
+    sg_parts = _owned_host(sg_h, lay.offsets, shapes) if any(on_cpu) else None
+    lv_dev = _owned(split(lv), shapes) if not all(on_cpu) else None
+    sg_dev = _owned(split(sg), shapes) if not all(on_cpu) else None
+    datas = [(lv_parts if cpu else lv_dev)[i] for i, cpu in enumerate(on_cpu)]
+    signs = [(sg_parts if cpu else sg_dev)[i] for i, cpu in enumerate(on_cpu)]
+    return _payloads(names, datas, signs, nm, lay.ntensors, codec, dtype)
+
+
+def _payloads(names, datas, signs, nm, ntensors: int, codec: str, dtype: torch.dtype = torch.float32):
     """{name: (data, signs, scale, scale_2)} as the reference's _quantize_tensor returns them."""
     out = {}
     for i, name in enumerate(names):
         data, norm = datas[i], nm[i]
-        if norm == 0.0:  # the reference's norm == 0 branch: uint8 zeros, tensor(0.) scale
-            scale = torch.tensor(0.0)
+        if norm == 0.0:  # the reference's norm == 0 branch: uint8 zeros, the 0-dim norm tensor as scale
+            scale = torch.tensor(0.0, dtype=dtype)
             data = data.view(torch.uint8)
             scale_2 = 0
         else:
@@ -233,17 +283,24 @@ class _StochChannel(Channel):
         """Biases and running metrics (ndim <= 1) are not quantized."""
         names = [name for name, p in params.items() if p.ndim > 1 and p.numel() > 0]
         for name in names:
-            _require_fp32(name, params[name], self.__class__.__name__)
-        encoded = (_encode_stoch(params, names, self.CODEC, bits, uniforms, seed, getattr(self, "torch_norm", False))
-                   if names else {})
+            _require_codable(name, params[name], self.__class__.__name__)
+        f32 = [n for n in names if params[n].dtype == torch.float32]
+        encoded = (_encode_stoch(params, f32, self.CODEC, bits, uniforms if uniforms is None or
+                                 uniforms.dtype == torch.float32 else None, seed,
+                                 getattr(self, "torch_norm", False)) if f32 else {})
+        for dtype in sops.DT_DTYPES:   # fp16 / bf16 / fp64: one bucket per dtype, in that dtype's arithmetic
+            group = [n for n in names if params[n].dtype == dtype]
+            if group:
+                encoded.update(_encode_stoch_dt(params, group, self.CODEC, bits, uniforms, seed))
         q_params = QuantParameters({}, 0)
         pass_signs = torch.zeros(1, dtype=torch.uint8)  # passthrough entries' unused signs, one per call
         for name, param in params.items():
             if name in encoded:
                 data, signs, scale, scale_2 = encoded[name]
             elif param.ndim > 1:  # empty: vector_norm is 0 -> zero branch
+                _require_codable(name, param, self.__class__.__name__)
                 data = torch.zeros_like(param, dtype=torch.uint8)
-                signs, scale, scale_2 = torch.ones_like(param, dtype=torch.int8), torch.tensor(0.0), 0
+                signs, scale, scale_2 = torch.ones_like(param, dtype=torch.int8), torch.tensor(0.0, dtype=param.dtype), 0
             else:
                 data, signs, scale, scale_2 = param, pass_signs, 0, 0
             q_params.params[name] = QuantParameter(data=data, bits=bits, scale=scale, signs=signs, shape=param.shape,

@@ -81,6 +81,10 @@ SIGNATURES = {
     "adfl_rqsgd_encode_batched_work": (INT, [P, P, I64, P, I64, INT, P, U64, U64, P, I64, P, P, P, P, P]),
     "adfl_cnat_encode_batched_work": (INT, [P, P, I64, P, I64, INT, P, U64, U64, P, I64, P, P, P, P]),
     "adfl_philox_uniforms": (INT, [P, I64, I64, U64, U64, P]),
+    "adfl_stoch_norms_batched_dt": (INT, [I32, P, P, I64, INT, P, I64, P, P, P]),
+    "adfl_stoch_quantize_batched_dt": (INT, [I32, I32, P, P, I64, INT, P, P, U64, U64, P, P, P]),
+    "adfl_stoch_encode_batched_dt": (INT, [I32, I32, P, P, I64, INT, P, U64, U64, P, I64, P, P, P, P, P]),
+    "adfl_philox_uniforms_dt": (INT, [I32, P, I64, I64, U64, U64, P]),
     # adfl_host.h
     "adfl_host_copy": (INT, [P, P, P, I64, I32]),
     "adfl_host_copy_ex": (INT, [P, P, P, I64, I32, I32]),
@@ -88,6 +92,8 @@ SIGNATURES = {
 }
 
 NORM_L2, NORM_LINF, NORM_L2_TORCH = 0, 1, 2  # ADFL_NORM_*
+CODEC_QSGD, CODEC_RQSGD, CODEC_CNAT = 0, 1, 2  # ADFL_CODEC_*
+DTYPE_F32, DTYPE_F16, DTYPE_BF16, DTYPE_F64 = 0, 1, 2, 3  # ADFL_DTYPE_*
 
 _lib = None
 

@@ -22,12 +22,14 @@ from typing import Optional, Tuple
 import torch
 
 from . import _lib
-from ._lib import NORM_L2, NORM_L2_TORCH, NORM_LINF, check
+from ._lib import (CODEC_CNAT, CODEC_QSGD, CODEC_RQSGD, DTYPE_BF16, DTYPE_F16, DTYPE_F64, NORM_L2, NORM_L2_TORCH,
+                   NORM_LINF, check)
 from .ops import BucketLayout, _dev, _stream
 
 __all__ = ["RngStream", "norms_batched", "qsgd_quantize_batched", "qsgd_encode_batched", "rqsgd_encode_batched",
            "qsgd_decode_batched", "rqsgd_decode_batched", "cnat_encode_batched", "cnat_decode_batched",
-           "philox_uniforms", "workspace", "NORM_L2", "NORM_LINF", "NORM_L2_TORCH"]
+           "philox_uniforms", "workspace", "NORM_L2", "NORM_LINF", "NORM_L2_TORCH", "DT_DTYPES", "encode_batched_dt",
+           "quantize_batched_dt", "norms_batched_dt", "philox_uniforms_dt"]
 
 
 class RngStream:
@@ -233,4 +235,96 @@ def philox_uniforms(n: int, seed: int, counter: int, start: int = 0, *, device=N
     dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
     out = torch.empty(n, dtype=torch.float32, device=dev)
     check(_lib.load().adfl_philox_uniforms(out.data_ptr(), n, start, seed & (2 ** 64 - 1), counter, _stream(dev)))
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
+# fp16 / bf16 / fp64 buckets (include/adfl_stoch.h *_dt): the reference's arithmetic in the tensor's dtype
+# ------------------------------------------------------------------------------------------------
+DT_DTYPES = {torch.float16: DTYPE_F16, torch.bfloat16: DTYPE_BF16, torch.float64: DTYPE_F64}
+_CODEC_IDS = {"qsgd": CODEC_QSGD, "rqsgd": CODEC_RQSGD, "cnat": CODEC_CNAT}
+
+
+def _check_flat_dt(flat: torch.Tensor, layout: BucketLayout) -> Tuple[torch.Tensor, int]:
+    if flat.dtype not in DT_DTYPES:
+        raise ValueError(f"adfl_amd.stoch: the *_dt codecs take fp16 / bf16 / fp64 buckets, got {flat.dtype}")
+    flat = _dev(flat, "flat")
+    if flat.numel() < layout.total:
+        raise ValueError("adfl_amd.stoch: flat buffer smaller than the layout")
+    return flat, DT_DTYPES[flat.dtype]
+
+
+def _uniforms_dt(u: Optional[torch.Tensor], layout: BucketLayout, dtype: torch.dtype) -> int:
+    if u is None:
+        return 0
+    if u.dtype != dtype or u.numel() < layout.total:
+        raise ValueError(f"adfl_amd.stoch: uniforms must be a {dtype} plane covering the layout")
+    if not u.is_cuda or not u.is_contiguous() or u.data_ptr() % 16:
+        raise ValueError("adfl_amd.stoch: uniforms must be a contiguous, 16-byte aligned device tensor")
+    return u.data_ptr()
+
+
+def norms_batched_dt(flat: torch.Tensor, layout: BucketLayout, mode: int = NORM_L2, *,
+                     ws: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """Per-tensor norms of an fp16 / bf16 / fp64 bucket as fp64 values of the dtype's norm: L2 (fp16 / bf16:
+    fp32 squares summed in fp64, rounded to fp32, sqrt, rounded to the dtype; fp64: fp64 sum) or
+    (max|x|, min|x|) with mode NORM_LINF."""
+    flat, dt = _check_flat_dt(flat, layout)
+    dev = flat.device
+    norms = torch.empty(layout.ntensors, dtype=torch.float64, device=dev)
+    mins = torch.empty(layout.ntensors, dtype=torch.float64, device=dev) if mode == NORM_LINF else None
+    ws = _ws(ws, layout, dev)
+    check(_lib.load().adfl_stoch_norms_batched_dt(dt, flat.data_ptr(), layout.device_chunks(dev).data_ptr(),
+                                                  layout.nchunks, mode, ws.data_ptr(), ws.numel(), norms.data_ptr(),
+                                                  mins.data_ptr() if mins is not None else None, _stream(dev)))
+    return norms, mins
+
+
+def quantize_batched_dt(codec: str, flat: torch.Tensor, layout: BucketLayout, bits: int, norms: torch.Tensor, *,
+                        uniforms: Optional[torch.Tensor] = None, seed: int = 0, counter: int = 0,
+                        levels: Optional[torch.Tensor] = None,
+                        signs: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Levels (QSGD / RQSGD; uint8) or exponents (CNAT; int8) + signs of an fp16 / bf16 / fp64 bucket from
+    given fp64 per-tensor norms (the parity tests inject the reference's)."""
+    flat, dt = _check_flat_dt(flat, layout)
+    dev = flat.device
+    levels, signs = _planes(layout, dev, levels, signs, torch.int8 if codec == "cnat" else torch.uint8)
+    norms = _dev(norms, "norms")
+    if norms.dtype != torch.float64 or norms.numel() < layout.ntensors:
+        raise ValueError("adfl_amd.stoch: norms must be fp64, one per tensor")
+    check(_lib.load().adfl_stoch_quantize_batched_dt(_CODEC_IDS[codec], dt, flat.data_ptr(),
+                                                     layout.device_chunks(dev).data_ptr(), layout.nchunks, bits,
+                                                     norms.data_ptr(), _uniforms_dt(uniforms, layout, flat.dtype),
+                                                     seed, counter, levels.data_ptr(), signs.data_ptr(), _stream(dev)))
+    return levels, signs
+
+
+def encode_batched_dt(codec: str, flat: torch.Tensor, layout: BucketLayout, bits: int, *,
+                      uniforms: Optional[torch.Tensor] = None, seed: int = 0, counter: int = 0,
+                      levels: Optional[torch.Tensor] = None, signs: Optional[torch.Tensor] = None,
+                      ws: Optional[torch.Tensor] = None):
+    """QSGD / RQSGD / CNAT encode of an fp16 / bf16 / fp64 bucket in the dtype's arithmetic
+    (quant.py:223-240, :364-382, :509-534): (levels, signs, norms f64, mins f64 or None)."""
+    flat, dt = _check_flat_dt(flat, layout)
+    dev = flat.device
+    levels, signs = _planes(layout, dev, levels, signs, torch.int8 if codec == "cnat" else torch.uint8)
+    norms = torch.empty(layout.ntensors, dtype=torch.float64, device=dev)
+    mins = torch.empty(layout.ntensors, dtype=torch.float64, device=dev) if codec == "rqsgd" else None
+    ws = _ws(ws, layout, dev)
+    check(_lib.load().adfl_stoch_encode_batched_dt(_CODEC_IDS[codec], dt, flat.data_ptr(),
+                                                   layout.device_chunks(dev).data_ptr(), layout.nchunks, bits,
+                                                   _uniforms_dt(uniforms, layout, flat.dtype), seed, counter,
+                                                   ws.data_ptr(), ws.numel(), levels.data_ptr(), signs.data_ptr(),
+                                                   norms.data_ptr(), mins.data_ptr() if mins is not None else None,
+                                                   _stream(dev)))
+    return levels, signs, norms, mins
+
+
+def philox_uniforms_dt(dtype: torch.dtype, n: int, seed: int, counter: int, start: int = 0, *,
+                       device=None) -> torch.Tensor:
+    """The uniforms (in `dtype`) elements start .. start+n-1 of stream (seed, counter) draw."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    out = torch.empty(n, dtype=dtype, device=dev)
+    check(_lib.load().adfl_philox_uniforms_dt(DT_DTYPES[dtype], out.data_ptr(), n, start, seed & (2 ** 64 - 1),
+                                              counter, _stream(dev)))
     return out

@@ -1,0 +1,454 @@
+// stoch_dtype.hip — the stochastic codecs (QSGD / RQSGD / CNAT) on fp16, bf16 and fp64 tensors, in the
+// tensor's own dtype as the reference computes them (Src/ADFL/Channel/quant.py:223-240, :364-382,
+// :509-534), and the C ABI of include/adfl_stoch.h's *_dt entries.
+//
+// The reference's ops on an fp16 / bf16 tensor each compute in fp32 and round the result to the dtype
+// once (torch's CPU kernels); on fp64 they are fp64 ops. Every step below does the same: arithmetic in
+// C = fp32 (fp64 for fp64), R() = round to the dtype after each op, in the reference's operation order:
+//   QSGD / RQSGD  scaled = R(R(s*|x|) / norm); l = floor(scaled); prob = R(scaled - l);
+//                 q = u8(l + (u < prob)); signs = i8(sign(x))
+//   CNAT          v = R(|x| + eps); f, c = floor / ceil of fl(log2 v) (the exact band rule of
+//                 cnat_log2_dt_table.h, from torch's own log2 in each dtype); prob = R(R(R(2^c) - |x|) / R(2^f));
+//                 e = (u < prob) ? f : c, clamped, min_exp where x == 0; i8(e)
+// Uniforms are on torch.rand's grid for the dtype (2^-11 fp16, 2^-8 bf16, 2^-53 fp64): injected (a plane of
+// the dtype, indexed like x) or drawn from the Philox4x32-7 stream (oracle/stoch_dt_oracle.py restates it).
+// Norms: fp16 / bf16 squares in fp32 accumulated in fp64, rounded once to fp32, correctly rounded sqrt,
+// rounded to the dtype; fp64 squares accumulated in fp64. Returned as fp64 (exactly the dtype's value).
+// Decode is the fp32 codecs' (the reference decodes to fp32 with scale = fp32(norm)).
+//
+// These tensors are rare in ADFL (models train in fp32), so the kernels are plain: one 256-thread block per
+// chunk, each thread four consecutive elements per step (one Philox block for fp16 / bf16, two for fp64).
+
+#include <hip/hip_fp16.h>
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "adfl_stoch.h"
+#include "cnat_log2_dt_table.h"
+#include "philox.h"
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / 64;
+
+// ------------------------------------------------------------------------------------------------
+// dtypes: storage S, compute C, rounding R, uniform from Philox words, CNAT's band rule
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ float rn_bf16(float v) {
+  const uint32_t b = __float_as_uint(v);
+  if ((b & 0x7fffffffu) > 0x7f800000u) return __uint_as_float((b | 0x00400000u) & 0xffff0000u);  // NaN
+  return __uint_as_float((b + 0x7fffu + ((b >> 16) & 1u)) & 0xffff0000u);
+}
+
+struct DtF16 {
+  using S = uint16_t;
+  using C = float;
+  static constexpr int kMBits = 10, kBias = 15, kKMin = kCnatF16KMin;
+  static constexpr float kEps = 0x1p-10f;
+  __device__ static float load(S s) { return __half2float(__ushort_as_half(s)); }
+  __device__ static float rn(float v) { return __half2float(__float2half_rn(v)); }
+  __device__ static uint32_t bits(float v_on_grid) { return __half_as_ushort(__float2half_rn(v_on_grid)); }
+  __device__ static float uniform(uint32_t w) { return (float)(w >> 21) * 0x1p-11f; }
+  __device__ static uint32_t below(int k) { return kCnatF16Below[k - kKMin]; }
+  __device__ static uint32_t above(int k) { return kCnatF16Above[k - kKMin]; }
+};
+
+struct DtBF16 {
+  using S = uint16_t;
+  using C = float;
+  static constexpr int kMBits = 7, kBias = 127, kKMin = kCnatBF16KMin;
+  static constexpr float kEps = 0x1p-7f;
+  __device__ static float load(S s) { return __uint_as_float((uint32_t)s << 16); }
+  __device__ static float rn(float v) { return rn_bf16(v); }
+  __device__ static uint32_t bits(float v_on_grid) { return __float_as_uint(v_on_grid) >> 16; }
+  __device__ static float uniform(uint32_t w) { return (float)(w >> 24) * 0x1p-8f; }
+  __device__ static uint32_t below(int k) { return kCnatBF16Below[k - kKMin]; }
+  __device__ static uint32_t above(int k) { return kCnatBF16Above[k - kKMin]; }
+};
+
+struct DtF64 {
+  using S = double;
+  using C = double;
+  static constexpr int kMBits = 52, kBias = 1023, kKMin = kCnatF64KMin;
+  static constexpr double kEps = 0x1p-52;
+  __device__ static double load(S s) { return s; }
+  __device__ static double rn(double v) { return v; }
+  __device__ static uint64_t bits(double v) { return (uint64_t)__double_as_longlong(v); }
+  __device__ static uint64_t below(int k) { return kCnatF64Below[k - kKMin]; }
+  __device__ static uint64_t above(int k) { return kCnatF64Above[k - kKMin]; }
+};
+
+// torch's fp -> uint8 / int8 conversion on x86: truncate to int32 (NaN / out of range -> INT32_MIN, low
+// byte 0), keep the low byte.
+template <typename C>
+__device__ __forceinline__ uint32_t low_byte(C v) {
+  if (!(v > (C)-2147483648.0 && v < (C)2147483648.0)) return 0u;
+  return (uint32_t)(int)v & 0xffu;
+}
+
+template <typename C>
+__device__ __forceinline__ uint32_t sign_byte(C x) {
+  return (uint32_t)((x > (C)0) - (x < (C)0)) & 0xffu;
+}
+
+// The four uniforms of elements g0 .. g0+3 (g0 % 4 == 0) of the stream.
+template <typename T>
+__device__ __forceinline__ void stream4(uint64_t seed, uint64_t counter, int64_t g0, typename T::C (&u)[4]) {
+  if constexpr (sizeof(typename T::S) == 8) {   // fp64: two Philox blocks, 64 bits per element
+    const uint4 a = adfl::philox4x32(counter + (uint64_t)(g0 >> 1), seed);
+    const uint4 b = adfl::philox4x32(counter + (uint64_t)(g0 >> 1) + 1, seed);
+    const uint64_t w[4] = {((uint64_t)a.x << 32) | a.y, ((uint64_t)a.z << 32) | a.w, ((uint64_t)b.x << 32) | b.y,
+                           ((uint64_t)b.z << 32) | b.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) u[j] = (double)(w[j] >> 11) * 0x1p-53;
+  } else {
+    const uint4 a = adfl::philox4x32(counter + (uint64_t)(g0 >> 2), seed);
+    u[0] = T::uniform(a.x);
+    u[1] = T::uniform(a.y);
+    u[2] = T::uniform(a.z);
+    u[3] = T::uniform(a.w);
+  }
+}
+
+// CNAT's floor / ceil of fl(log2 v) for v = R(|x| + eps) (>= eps: normal), by the band rule.
+template <typename T>
+__device__ __forceinline__ void cnat_bounds(typename T::C v, typename T::C& f, typename T::C& c) {
+  using C = typename T::C;
+  if (!(v == v)) {
+    f = c = v;  // NaN
+    return;
+  }
+  if (__builtin_isinf(v)) {
+    f = c = v;  // +inf: log2 inf = inf
+    return;
+  }
+  const auto b = T::bits(v);
+  using B = decltype(b);
+  const B one = (B)1 << T::kMBits;  // 2^mantissa bits: ulps per binade
+  const int e = (int)(b >> T::kMBits) - T::kBias;
+  const B m = b & (one - 1);
+  int lo = e, hi = e + 1;
+  if (m <= T::above(e)) {
+    hi = e;
+  } else if (one - m <= T::below(e + 1)) {
+    lo = e + 1;
+  }
+  f = (C)lo;
+  c = (C)hi;
+}
+
+template <typename C>
+__device__ __forceinline__ C pow2(C k) {  // 2^k for integral k (inf past the range)
+  if constexpr (sizeof(C) == 4) {
+    return ldexpf(1.0f, (int)fmaxf(fminf(k, 300.0f), -300.0f));
+  } else {
+    return ldexp(1.0, (int)fmax(fmin(k, 3000.0), -3000.0));
+  }
+}
+
+// One element. KIND: 0 QSGD / 1 RQSGD (levels), 2 CNAT (exponents).
+template <typename T, int KIND>
+__device__ __forceinline__ void encode_elem(typename T::C x, typename T::C u, typename T::C norm, int bits,
+                                            uint8_t* __restrict__ lv, int8_t* __restrict__ sg) {
+  using C = typename T::C;
+  const C xa = __builtin_fabs(x);
+  *sg = (int8_t)sign_byte(x);
+  if constexpr (KIND != 2) {
+    const C s = (C)((1 << bits) - 1);
+    const C a = T::rn(s * xa);
+    const C scaled = T::rn(a / norm);
+    const C l = sizeof(C) == 4 ? (C)floorf((float)scaled) : (C)floor((double)scaled);
+    const C prob = T::rn(scaled - l);
+    const C lev = l + (u < prob ? (C)1 : (C)0);
+    *lv = (uint8_t)low_byte(lev);
+  } else {
+    const C min_e = (C)(-(1 << (bits - 1))), max_e = (C)((1 << (bits - 1)) - 1);
+    C r;
+    if (x == (C)0) {
+      r = min_e;
+    } else {
+      const C v = T::rn(xa + (C)T::kEps);
+      C f, c;
+      cnat_bounds<T>(v, f, c);
+      const C prob = T::rn(T::rn(T::rn(pow2(c)) - xa) / T::rn(pow2(f)));
+      r = u < prob ? f : c;
+      if (r == r) r = r < min_e ? min_e : (r > max_e ? max_e : r);  // clamp_ keeps NaN
+    }
+    *lv = (uint8_t)low_byte(r);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// kernels
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ double block_sum(double v) {
+  __shared__ double red[kWaves];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  v = (red[0] + red[1]) + (red[2] + red[3]);
+  __syncthreads();
+  return v;
+}
+
+__device__ __forceinline__ double block_max(double v) {
+  __shared__ double red[kWaves];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  v = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+  __syncthreads();
+  return v;
+}
+
+__device__ __forceinline__ double block_min(double v) {
+  __shared__ double red[kWaves];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  v = fmin(fmin(red[0], red[1]), fmin(red[2], red[3]));
+  __syncthreads();
+  return v;
+}
+
+// Chunk partials: L2 = fp64 sum of squares (fp16 / bf16: the fp32 square, exact); LINF = {max|x|, min|x|}
+// with NaN carried as a count.
+template <typename T, int MODE>
+__global__ __launch_bounds__(kBlock) void k_dt_norm_partials(const typename T::S* __restrict__ x,
+                                                             const adfl_slq_chunk* __restrict__ chunks,
+                                                             double* __restrict__ partials) {
+  using C = typename T::C;
+  const adfl_slq_chunk c = chunks[blockIdx.x];
+  const typename T::S* xc = x + c.start;
+  if (MODE == ADFL_NORM_L2) {
+    double acc = 0.0;
+    for (int i = threadIdx.x; i < c.len; i += kBlock) {
+      const C v = T::load(xc[i]);
+      acc += (double)(v * v);
+    }
+    acc = block_sum(acc);
+    if (threadIdx.x == 0) partials[2 * blockIdx.x] = acc;
+  } else {
+    double mx = 0.0, mn = __builtin_inf(), nan = 0.0;
+    for (int i = threadIdx.x; i < c.len; i += kBlock) {
+      const double a = fabs((double)T::load(xc[i]));
+      if (a != a) nan = 1.0;
+      mx = fmax(mx, a);
+      mn = fmin(mn, a);
+    }
+    mx = block_max(mx);
+    mn = block_min(mn);
+    nan = block_max(nan);
+    if (threadIdx.x == 0) {
+      partials[2 * blockIdx.x] = nan != 0.0 ? (double)NAN : mx;
+      partials[2 * blockIdx.x + 1] = nan != 0.0 ? (double)NAN : mn;
+    }
+  }
+}
+
+// Per tensor (one thread per chunk; the tensor's first chunk sums its partials in chunk order).
+template <typename T, int MODE>
+__global__ __launch_bounds__(kBlock) void k_dt_norm_finalize(const adfl_slq_chunk* __restrict__ chunks,
+                                                             int64_t nchunks, const double* __restrict__ partials,
+                                                             double* __restrict__ norms, double* __restrict__ mins) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= nchunks) return;
+  const adfl_slq_chunk c = chunks[i];
+  if (c.first_chunk != i) return;
+  if (MODE == ADFL_NORM_L2) {
+    double s = 0.0;
+    for (int k = 0; k < c.nchunks; ++k) s += partials[2 * (c.first_chunk + k)];
+    if constexpr (sizeof(typename T::C) == 4) {
+      const float n32 = __fsqrt_rn((float)s);  // fp32 sum, correctly rounded fp32 sqrt
+      norms[c.tensor] = (double)T::rn(n32);
+    } else {
+      norms[c.tensor] = sqrt(s);
+    }
+  } else {
+    double mx = 0.0, mn = __builtin_inf();
+    bool nan = false;
+    for (int k = 0; k < c.nchunks; ++k) {
+      const double a = partials[2 * (c.first_chunk + k)], b = partials[2 * (c.first_chunk + k) + 1];
+      nan |= (a != a);
+      mx = fmax(mx, a);
+      mn = fmin(mn, b);
+    }
+    norms[c.tensor] = nan ? (double)NAN : mx;
+    if (mins) mins[c.tensor] = nan ? (double)NAN : mn;
+  }
+}
+
+// Levels / exponents + signs from given per-tensor norms. Thread t takes the aligned 4-element groups
+// g0 = 4 * (floor(start / 4) + t + k * 256) of the chunk; elements of a group outside the chunk are skipped.
+template <typename T, int KIND>
+__global__ __launch_bounds__(kBlock) void k_dt_quantize(const typename T::S* __restrict__ x,
+                                                        const adfl_slq_chunk* __restrict__ chunks, int bits,
+                                                        const double* __restrict__ norms,
+                                                        const typename T::S* __restrict__ inj, uint64_t seed,
+                                                        uint64_t counter, uint8_t* __restrict__ levels,
+                                                        int8_t* __restrict__ signs) {
+  using C = typename T::C;
+  const adfl_slq_chunk c = chunks[blockIdx.x];
+  const C norm = (C)norms[c.tensor];
+  const int64_t end = c.start + c.len;
+  if (norm == (C)0) {  // quant.py:227-228 / :368-369 / :513-514: u8 zeros, int8 ones
+    for (int64_t g = c.start + threadIdx.x; g < end; g += kBlock) {
+      levels[g] = 0;
+      signs[g] = 1;
+    }
+    return;
+  }
+  for (int64_t g0 = (c.start & ~(int64_t)3) + 4 * (int64_t)threadIdx.x; g0 < end; g0 += 4 * kBlock) {
+    C u[4];
+    if (inj == nullptr) stream4<T>(seed, counter, g0, u);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t g = g0 + j;
+      if (g < c.start || g >= end) continue;
+      const C uj = inj ? T::load(inj[g]) : u[j];
+      encode_elem<T, KIND>(T::load(x[g]), uj, norm, bits, levels + g, signs + g);
+    }
+  }
+}
+
+// The stream's uniforms for elements start .. start+n-1, stored in the dtype (tests).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_dt_uniforms(typename T::S* __restrict__ out, int64_t n, int64_t start,
+                                                        uint64_t seed, uint64_t counter) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    const int64_t g = start + i;
+    typename T::C u[4];
+    stream4<T>(seed, counter, g & ~(int64_t)3, u);
+    const typename T::C v = u[g & 3];
+    if constexpr (sizeof(typename T::S) == 8) {
+      out[i] = v;
+    } else {
+      out[i] = (typename T::S)T::bits(v);
+    }
+  }
+}
+
+inline int launch_status() {
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+template <typename T>
+int norms_t(const void* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, int mode, void* d_ws, double* d_norms,
+            double* d_mins, hipStream_t st) {
+  const auto* x = static_cast<const typename T::S*>(d_x);
+  double* part = static_cast<double*>(d_ws);
+  const unsigned fin = (unsigned)((nchunks + kBlock - 1) / kBlock);
+  if (mode == ADFL_NORM_L2) {
+    hipLaunchKernelGGL((k_dt_norm_partials<T, ADFL_NORM_L2>), dim3((unsigned)nchunks), dim3(kBlock), 0, st, x, d_chunks,
+                       part);
+    hipLaunchKernelGGL((k_dt_norm_finalize<T, ADFL_NORM_L2>), dim3(fin), dim3(kBlock), 0, st, d_chunks, nchunks, part,
+                       d_norms, d_mins);
+  } else {
+    hipLaunchKernelGGL((k_dt_norm_partials<T, ADFL_NORM_LINF>), dim3((unsigned)nchunks), dim3(kBlock), 0, st, x,
+                       d_chunks, part);
+    hipLaunchKernelGGL((k_dt_norm_finalize<T, ADFL_NORM_LINF>), dim3(fin), dim3(kBlock), 0, st, d_chunks, nchunks,
+                       part, d_norms, d_mins);
+  }
+  return launch_status();
+}
+
+template <typename T>
+int quantize_t(int codec, const void* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, int bits,
+               const double* d_norms, const void* d_u, uint64_t seed, uint64_t counter, uint8_t* d_levels,
+               int8_t* d_signs, hipStream_t st) {
+  const auto* x = static_cast<const typename T::S*>(d_x);
+  const auto* inj = static_cast<const typename T::S*>(d_u);
+  if (codec == ADFL_CODEC_CNAT) {
+    hipLaunchKernelGGL((k_dt_quantize<T, 2>), dim3((unsigned)nchunks), dim3(kBlock), 0, st, x, d_chunks, bits, d_norms,
+                       inj, seed, counter, d_levels, d_signs);
+  } else {
+    hipLaunchKernelGGL((k_dt_quantize<T, 0>), dim3((unsigned)nchunks), dim3(kBlock), 0, st, x, d_chunks, bits, d_norms,
+                       inj, seed, counter, d_levels, d_signs);
+  }
+  return launch_status();
+}
+
+int check_common(int32_t dtype, const void* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks) {
+  if (dtype != ADFL_DTYPE_F16 && dtype != ADFL_DTYPE_BF16 && dtype != ADFL_DTYPE_F64) return ADFL_E_ARG;
+  if (!d_x || !d_chunks || nchunks < 1 || nchunks > INT32_MAX) return ADFL_E_ARG;
+  if (!aligned16(d_x)) return ADFL_E_ALIGN;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int adfl_stoch_norms_batched_dt(int32_t dtype, const void* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks,
+                                int mode, void* d_workspace, int64_t workspace_bytes, double* d_norms, double* d_mins,
+                                void* stream) {
+  if (const int r = check_common(dtype, d_x, d_chunks, nchunks)) return r;
+  if (!d_norms || !d_workspace || workspace_bytes < adfl_stoch_workspace_bytes(nchunks)) return ADFL_E_ARG;
+  if (mode != ADFL_NORM_L2 && mode != ADFL_NORM_LINF) return ADFL_E_ARG;
+  if (!aligned16(d_workspace)) return ADFL_E_ALIGN;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == ADFL_DTYPE_F16) return norms_t<DtF16>(d_x, d_chunks, nchunks, mode, d_workspace, d_norms, d_mins, st);
+  if (dtype == ADFL_DTYPE_BF16) return norms_t<DtBF16>(d_x, d_chunks, nchunks, mode, d_workspace, d_norms, d_mins, st);
+  return norms_t<DtF64>(d_x, d_chunks, nchunks, mode, d_workspace, d_norms, d_mins, st);
+}
+
+int adfl_stoch_quantize_batched_dt(int32_t codec, int32_t dtype, const void* d_x, const adfl_slq_chunk* d_chunks,
+                                   int64_t nchunks, int bits, const double* d_norms, const void* d_uniforms,
+                                   uint64_t seed, uint64_t counter, uint8_t* d_levels, int8_t* d_signs,
+                                   void* stream) {
+  if (const int r = check_common(dtype, d_x, d_chunks, nchunks)) return r;
+  if (codec != ADFL_CODEC_QSGD && codec != ADFL_CODEC_RQSGD && codec != ADFL_CODEC_CNAT) return ADFL_E_ARG;
+  if (!d_norms || !d_levels || !d_signs || bits < 1 || bits > 16) return ADFL_E_ARG;
+  if (d_uniforms && !aligned16(d_uniforms)) return ADFL_E_ALIGN;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == ADFL_DTYPE_F16)
+    return quantize_t<DtF16>(codec, d_x, d_chunks, nchunks, bits, d_norms, d_uniforms, seed, counter, d_levels,
+                             d_signs, st);
+  if (dtype == ADFL_DTYPE_BF16)
+    return quantize_t<DtBF16>(codec, d_x, d_chunks, nchunks, bits, d_norms, d_uniforms, seed, counter, d_levels,
+                              d_signs, st);
+  return quantize_t<DtF64>(codec, d_x, d_chunks, nchunks, bits, d_norms, d_uniforms, seed, counter, d_levels, d_signs,
+                           st);
+}
+
+int adfl_stoch_encode_batched_dt(int32_t codec, int32_t dtype, const void* d_x, const adfl_slq_chunk* d_chunks,
+                                 int64_t nchunks, int bits, const void* d_uniforms, uint64_t seed, uint64_t counter,
+                                 void* d_workspace, int64_t workspace_bytes, uint8_t* d_levels, int8_t* d_signs,
+                                 double* d_norms, double* d_mins, void* stream) {
+  if (codec == ADFL_CODEC_RQSGD && !d_mins) return ADFL_E_ARG;
+  const int mode = codec == ADFL_CODEC_RQSGD ? ADFL_NORM_LINF : ADFL_NORM_L2;
+  if (const int r = adfl_stoch_norms_batched_dt(dtype, d_x, d_chunks, nchunks, mode, d_workspace, workspace_bytes,
+                                                d_norms, d_mins, stream))
+    return r;
+  return adfl_stoch_quantize_batched_dt(codec, dtype, d_x, d_chunks, nchunks, bits, d_norms, d_uniforms, seed, counter,
+                                        d_levels, d_signs, stream);
+}
+
+int adfl_philox_uniforms_dt(int32_t dtype, void* d_out, int64_t n, int64_t start, uint64_t seed, uint64_t counter,
+                            void* stream) {
+  if (dtype != ADFL_DTYPE_F16 && dtype != ADFL_DTYPE_BF16 && dtype != ADFL_DTYPE_F64) return ADFL_E_ARG;
+  if (!d_out || n < 1 || start < 0) return ADFL_E_ARG;
+  const unsigned grid = (unsigned)((n + kBlock - 1) / kBlock < 4096 ? (n + kBlock - 1) / kBlock : 4096);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == ADFL_DTYPE_F16)
+    hipLaunchKernelGGL(k_dt_uniforms<DtF16>, dim3(grid), dim3(kBlock), 0, st, static_cast<uint16_t*>(d_out), n, start,
+                       seed, counter);
+  else if (dtype == ADFL_DTYPE_BF16)
+    hipLaunchKernelGGL(k_dt_uniforms<DtBF16>, dim3(grid), dim3(kBlock), 0, st, static_cast<uint16_t*>(d_out), n, start,
+                       seed, counter);
+  else
+    hipLaunchKernelGGL(k_dt_uniforms<DtF64>, dim3(grid), dim3(kBlock), 0, st, static_cast<double*>(d_out), n, start,
+                       seed, counter);
+  return launch_status();
+}
+
+}  // extern "C"

@@ -37,6 +37,8 @@ extern "C" {
 #endif
 
 enum { ADFL_NORM_L2 = 0, ADFL_NORM_LINF = 1, ADFL_NORM_L2_TORCH = 2 };
+enum { ADFL_CODEC_QSGD = 0, ADFL_CODEC_RQSGD = 1, ADFL_CODEC_CNAT = 2 };
+enum { ADFL_DTYPE_F32 = 0, ADFL_DTYPE_F16 = 1, ADFL_DTYPE_BF16 = 2, ADFL_DTYPE_F64 = 3 };
 
 /* Device workspace bytes the encode / norm calls need for a table of nchunks chunks (16 B per chunk). */
 int64_t adfl_stoch_workspace_bytes(int64_t nchunks);
@@ -116,6 +118,35 @@ int adfl_cnat_encode_batched_work(const float* d_x, const adfl_slq_chunk* d_chun
 /* The Philox uniforms the codecs draw: d_out[i] = u(start + i) of stream (seed, counter), i < n.
  * (Exposed for tests and for callers that want the uniforms a call used.) */
 int adfl_philox_uniforms(float* d_out, int64_t n, int64_t start, uint64_t seed, uint64_t counter, void* stream);
+
+/* ---- fp16 / bf16 / fp64 tensors -------------------------------------------------------------------
+ * The reference computes QSGD / RQSGD / CNAT in the tensor's own dtype (quant.py:223-240, :364-382,
+ * :509-534): each op on fp16 / bf16 computes in fp32 and rounds to the dtype; fp64 ops are fp64. These
+ * entries do the same on a bucket of one dtype (d_x: uint16 bit patterns for fp16 / bf16, doubles for fp64;
+ * 16-byte aligned base). Uniforms are on torch.rand's grid for the dtype: d_uniforms (NULL or a plane of
+ * the dtype indexed like x) or the Philox4x32-7 stream — fp16 / bf16: element g takes word g % 4 of block
+ * (counter + g / 4), u = (word >> 21) * 2^-11 (fp16) or (word >> 24) * 2^-8 (bf16); fp64: element g takes
+ * words 2 (g % 2), 2 (g % 2) + 1 of block (counter + g / 2) as the high / low halves of 64 bits,
+ * u = (bits >> 11) * 2^-53 (advance counter by ceil(total / 4), fp64 ceil(total / 2), per call).
+ * Norms are fp64 values of the dtype's norm: fp16 / bf16 L2 = R(sqrt(fp32(sum of fp32 squares in fp64)));
+ * fp64 L2 = sqrt(fp64 sum); LINF = max|x| / min|x|. CNAT's floor / ceil(log2) is the exact band rule of
+ * cnat_log2_dt_table.h. Decode with the fp32 dequantize entries and fp32(norm) (the reference decodes to
+ * fp32 with the Python-float norm as an fp32 scalar). Workspace: adfl_stoch_workspace_bytes(nchunks). */
+int adfl_stoch_norms_batched_dt(int32_t dtype, const void* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks,
+                                int mode, void* d_workspace, int64_t workspace_bytes, double* d_norms, double* d_mins,
+                                void* stream);
+/* Levels (QSGD / RQSGD: codec's norm in d_norms) or CNAT exponents + signs; norm == 0 gives 0 / 1. */
+int adfl_stoch_quantize_batched_dt(int32_t codec, int32_t dtype, const void* d_x, const adfl_slq_chunk* d_chunks,
+                                   int64_t nchunks, int bits, const double* d_norms, const void* d_uniforms,
+                                   uint64_t seed, uint64_t counter, uint8_t* d_levels, int8_t* d_signs, void* stream);
+/* norms (L2; RQSGD: LINF with d_mins) + quantize. */
+int adfl_stoch_encode_batched_dt(int32_t codec, int32_t dtype, const void* d_x, const adfl_slq_chunk* d_chunks,
+                                 int64_t nchunks, int bits, const void* d_uniforms, uint64_t seed, uint64_t counter,
+                                 void* d_workspace, int64_t workspace_bytes, uint8_t* d_levels, int8_t* d_signs,
+                                 double* d_norms, double* d_mins, void* stream);
+/* The uniforms elements start .. start+n-1 draw from stream (seed, counter) in the dtype (tests). */
+int adfl_philox_uniforms_dt(int32_t dtype, void* d_out, int64_t n, int64_t start, uint64_t seed, uint64_t counter,
+                            void* stream);
 
 #ifdef __cplusplus
 }

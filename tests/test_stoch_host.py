@@ -90,9 +90,14 @@ def test_receive_asserts_quant_parameters():
     assert isinstance(QuantParameters({}, 0), QuantParameters)
 
 
-def test_non_fp32_is_rejected_loudly():
-    with pytest.raises(ValueError, match="fp32"):
-        QSGDChannel(8).on_client_send({"w": torch.ones(2, 2, dtype=torch.float64)})
+def test_integer_tensors_raise_the_reference_error():
+    """The reference's first op on an integer tensor, torch.linalg.vector_norm, raises (quant.py:226,367,512);
+    fp16 / bf16 / fp64 tensors are encoded in their own dtype (tests/test_gpu_stoch_dt.py)."""
+    for cls in (QSGDChannel, RQSGDChannel, CNATChannel):
+        with pytest.raises(RuntimeError, match="Expected a floating point or complex tensor as input. Got Long"):
+            cls(8).on_client_send({"w": torch.ones(2, 2, dtype=torch.int64)})
+        with pytest.raises(RuntimeError, match="Got Int"):
+            cls(8).on_client_send({"w": torch.ones(0, 2, dtype=torch.int32)})
 
 
 @pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU behaviour")
