@@ -272,13 +272,16 @@ class PeerExchange:
         x's contents at that time, with no Python and one launch call on the host: the C3 bucket at world 1
         measured 0.096 ms eager and 0.041 ms replayed (tools/exchange_graph_probe.py). Collective over the
         group: every rank must capture (and later replay) in the same order. RCCL (device-direct) groups
-        only; x and out stay bound to the graph."""
+        only; x and out stay bound to the graph. With a bucket layout, out's gaps between tensors are zeroed
+        here and never written again."""
         if self.device.type != "cuda" or self.host_staged:
             raise ValueError("PeerExchange.graph: needs device tensors over an RCCL group (host staging cannot "
                              "be captured)")
         if x.numel() != self.numel or x.dtype != torch.float32 or out.numel() != self.numel or \
                 out.dtype != torch.float32 or not x.is_contiguous() or not out.is_contiguous():
             raise ValueError("PeerExchange.graph: x and out must be contiguous fp32 tensors of numel elements")
+        if self.layout is not None:   # the mean never writes a bucket's gaps: zero them once, as mean(out=None) does
+            out.zero_()
         g = torch.cuda.CUDAGraph()
         cap = torch.cuda.Stream(self.device)
         cap.wait_stream(torch.cuda.current_stream(self.device))
