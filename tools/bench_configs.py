@@ -611,6 +611,30 @@ def mode_stoch(args, world, rank, dev):
                     "encode_frac_moved": round(moved / enc / 1e6 / HBM_PEAK_GBS, 3),
                     "decode_frac": round(6 * n / dec / 1e6 / HBM_PEAK_GBS, 3),
                     "round_trip_GiBs": round(4 * n / GIB / ((enc + dec) / 1e3), 1)}
+    # fp16 / bf16 / fp64 C3 buckets (the *_dt kernels: the reference's arithmetic in each dtype), encode only
+    # (decode is the fp32 kernels'); flushed
+    lay = ops.BucketLayout(workloads["c3_bucket"], align=1)
+    for dtype in (torch.float16, torch.bfloat16, torch.float64):
+        xd = (torch.randn(lay.total, device=dev) * 1e-3).to(dtype)
+        lvd = torch.empty(lay.total, dtype=torch.uint8, device=dev)
+        sgd = torch.empty(lay.total, dtype=torch.int8, device=dev)
+        wsd = stoch.workspace(lay, dev)
+        for codec in ("qsgd", "cnat"):
+            def step_dt(ev, codec=codec):
+                junk.amax()
+                if ev is not None:
+                    ev[0].record()
+                stoch.encode_batched_dt(codec, xd, lay, 8, seed=7, counter=0,
+                                        levels=lvd.view(torch.int8) if codec == "cnat" else lvd, signs=sgd, ws=wsd)
+                if ev is not None:
+                    ev[1].record()
+            _, evs = timed(step_dt, args.steps, args.warmup, world, 2)
+            enc = seg_ms(evs, 0, 1)
+            eb = (2 * xd.element_size() + 2) * lay.total   # x read twice (norm pass, quantize) + 2 planes
+            res[f"c3_bucket_{str(dtype).replace('torch.', '')}_{codec}_flushed"] = {
+                "encode_ms": round(enc, 4), "encode_GBs": round(eb / enc / 1e6, 1),
+                "encode_frac": round(eb / enc / 1e6 / HBM_PEAK_GBS, 3)}
+        del xd, lvd, sgd
     del junk
     # calibration on the same box: the SLQ flat round trip of bench.py's headline kernels
     from adfl_amd import _lib
