@@ -17,7 +17,8 @@
 // Decode is the fp32 codecs' (the reference decodes to fp32 with scale = fp32(norm)).
 //
 // These tensors are rare in ADFL (models train in fp32), so the kernels are plain: one 256-thread block per
-// chunk, each thread four consecutive elements per step (one Philox block for fp16 / bf16, two for fp64).
+// chunk, each thread one 16-byte vector of x per step (8 fp16 / bf16 or 2 fp64 elements; two Philox blocks
+// or one), scalar head / tail elements around the vectors.
 
 #include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
@@ -149,13 +150,13 @@ __device__ __forceinline__ C pow2(C k) {  // 2^k for integral k (inf past the ra
   }
 }
 
-// One element. KIND: 0 QSGD / 1 RQSGD (levels), 2 CNAT (exponents).
+// One element -> (level / exponent byte, sign byte). KIND: 0 QSGD / 1 RQSGD (levels), 2 CNAT (exponents).
 template <typename T, int KIND>
-__device__ __forceinline__ void encode_elem(typename T::C x, typename T::C u, typename T::C norm, int bits,
-                                            uint8_t* __restrict__ lv, int8_t* __restrict__ sg) {
+__device__ __forceinline__ uint32_t encode_elem(typename T::C x, typename T::C u, typename T::C norm, int bits,
+                                                uint32_t& sg) {
   using C = typename T::C;
   const C xa = __builtin_fabs(x);
-  *sg = (int8_t)sign_byte(x);
+  sg = sign_byte(x);
   if constexpr (KIND != 2) {
     const C s = (C)((1 << bits) - 1);
     const C a = T::rn(s * xa);
@@ -163,7 +164,7 @@ __device__ __forceinline__ void encode_elem(typename T::C x, typename T::C u, ty
     const C l = sizeof(C) == 4 ? (C)floorf((float)scaled) : (C)floor((double)scaled);
     const C prob = T::rn(scaled - l);
     const C lev = l + (u < prob ? (C)1 : (C)0);
-    *lv = (uint8_t)low_byte(lev);
+    return low_byte(lev);
   } else {
     const C min_e = (C)(-(1 << (bits - 1))), max_e = (C)((1 << (bits - 1)) - 1);
     C r;
@@ -177,8 +178,37 @@ __device__ __forceinline__ void encode_elem(typename T::C x, typename T::C u, ty
       r = u < prob ? f : c;
       if (r == r) r = r < min_e ? min_e : (r > max_e ? max_e : r);  // clamp_ keeps NaN
     }
-    *lv = (uint8_t)low_byte(r);
+    return low_byte(r);
   }
+}
+
+// 16-byte vectors: V elements (8 for fp16 / bf16, 2 for fp64). A chunk is split into a scalar head up to
+// the first V-element boundary, whole vectors, and a scalar tail.
+template <typename T>
+constexpr int kVec = 16 / (int)sizeof(typename T::S);
+
+struct Span {
+  int64_t b0, nv, b1, end;  // vectors cover [b0, b1), b1 = b0 + nv * V
+};
+
+template <typename T>
+__device__ __forceinline__ Span split_chunk(const adfl_slq_chunk& c) {
+  constexpr int V = kVec<T>;
+  Span sp;
+  sp.end = c.start + c.len;
+  const int64_t a0 = (c.start + V - 1) / V * V;
+  sp.b0 = a0 < sp.end ? a0 : sp.end;
+  sp.nv = (sp.end - sp.b0) / V;
+  sp.b1 = sp.b0 + sp.nv * V;
+  return sp;
+}
+
+// The uniform of element g alone (head / tail elements).
+template <typename T>
+__device__ __forceinline__ typename T::C stream1(uint64_t seed, uint64_t counter, int64_t g) {
+  typename T::C u[4];
+  stream4<T>(seed, counter, g & ~(int64_t)3, u);
+  return u[g & 3];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -223,25 +253,36 @@ template <typename T, int MODE>
 __global__ __launch_bounds__(kBlock) void k_dt_norm_partials(const typename T::S* __restrict__ x,
                                                              const adfl_slq_chunk* __restrict__ chunks,
                                                              double* __restrict__ partials) {
-  using C = typename T::C;
+  using S = typename T::S;
+  constexpr int V = kVec<T>;
   const adfl_slq_chunk c = chunks[blockIdx.x];
-  const typename T::S* xc = x + c.start;
-  if (MODE == ADFL_NORM_L2) {
-    double acc = 0.0;
-    for (int i = threadIdx.x; i < c.len; i += kBlock) {
-      const C v = T::load(xc[i]);
+  const Span sp = split_chunk<T>(c);
+  double acc = 0.0, mx = 0.0, mn = __builtin_inf(), nan = 0.0;
+  auto visit = [&](S raw) {
+    const typename T::C v = T::load(raw);
+    if (MODE == ADFL_NORM_L2) {
       acc += (double)(v * v);
-    }
-    acc = block_sum(acc);
-    if (threadIdx.x == 0) partials[2 * blockIdx.x] = acc;
-  } else {
-    double mx = 0.0, mn = __builtin_inf(), nan = 0.0;
-    for (int i = threadIdx.x; i < c.len; i += kBlock) {
-      const double a = fabs((double)T::load(xc[i]));
+    } else {
+      const double a = fabs((double)v);
       if (a != a) nan = 1.0;
       mx = fmax(mx, a);
       mn = fmin(mn, a);
     }
+  };
+  for (int64_t g = c.start + threadIdx.x; g < sp.b0; g += kBlock) visit(x[g]);
+  const uint4* xv = reinterpret_cast<const uint4*>(x + sp.b0);
+  for (int64_t i = threadIdx.x; i < sp.nv; i += kBlock) {
+    const uint4 w = xv[i];
+    S vals[V];
+    __builtin_memcpy(vals, &w, 16);
+#pragma unroll
+    for (int j = 0; j < V; ++j) visit(vals[j]);
+  }
+  for (int64_t g = sp.b1 + threadIdx.x; g < sp.end; g += kBlock) visit(x[g]);
+  if (MODE == ADFL_NORM_L2) {
+    acc = block_sum(acc);
+    if (threadIdx.x == 0) partials[2 * blockIdx.x] = acc;
+  } else {
     mx = block_max(mx);
     mn = block_min(mn);
     nan = block_max(nan);
@@ -284,8 +325,9 @@ __global__ __launch_bounds__(kBlock) void k_dt_norm_finalize(const adfl_slq_chun
   }
 }
 
-// Levels / exponents + signs from given per-tensor norms. Thread t takes the aligned 4-element groups
-// g0 = 4 * (floor(start / 4) + t + k * 256) of the chunk; elements of a group outside the chunk are skipped.
+// Levels / exponents + signs from given per-tensor norms. Whole 16-byte vectors of x (V elements) per thread
+// step, their V level bytes and V sign bytes stored together (8 B for fp16 / bf16, 2 B for fp64); the
+// uniforms of a vector are one (fp64) or two (fp16 / bf16) Philox blocks. Head / tail elements one by one.
 template <typename T, int KIND>
 __global__ __launch_bounds__(kBlock) void k_dt_quantize(const typename T::S* __restrict__ x,
                                                         const adfl_slq_chunk* __restrict__ chunks, int bits,
@@ -294,27 +336,66 @@ __global__ __launch_bounds__(kBlock) void k_dt_quantize(const typename T::S* __r
                                                         uint64_t counter, uint8_t* __restrict__ levels,
                                                         int8_t* __restrict__ signs) {
   using C = typename T::C;
+  using S = typename T::S;
+  constexpr int V = kVec<T>;
   const adfl_slq_chunk c = chunks[blockIdx.x];
   const C norm = (C)norms[c.tensor];
-  const int64_t end = c.start + c.len;
+  const Span sp = split_chunk<T>(c);
   if (norm == (C)0) {  // quant.py:227-228 / :368-369 / :513-514: u8 zeros, int8 ones
-    for (int64_t g = c.start + threadIdx.x; g < end; g += kBlock) {
+    for (int64_t g = c.start + threadIdx.x; g < sp.end; g += kBlock) {
       levels[g] = 0;
       signs[g] = 1;
     }
     return;
   }
-  for (int64_t g0 = (c.start & ~(int64_t)3) + 4 * (int64_t)threadIdx.x; g0 < end; g0 += 4 * kBlock) {
-    C u[4];
-    if (inj == nullptr) stream4<T>(seed, counter, g0, u);
+  auto one = [&](int64_t g) {
+    const C u = inj ? T::load(inj[g]) : stream1<T>(seed, counter, g);
+    uint32_t sg;
+    levels[g] = (uint8_t)encode_elem<T, KIND>(T::load(x[g]), u, norm, bits, sg);
+    signs[g] = (int8_t)sg;
+  };
+  for (int64_t g = c.start + threadIdx.x; g < sp.b0; g += kBlock) one(g);
+  const uint4* xv = reinterpret_cast<const uint4*>(x + sp.b0);
+  for (int64_t i = threadIdx.x; i < sp.nv; i += kBlock) {
+    const int64_t g0 = sp.b0 + i * V;
+    const uint4 w = xv[i];
+    S vals[V];
+    __builtin_memcpy(vals, &w, 16);
+    C u[V];
+    if (inj) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t g = g0 + j;
-      if (g < c.start || g >= end) continue;
-      const C uj = inj ? T::load(inj[g]) : u[j];
-      encode_elem<T, KIND>(T::load(x[g]), uj, norm, bits, levels + g, signs + g);
+      for (int j = 0; j < V; ++j) u[j] = T::load(inj[g0 + j]);
+    } else if constexpr (V == 8) {
+      C a[4], b2[4];
+      stream4<T>(seed, counter, g0, a);
+      stream4<T>(seed, counter, g0 + 4, b2);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        u[j] = a[j];
+        u[4 + j] = b2[j];
+      }
+    } else {  // V == 2 (fp64): elements g0, g0 + 1 are words (x, y) and (z, w) of block counter + g0 / 2
+      const uint4 q = adfl::philox4x32(counter + (uint64_t)(g0 >> 1), seed);
+      u[0] = (double)((((uint64_t)q.x << 32) | q.y) >> 11) * 0x1p-53;
+      u[1] = (double)((((uint64_t)q.z << 32) | q.w) >> 11) * 0x1p-53;
+    }
+    uint64_t lw = 0, sw = 0;
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      uint32_t sg;
+      const uint32_t lb = encode_elem<T, KIND>(T::load(vals[j]), u[j], norm, bits, sg);
+      lw |= (uint64_t)lb << (8 * j);
+      sw |= (uint64_t)sg << (8 * j);
+    }
+    if constexpr (V == 8) {
+      *reinterpret_cast<uint64_t*>(levels + g0) = lw;
+      *reinterpret_cast<uint64_t*>(signs + g0) = sw;
+    } else {
+      *reinterpret_cast<uint16_t*>(levels + g0) = (uint16_t)lw;
+      *reinterpret_cast<uint16_t*>(signs + g0) = (uint16_t)sw;
     }
   }
+  for (int64_t g = sp.b1 + threadIdx.x; g < sp.end; g += kBlock) one(g);
 }
 
 // The stream's uniforms for elements start .. start+n-1, stored in the dtype (tests).
@@ -408,7 +489,7 @@ int adfl_stoch_quantize_batched_dt(int32_t codec, int32_t dtype, const void* d_x
   if (const int r = check_common(dtype, d_x, d_chunks, nchunks)) return r;
   if (codec != ADFL_CODEC_QSGD && codec != ADFL_CODEC_RQSGD && codec != ADFL_CODEC_CNAT) return ADFL_E_ARG;
   if (!d_norms || !d_levels || !d_signs || bits < 1 || bits > 16) return ADFL_E_ARG;
-  if (d_uniforms && !aligned16(d_uniforms)) return ADFL_E_ALIGN;
+  if ((d_uniforms && !aligned16(d_uniforms)) || !aligned16(d_levels) || !aligned16(d_signs)) return ADFL_E_ALIGN;
   hipStream_t st = (hipStream_t)stream;
   if (dtype == ADFL_DTYPE_F16)
     return quantize_t<DtF16>(codec, d_x, d_chunks, nchunks, bits, d_norms, d_uniforms, seed, counter, d_levels,

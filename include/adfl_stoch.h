@@ -123,8 +123,9 @@ int adfl_philox_uniforms(float* d_out, int64_t n, int64_t start, uint64_t seed, 
  * The reference computes QSGD / RQSGD / CNAT in the tensor's own dtype (quant.py:223-240, :364-382,
  * :509-534): each op on fp16 / bf16 computes in fp32 and rounds to the dtype; fp64 ops are fp64. These
  * entries do the same on a bucket of one dtype (d_x: uint16 bit patterns for fp16 / bf16, doubles for fp64;
- * 16-byte aligned base). Uniforms are on torch.rand's grid for the dtype: d_uniforms (NULL or a plane of
- * the dtype indexed like x) or the Philox4x32-7 stream — fp16 / bf16: element g takes word g % 4 of block
+ * 16-byte aligned bases, the level / sign planes too). Uniforms are on torch.rand's grid for the dtype:
+ * d_uniforms (NULL or a plane of the dtype indexed like x) or the Philox4x32-7 stream — fp16 / bf16:
+ * element g takes word g % 4 of block
  * (counter + g / 4), u = (word >> 21) * 2^-11 (fp16) or (word >> 24) * 2^-8 (bf16); fp64: element g takes
  * words 2 (g % 2), 2 (g % 2) + 1 of block (counter + g / 2) as the high / low halves of 64 bits,
  * u = (bits >> 11) * 2^-53 (advance counter by ceil(total / 4), fp64 ceil(total / 2), per call).
