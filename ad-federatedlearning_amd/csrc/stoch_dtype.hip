@@ -293,35 +293,42 @@ __global__ __launch_bounds__(kBlock) void k_dt_norm_partials(const typename T::S
   }
 }
 
-// Per tensor (one thread per chunk; the tensor's first chunk sums its partials in chunk order).
+// Per tensor: one block per chunk, and the block of a tensor's first chunk reduces that tensor's partials
+// (its 256 threads strided over the chunks, then a fixed tree: deterministic). A 1 GiB fp16 tensor has
+// 65,536 chunks: one thread summing them in order would be a chain of dependent loads.
 template <typename T, int MODE>
 __global__ __launch_bounds__(kBlock) void k_dt_norm_finalize(const adfl_slq_chunk* __restrict__ chunks,
-                                                             int64_t nchunks, const double* __restrict__ partials,
+                                                             const double* __restrict__ partials,
                                                              double* __restrict__ norms, double* __restrict__ mins) {
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= nchunks) return;
-  const adfl_slq_chunk c = chunks[i];
-  if (c.first_chunk != i) return;
+  const adfl_slq_chunk c = chunks[blockIdx.x];
+  if (c.first_chunk != (int32_t)blockIdx.x) return;  // block-uniform
   if (MODE == ADFL_NORM_L2) {
     double s = 0.0;
-    for (int k = 0; k < c.nchunks; ++k) s += partials[2 * (c.first_chunk + k)];
-    if constexpr (sizeof(typename T::C) == 4) {
-      const float n32 = __fsqrt_rn((float)s);  // fp32 sum, correctly rounded fp32 sqrt
-      norms[c.tensor] = (double)T::rn(n32);
-    } else {
-      norms[c.tensor] = sqrt(s);
+    for (int k = threadIdx.x; k < c.nchunks; k += kBlock) s += partials[2 * (c.first_chunk + k)];
+    s = block_sum(s);
+    if (threadIdx.x == 0) {
+      if constexpr (sizeof(typename T::C) == 4) {
+        const float n32 = __fsqrt_rn((float)s);  // fp32 sum, correctly rounded fp32 sqrt
+        norms[c.tensor] = (double)T::rn(n32);
+      } else {
+        norms[c.tensor] = sqrt(s);
+      }
     }
   } else {
-    double mx = 0.0, mn = __builtin_inf();
-    bool nan = false;
-    for (int k = 0; k < c.nchunks; ++k) {
+    double mx = 0.0, mn = __builtin_inf(), nan = 0.0;
+    for (int k = threadIdx.x; k < c.nchunks; k += kBlock) {
       const double a = partials[2 * (c.first_chunk + k)], b = partials[2 * (c.first_chunk + k) + 1];
-      nan |= (a != a);
+      if (a != a) nan = 1.0;
       mx = fmax(mx, a);
       mn = fmin(mn, b);
     }
-    norms[c.tensor] = nan ? (double)NAN : mx;
-    if (mins) mins[c.tensor] = nan ? (double)NAN : mn;
+    mx = block_max(mx);
+    mn = block_min(mn);
+    nan = block_max(nan);
+    if (threadIdx.x == 0) {
+      norms[c.tensor] = nan != 0.0 ? (double)NAN : mx;
+      if (mins) mins[c.tensor] = nan != 0.0 ? (double)NAN : mn;
+    }
   }
 }
 
@@ -427,17 +434,15 @@ int norms_t(const void* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, in
             double* d_mins, hipStream_t st) {
   const auto* x = static_cast<const typename T::S*>(d_x);
   double* part = static_cast<double*>(d_ws);
-  const unsigned fin = (unsigned)((nchunks + kBlock - 1) / kBlock);
+  const dim3 grid((unsigned)nchunks);
   if (mode == ADFL_NORM_L2) {
-    hipLaunchKernelGGL((k_dt_norm_partials<T, ADFL_NORM_L2>), dim3((unsigned)nchunks), dim3(kBlock), 0, st, x, d_chunks,
-                       part);
-    hipLaunchKernelGGL((k_dt_norm_finalize<T, ADFL_NORM_L2>), dim3(fin), dim3(kBlock), 0, st, d_chunks, nchunks, part,
-                       d_norms, d_mins);
+    hipLaunchKernelGGL((k_dt_norm_partials<T, ADFL_NORM_L2>), grid, dim3(kBlock), 0, st, x, d_chunks, part);
+    hipLaunchKernelGGL((k_dt_norm_finalize<T, ADFL_NORM_L2>), grid, dim3(kBlock), 0, st, d_chunks, part, d_norms,
+                       d_mins);
   } else {
-    hipLaunchKernelGGL((k_dt_norm_partials<T, ADFL_NORM_LINF>), dim3((unsigned)nchunks), dim3(kBlock), 0, st, x,
-                       d_chunks, part);
-    hipLaunchKernelGGL((k_dt_norm_finalize<T, ADFL_NORM_LINF>), dim3(fin), dim3(kBlock), 0, st, d_chunks, nchunks,
-                       part, d_norms, d_mins);
+    hipLaunchKernelGGL((k_dt_norm_partials<T, ADFL_NORM_LINF>), grid, dim3(kBlock), 0, st, x, d_chunks, part);
+    hipLaunchKernelGGL((k_dt_norm_finalize<T, ADFL_NORM_LINF>), grid, dim3(kBlock), 0, st, d_chunks, part, d_norms,
+                       d_mins);
   }
   return launch_status();
 }

@@ -169,3 +169,26 @@ def test_channel_mixed_dtype_dict(codec):
         np.testing.assert_array_equal(p.signs.numpy().reshape(-1), so_, err_msg=name)
         want = do.decode(codec, qo, so_, 8, norm, p.scale_2 if codec == "rqsgd" else 0.0)
         assert same_f32(dec[name].numpy().reshape(-1), want.reshape(-1)), name
+
+
+@pytest.mark.parametrize("dtname,n", [("float16", 1 << 24), ("bfloat16", (1 << 23) + 5), ("float64", (1 << 22) + 3)])
+def test_large_tensor_multichunk_norm_and_bytes(dtname, n):
+    """One large tensor (thousands of chunks: the per-tensor norm is reduced by a block over its chunk
+    partials): the norm equals the oracle's (fp64 within a few ulps) and every byte equals the oracle on the
+    kernel's norm with the same Philox stream."""
+    dt = DT[dtname]
+    g = torch.Generator().manual_seed(n)
+    xt = (torch.randn(n, generator=g, dtype=torch.float64) * 1e-2).to(TDT[dtname])
+    raw = xt.numpy() if dtname == "float64" else xt.view(torch.int16).numpy().view(np.uint16)
+    lay = ops.BucketLayout([n], align=1)
+    for codec in ("qsgd", "cnat"):
+        q, s, norms, _ = stoch.encode_batched_dt(codec, xt.to(DEV), lay, 8, seed=77, counter=0)
+        norm = float(norms.cpu()[0])
+        want = do.l2_norm(raw, dt)
+        if dt == do.DT_F64:
+            assert abs(norm - want) <= 64 * 2.0 ** -52 * want
+        else:
+            assert norm == want
+        qo, so_ = do.quantize(codec, raw, dt, 8, norm, do.philox_uniforms_dt(dt, n, 77, 0))
+        assert np.array_equal(q.cpu().numpy().view(np.uint8), qo.view(np.uint8)), codec
+        assert np.array_equal(s.cpu().numpy(), so_), codec
