@@ -116,6 +116,11 @@ def _worker(rank, world, port, cases, errors):
             ref = torch.stack([torch.from_numpy(d) for d in decoded]).mean(0).numpy()
             np.testing.assert_allclose(got, ref, rtol=1e-6, atol=1e-30)
             assert ex.bytes_per_rank == sum(ex.row_bytes)
+        try:   # host tensors cannot be captured into a HIP graph: refused, not half-captured
+            ex.graph(torch.zeros(ex.numel), torch.zeros(ex.numel))
+            raise AssertionError("PeerExchange.graph accepted host tensors")
+        except ValueError:
+            pass
         dist.destroy_process_group()
     except Exception as e:  # surfaced to the parent
         import traceback

@@ -183,6 +183,7 @@ int main(int argc, char** argv) {
   };
   std::vector<V> D = {
       {"d_fwd", [&] { hipLaunchKernelGGL((k_dequantize_flat<false, false>), dim3(tg), dim3(kBlock), 0, st, q, n, scale, out); }},
+      {"d_ldnt", [&] { hipLaunchKernelGGL((k_dequantize_flat<false, true>), dim3(tg), dim3(kBlock), 0, st, q, n, scale, out); }},
       {"d_pf1", [&] { hipLaunchKernelGGL((mb::k_deq_pf<1>), dim3(tg), dim3(kBlock), 0, st, q, n, scale, out); }},
       {"d_pf2", [&] { hipLaunchKernelGGL((mb::k_deq_pf<2>), dim3(tg), dim3(kBlock), 0, st, q, n, scale, out); }},
       {"d_pf2_g1024", [&] { hipLaunchKernelGGL((mb::k_deq_pf<2>), dim3(1024), dim3(kBlock), 0, st, q, n, scale, out); }},
