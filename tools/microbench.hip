@@ -38,6 +38,17 @@ __global__ __launch_bounds__(256) void k_write_nt(float4* __restrict__ out, int6
   const int64_t s = (int64_t)gridDim.x * 256;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += s) store4_nt(out + i, make_float4(1.f, 2.f, 3.f, 4.f));
 }
+// the decode's store shape without its loads: wave tiles of 4 float4 NT stores per lane (1 KiB per
+// wave-instruction), tile_grid blocks
+__global__ __launch_bounds__(256) void k_write_nt_tiles(float4* __restrict__ out, int64_t ntiles) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t wstride = (int64_t)gridDim.x * 4;
+  for (int64_t t = (int64_t)blockIdx.x * 4 + wave; t < ntiles; t += wstride) {
+    float4* o4 = out + t * 256;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) store4_nt(o4 + j * 64 + lane, make_float4(1.f, 2.f, 3.f, (float)j));
+  }
+}
 // quantize with the first tiles' loads issued before the partial reduction (hides its latency) and UT
 // tiles in flight per wave iteration.
 template <int UT, bool PREFETCH>
@@ -319,5 +330,7 @@ int main(int argc, char** argv) {
   ceil("read_f32", 4, [&] { hipLaunchKernelGGL(mb::k_read<false>, dim3(2048), dim3(256), 0, st, (const float4*)x, n >> 2, ws); });
   ceil("read_f32_nt", 4, [&] { hipLaunchKernelGGL(mb::k_read<true>, dim3(2048), dim3(256), 0, st, (const float4*)x, n >> 2, ws); });
   ceil("write_f32_nt", 4, [&] { hipLaunchKernelGGL(mb::k_write_nt, dim3(2048), dim3(256), 0, st, (float4*)tmp, n >> 2); });
+  ceil("write_f32_nt_tiles", 4, [&] { hipLaunchKernelGGL(mb::k_write_nt_tiles, dim3(tg), dim3(256), 0, st, (float4*)tmp, n / kTile); });
+  ceil("write_f32_nt_tiles_out", 4, [&] { hipLaunchKernelGGL(mb::k_write_nt_tiles, dim3(tg), dim3(256), 0, st, (float4*)out, n / kTile); });
   return 0;
 }
