@@ -292,15 +292,16 @@ class PeerExchange:
                 for s in (self.quant_stream, self.gather_stream):   # every forked stream rejoins the capture
                     cap.wait_stream(s)
         torch.cuda.current_stream(self.device).wait_stream(cap)
-        return ExchangeGraph(g, x, out)
+        return ExchangeGraph(g, x, out, self)
 
 
 class ExchangeGraph:
     """A captured PeerExchange step (PeerExchange.graph): replay() enqueues it on the current stream's
-    device; `x` is read and `out` written at replay time."""
+    device; `x` is read and `out` written at replay time. It keeps the exchange (whose message rows, staging
+    and streams the graph uses) alive as long as itself."""
 
-    def __init__(self, graph: "torch.cuda.CUDAGraph", x: torch.Tensor, out: torch.Tensor):
-        self.g, self.x, self.out = graph, x, out
+    def __init__(self, graph: "torch.cuda.CUDAGraph", x: torch.Tensor, out: torch.Tensor, exchange: "PeerExchange"):
+        self.g, self.x, self.out, self.exchange = graph, x, out, exchange
 
     def replay(self) -> torch.Tensor:
         self.g.replay()
