@@ -17,7 +17,9 @@ Also reported on the same line:
   (rank 0, N=1), over a bounded sample of the same workload;
 * exchange (N > 1, or --exchange on) — BASELINE configs[3] (C4) on the same buffers after the timed
   headline: encode + RCCL all-gather of the int8 payloads over xGMI + fused decode-mean, with the
-  all-gather's bus bandwidth. Never part of `value`.
+  all-gather's bus bandwidth; and `exchange_c3`, a ResNet-18-sized state dict per client exchanged as one
+  bucket with per-tensor scales. Both check the gathered rows and the mean across ranks. Never part of
+  `value`.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
@@ -538,6 +540,43 @@ def exchange_leg(x: torch.Tensor, out: torch.Tensor, bits: int, world: int, step
             "backend": dist.get_backend()}
 
 
+def exchange_bucket_leg(dev, bits: int, world: int, steps: int, warmup: int):
+    """BASELINE configs[2] exchanged as configs[3] does: every rank's ResNet-18-sized state dict
+    (11,689,512 fp32 in 256 equal tensors, one bucket, SLQChannel's per-tensor scales) encoded, all-gathered
+    over RCCL as one row (payload + 256 scales) and averaged per tensor in one launch (adfl_amd.exchange
+    with a BucketLayout; Examples/ray_ad.py:164-190). Checked like the C4 leg. Never part of `value`."""
+    import torch.distributed as dist
+    from adfl_amd import ops
+    from adfl_amd.exchange import PeerExchange
+
+    base, rem = divmod(11_689_512, 256)
+    lay = ops.BucketLayout([base + (1 if i < rem else 0) for i in range(256)])
+    rank = dist.get_rank()
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    flat = torch.zeros(lay.total, device=dev)
+    for o, n in zip(lay.offsets.tolist(), lay.sizes.tolist()):
+        flat[o:o + n] = torch.randn(n, device=dev, generator=g) * 1e-3
+    out = torch.empty(lay.total, device=dev)
+    ex = PeerExchange(lay.total, bits=bits, device=dev, layout=lay)
+    for _ in range(warmup):
+        ex.exchange_mean(flat, out)
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ex.exchange_mean(flat, out)
+    torch.cuda.synchronize()
+    barrier(world)
+    t = max_over_ranks(time.perf_counter() - t0, world) / steps
+    check = exchange_verify(ex, flat, world)
+    return {"workload": f"C3 state dict per client: {world} clients x 11,689,512 fp32 in 256 tensors, SLQ bits={bits} "
+                        f"per-tensor scales, RCCL all_gather_into_tensor of one bucket row + per-tensor fused mean",
+            "steps": steps, "parity": check.pop("parity"), "check": check, "ms_per_step": round(t * 1e3, 4),
+            "bytes_per_rank_on_wire": ex.bytes_per_rank,
+            "GiB_per_s": round(world * int(lay.sizes.sum()) * 4 / GIB / t, 2)}
+
+
 def plumbing_check(args):
     """--plumbing-check: the N-rank path of this script without a GPU (gloo): every rank joins, reports
     itself, spins for (rank + 1) * 50 ms between the two barriers, and rank 0 prints the max over ranks."""
@@ -633,6 +672,10 @@ def main():
             exchange = exchange_leg(x, out, args.bits, world, min(args.steps, 20), min(args.warmup, 3))
         except Exception as e:  # noqa: BLE001
             exchange = {"error": f"{type(e).__name__}: {e}"[:400]}
+        try:
+            exchange_c3 = exchange_bucket_leg(dev, args.bits, world, min(args.steps, 20), min(args.warmup, 3))
+        except Exception as e:  # noqa: BLE001
+            exchange_c3 = {"error": f"{type(e).__name__}: {e}"[:400]}
 
     per_kernel = {name: sum(e[i].elapsed_time(e[i + 1]) for e in events) / args.steps
                   for i, name in enumerate(("absmax", "quantize", "dequantize"))}
@@ -675,6 +718,7 @@ def main():
     }
     if exchange is not None:
         line["exchange"] = exchange
+        line["exchange_c3"] = exchange_c3
     if world == 1 and not args.no_cpu_baseline:
         cpu, parity = cpu_baseline(x, args.bits, args.cpu_seconds, q, scale)
         line["cpu_baseline"] = cpu

@@ -53,6 +53,10 @@ def test_bench_exchange_leg_checks_itself():
     assert "error" not in ex, ex
     assert ex["parity"] is True, ex
     assert ex["check"]["own_row_equal"] and ex["check"]["rows_checked"] == 1 and ex["backend"] == "nccl"
+    c3 = d["exchange_c3"]   # the ResNet-18-sized state dict exchanged as one bucket
+    assert "error" not in c3, c3
+    assert c3["parity"] is True and c3["check"]["rows_checked"] == 1, c3
+    assert c3["bytes_per_rank_on_wire"] > 11_689_512 and c3["GiB_per_s"] > 0
 
 
 def test_bench_two_ranks_share_one_gpu():
@@ -72,3 +76,6 @@ def test_bench_two_ranks_share_one_gpu():
     assert "error" not in ex, ex
     assert ex["parity"] is True and ex["backend"] == "gloo", ex
     assert ex["check"]["rows_checked"] == 2 and ex["check"]["mean_identical_on_all_ranks"]
+    c3 = d["exchange_c3"]
+    assert "error" not in c3, c3
+    assert c3["parity"] is True and c3["check"]["rows_checked"] == 2 and c3["check"]["mean_identical_on_all_ranks"]
