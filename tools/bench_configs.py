@@ -95,6 +95,11 @@ def c3_round_trip(lay, packed, args, world, rank, dev, lib, sh, junk, mode="auto
         _lib.check(dec_fn(q.data_ptr(), chunks.data_ptr(), lay.nchunks, scales.data_ptr(), out.data_ptr(), sh))
 
     res = {"encode": "resident" if nwork else "twopass", "encode_launches": 1 if nwork else 2}
+    resident = bool(lay.nwork if packed else nwork)
+    # bytes per element the kernels that ran must move: the one-launch encode reads x
+    # once (int8: 4 + 1, int4: 4 + 0.5), the two passes twice; decode 1 + 4 (int4: 0.5 + 4)
+    enc_moved = (4.5 if packed else 5.0) if resident else (8.5 if packed else 9.0)
+    dec_moved = 4.5 if packed else 5.0
     for flush in (False, True):
         def flush_cache():
             if flush:
@@ -127,6 +132,8 @@ def c3_round_trip(lay, packed, args, world, rank, dev, lib, sh, junk, mode="auto
         res["flushed" if flush else "cache_resident"] = {
             "round_trip_ms": round(rt, 4), "GiB_per_s": round(n * 4 / GIB / (rt * 1e-3), 1),
             "hbm_frac": round((13 if packed else 14) * n / (rt * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "hbm_frac_moved": round((enc_moved + dec_moved) * n / (rt * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "encode_frac_moved": round(enc_moved * n / (e * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "encode_ms": round(e, 4), "decode_ms": round(d, 4), "split_round_trip_ms": round(e + d, 4)}
     return res
 
