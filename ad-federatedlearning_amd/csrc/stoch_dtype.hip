@@ -478,8 +478,9 @@ int adfl_stoch_norms_batched_dt(int32_t dtype, const void* d_x, const adfl_slq_c
                                 int mode, void* d_workspace, int64_t workspace_bytes, double* d_norms, double* d_mins,
                                 void* stream) {
   if (const int r = check_common(dtype, d_x, d_chunks, nchunks)) return r;
-  if (!d_norms || !d_workspace || workspace_bytes < adfl_stoch_workspace_bytes(nchunks)) return ADFL_E_ARG;
+  if (!d_norms || !d_workspace) return ADFL_E_ARG;
   if (mode != ADFL_NORM_L2 && mode != ADFL_NORM_LINF) return ADFL_E_ARG;
+  if (workspace_bytes < adfl_stoch_workspace_bytes(nchunks)) return ADFL_E_WORKSPACE;
   if (!aligned16(d_workspace)) return ADFL_E_ALIGN;
   hipStream_t st = (hipStream_t)stream;
   if (dtype == ADFL_DTYPE_F16) return norms_t<DtF16>(d_x, d_chunks, nchunks, mode, d_workspace, d_norms, d_mins, st);
@@ -493,7 +494,8 @@ int adfl_stoch_quantize_batched_dt(int32_t codec, int32_t dtype, const void* d_x
                                    void* stream) {
   if (const int r = check_common(dtype, d_x, d_chunks, nchunks)) return r;
   if (codec != ADFL_CODEC_QSGD && codec != ADFL_CODEC_RQSGD && codec != ADFL_CODEC_CNAT) return ADFL_E_ARG;
-  if (!d_norms || !d_levels || !d_signs || bits < 1 || bits > 16) return ADFL_E_ARG;
+  if (bits < 1 || bits > 16) return ADFL_E_BITS;
+  if (!d_norms || !d_levels || !d_signs) return ADFL_E_ARG;
   if ((d_uniforms && !aligned16(d_uniforms)) || !aligned16(d_levels) || !aligned16(d_signs)) return ADFL_E_ALIGN;
   hipStream_t st = (hipStream_t)stream;
   if (dtype == ADFL_DTYPE_F16)

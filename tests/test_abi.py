@@ -106,6 +106,34 @@ def test_stochastic_argument_errors_return_codes_without_launching():
     assert lib.adfl_slq_dequantize_add_batched(20, 16, 1, 16, 16, 1, 1, None) == -3
 
 
+def test_dtype_and_bucket_mean_argument_errors_return_codes_without_launching():
+    """The fp16 / bf16 / fp64 stochastic entries and the bucketed peer means check their arguments before
+    any HIP call (so this runs without a GPU)."""
+    lib = _lib.load()
+    F16, F64, QSGD, CNAT = _lib.DTYPE_F16, _lib.DTYPE_F64, _lib.CODEC_QSGD, _lib.CODEC_CNAT
+    # dtype / codec / bits / planes / alignment
+    assert lib.adfl_stoch_quantize_batched_dt(QSGD, 0, 16, 16, 1, 8, 16, None, 0, 0, 16, 16, None) == -1   # fp32 here
+    assert lib.adfl_stoch_quantize_batched_dt(9, F16, 16, 16, 1, 8, 16, None, 0, 0, 16, 16, None) == -1
+    assert lib.adfl_stoch_quantize_batched_dt(QSGD, F16, 16, 16, 1, 0, 16, None, 0, 0, 16, 16, None) == -2
+    assert lib.adfl_stoch_quantize_batched_dt(QSGD, F16, 16, 16, 1, 8, None, None, 0, 0, 16, 16, None) == -1
+    assert lib.adfl_stoch_quantize_batched_dt(QSGD, F16, 20, 16, 1, 8, 16, None, 0, 0, 16, 16, None) == -3
+    assert lib.adfl_stoch_quantize_batched_dt(CNAT, F64, 16, 16, 1, 8, 16, 24, 0, 0, 16, 16, None) == -3
+    assert lib.adfl_stoch_quantize_batched_dt(CNAT, F64, 16, 16, 1, 8, 16, None, 0, 0, 16, 24, None) == -3
+    assert lib.adfl_stoch_norms_batched_dt(F16, 16, 16, 4, 0, 16, 63, 16, None, None) == -4      # workspace
+    assert lib.adfl_stoch_norms_batched_dt(F16, 16, 16, 1, 7, 16, 1 << 20, 16, None, None) == -1  # mode
+    assert lib.adfl_stoch_norms_batched_dt(F16, 16, 16, 0, 0, 16, 1 << 20, 16, None, None) == -1  # no chunks
+    assert lib.adfl_stoch_encode_batched_dt(_lib.CODEC_RQSGD, F16, 16, 16, 1, 8, None, 0, 0, 16, 1 << 20, 16, 16,
+                                            16, None, None) == -1                                   # RQSGD needs mins
+    assert lib.adfl_philox_uniforms_dt(7, 16, 10, 0, 1, 0, None) == -1
+    assert lib.adfl_philox_uniforms_dt(F16, 16, 0, 0, 1, 0, None) == -1
+    # bucketed peer means: row stride a 16-byte multiple, aligned rows / output, self row in range
+    assert lib.adfl_slq_dequantize_mean_batched(16, 24, 2, 16, 1, 16, 1, -1, None, 16, None) == -3
+    assert lib.adfl_slq_dequantize_mean_batched(16, 32, 2, 16, 1, 16, 1, 2, 16, 16, None) == -1
+    assert lib.adfl_slq_dequantize_mean_batched_int4(16, 32, 2, 16, 1, 16, 1, 0, None, 16, None) == -1
+    assert lib.adfl_slq_dequantize_mean_batched_int4(20, 32, 2, 16, 1, 16, 1, -1, None, 16, None) == -3
+    assert lib.adfl_slq_dequantize_mean_batched_int4(16, 32, 0, 16, 1, 16, 1, -1, None, 16, None) == -1
+
+
 def test_build_chunks_host_planning():
     lib = _lib.load()
     sizes = np.array([10, 8192, 8193, 64, 3 * 8192 + 5], np.int64)
