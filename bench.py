@@ -537,6 +537,9 @@ def exchange_leg(x: torch.Tensor, out: torch.Tensor, bits: int, world: int, step
             "encode_ms": round(seg[0], 4), "allgather_wait_ms": round(seg[1], 4), "mean_ms": round(seg[2], 4),
             "bytes_per_rank_on_wire": ex.bytes_per_rank,
             "allgather_busbw_GBs": round(recv / (seg[1] * 1e-3) / 1e9, 1) if world > 1 and seg[1] > 0 else None,
+            # rccl-tests convention: algbw = gathered bytes / time; busbw = algbw * (n - 1) / n
+            "allgather_algbw_GBs": (round(world * ex.bytes_per_rank / (seg[1] * 1e-3) / 1e9, 1)
+                                    if world > 1 and seg[1] > 0 else None),
             "backend": dist.get_backend()}
 
 
