@@ -555,9 +555,10 @@ class SLQChannel(Channel):
 
         Tensors quantized in every update are decoded and averaged on the device in one launch: the K
         payloads are read once and no decoded copy is materialised (ops.dequantize_mean_batched). Their
-        mean is the fp32 sum in client order, then / K: bit-identical to simple_aggregate for K <= 4;
-        for K >= 5 torch's CPU sum regroups the additions (multi-accumulator tails, cascade levels),
-        so the two agree to fp32 summation error. Everything else (biases, running statistics,
+        mean is the fp32 sum in client order, then / K: bit-identical to simple_aggregate on CPU tensors
+        (as the reference runs it, model.py:195-197) for K <= 4; for K >= 5 torch's CPU sum regroups the
+        additions (multi-accumulator tails, cascade levels), and torch's GPU sum groups them its own way,
+        so there the two agree to fp32 summation error. Everything else (biases, running statistics,
         non-quantized payloads) is decoded and aggregated as the reference does, on the host."""
         if not all_c_params:
             raise AssertionError("receive_mean: no updates")   # simple_aggregate asserts len > 0

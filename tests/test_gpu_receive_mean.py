@@ -80,7 +80,8 @@ def test_receive_mean_matches_simple_aggregate(k, packed):
 
 def test_receive_mean_device_updates_and_c3_layout():
     """Device-resident updates stay on the device; a C3-sized dict (ResNet-18's 11.7 M parameters in 256
-    tensors, equal layout) from 4 clients is one launch and bit-identical to simple_aggregate."""
+    tensors, equal layout) from 4 clients is one launch and bit-identical to simple_aggregate (on CPU copies,
+    as the reference aggregates)."""
     import recipes
     sizes = recipes.bucket_sizes("equal")
     ch = SLQChannel(8)
@@ -91,9 +92,25 @@ def test_receive_mean_device_updates_and_c3_layout():
         updates.append(ch.on_client_send({f"t{i}.weight": torch.randn(1, n, device=dev, generator=g) * 1e-3
                                           for i, n in enumerate(sizes)})[0])
     got, _ = ch.receive_mean(updates)
-    want = simple_aggregate([ch.on_server_receive(u)[0] for u in updates])
+    want = simple_aggregate([{n: t.cpu() for n, t in ch.on_server_receive(u)[0].items()} for u in updates])
     for n in want:
-        assert got[n].is_cuda and torch.equal(got[n], want[n]), n
+        assert got[n].is_cuda and torch.equal(got[n].cpu(), want[n]), n
+
+
+@pytest.mark.parametrize("packed", [False, True])
+def test_receive_mean_device_payloads_small(packed):
+    """Device-resident payloads (the per-tensor device staging path) for both channels, K = 3: the result
+    stays on the device and equals simple_aggregate of the channel's own decodes as the reference runs it,
+    on CPU tensors (model.py:195-197 hands the strategies CPU state dicts), bit for bit. (torch's GPU sum
+    over dim 0 may group the additions differently.)"""
+    ch = PackedSLQChannel(4) if packed else SLQChannel(8)
+    dev = torch.device("cuda", 0)
+    updates = [ch.on_client_send({n: t.to(dev) if t.ndim > 1 else t for n, t in _client(r).items()})[0]
+               for r in range(3)]
+    got, _ = ch.receive_mean(updates)
+    want = simple_aggregate([{n: t.cpu() for n, t in ch.on_server_receive(u)[0].items()} for u in updates])
+    for n in want:
+        assert got[n].is_cuda == (n in SHAPES) and torch.equal(got[n].cpu(), want[n]), n
 
 
 def test_receive_mean_errors():
