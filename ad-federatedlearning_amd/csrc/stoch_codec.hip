@@ -411,15 +411,26 @@ __device__ __forceinline__ void finalize_small(const adfl_slq_chunk* __restrict_
   if (ci >= nchunks) return;
   const adfl_slq_chunk c = chunks[ci];
   if (c.first_chunk != ci || c.nchunks > kSmallChunks) return;
+  // All kSmallChunks loads issued before the first use (the index clamped to the tensor's last slot), then
+  // summed in slot order with the absent slots masked out: a loop of `k < c.nchunks` loads compiled to one
+  // load + wait per slot, a chain of dependent memory latencies.
+  const int last = c.nchunks - 1;
   double s = 0.0;
   uint32_t mx = 0u, mn = 0xffffffffu;
-  for (int k = 0; k < c.nchunks; ++k) {
-    if (MODE == ADFL_NORM_L2) {
-      s += reinterpret_cast<const double*>(partials)[ci + k];
-    } else {
-      const uint2 v = reinterpret_cast<const uint2*>(partials)[ci + k];
-      mx = max(mx, v.x);
-      mn = min(mn, v.y);
+  if (MODE == ADFL_NORM_L2) {
+    double p[kSmallChunks];
+#pragma unroll
+    for (int k = 0; k < kSmallChunks; ++k) p[k] = reinterpret_cast<const double*>(partials)[ci + min(k, last)];
+#pragma unroll
+    for (int k = 0; k < kSmallChunks; ++k) s += k <= last ? p[k] : 0.0;  // sums are >= +0: adding +0 is exact
+  } else {
+    uint2 p[kSmallChunks];
+#pragma unroll
+    for (int k = 0; k < kSmallChunks; ++k) p[k] = reinterpret_cast<const uint2*>(partials)[ci + min(k, last)];
+#pragma unroll
+    for (int k = 0; k < kSmallChunks; ++k) {  // repeats of the last slot change neither max nor min
+      mx = max(mx, p[k].x);
+      mn = min(mn, p[k].y);
     }
   }
   write_norm<MODE>(c, s, mx, mn, norms, mins);
@@ -456,18 +467,22 @@ __global__ __launch_bounds__(kBigBlock) void k_norm_finalize(const adfl_slq_chun
     uint32_t mx = 0u, mn = 0xffffffffu;
 #pragma unroll
     for (int u = 0; u < U; ++u) a[u] = 0.0;
-    for (int k0 = threadIdx.x; k0 < c.nchunks; k0 += U * kBigBlock) {
+    const int last = c.nchunks - 1;
+    for (int k0 = threadIdx.x; k0 < c.nchunks; k0 += U * kBigBlock) {  // U loads in flight, as in finalize_small
+      if (MODE == ADFL_NORM_L2) {
+        double p[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int k = k0 + u * kBigBlock;
-        if (k < c.nchunks) {
-          if (MODE == ADFL_NORM_L2) {
-            a[u] += reinterpret_cast<const double*>(partials)[ci + k];
-          } else {
-            const uint2 v = reinterpret_cast<const uint2*>(partials)[ci + k];
-            mx = max(mx, v.x);
-            mn = min(mn, v.y);
-          }
+        for (int u = 0; u < U; ++u) p[u] = reinterpret_cast<const double*>(partials)[ci + min(k0 + u * kBigBlock, last)];
+#pragma unroll
+        for (int u = 0; u < U; ++u) a[u] += k0 + u * kBigBlock <= last ? p[u] : 0.0;
+      } else {
+        uint2 p[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) p[u] = reinterpret_cast<const uint2*>(partials)[ci + min(k0 + u * kBigBlock, last)];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          mx = max(mx, p[u].x);
+          mn = min(mn, p[u].y);
         }
       }
     }

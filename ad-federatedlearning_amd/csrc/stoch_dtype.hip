@@ -18,7 +18,7 @@
 //
 // These tensors are rare in ADFL (models train in fp32), so the kernels are plain: one 256-thread block per
 // chunk, each thread one 16-byte vector of x per step (8 fp16 / bf16 or 2 fp64 elements; two Philox blocks
-// or one), scalar head / tail elements around the vectors.
+// or one), kBatch steps' loads in flight, scalar head / tail elements around the vectors.
 
 #include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
@@ -53,8 +53,9 @@ struct DtF16 {
   __device__ static float rn(float v) { return __half2float(__float2half_rn(v)); }
   __device__ static uint32_t bits(float v_on_grid) { return __half_as_ushort(__float2half_rn(v_on_grid)); }
   __device__ static float uniform(uint32_t w) { return (float)(w >> 21) * 0x1p-11f; }
-  __device__ static uint32_t below(int k) { return kCnatF16Below[k - kKMin]; }
-  __device__ static uint32_t above(int k) { return kCnatF16Above[k - kKMin]; }
+  static constexpr int kBands = kCnatF16KMax - kCnatF16KMin + 1;
+  __device__ static const uint16_t* below_tab() { return kCnatF16Below; }
+  __device__ static const uint16_t* above_tab() { return kCnatF16Above; }
 };
 
 struct DtBF16 {
@@ -66,8 +67,9 @@ struct DtBF16 {
   __device__ static float rn(float v) { return rn_bf16(v); }
   __device__ static uint32_t bits(float v_on_grid) { return __float_as_uint(v_on_grid) >> 16; }
   __device__ static float uniform(uint32_t w) { return (float)(w >> 24) * 0x1p-8f; }
-  __device__ static uint32_t below(int k) { return kCnatBF16Below[k - kKMin]; }
-  __device__ static uint32_t above(int k) { return kCnatBF16Above[k - kKMin]; }
+  static constexpr int kBands = kCnatBF16KMax - kCnatBF16KMin + 1;
+  __device__ static const uint16_t* below_tab() { return kCnatBF16Below; }
+  __device__ static const uint16_t* above_tab() { return kCnatBF16Above; }
 };
 
 struct DtF64 {
@@ -78,8 +80,9 @@ struct DtF64 {
   __device__ static double load(S s) { return s; }
   __device__ static double rn(double v) { return v; }
   __device__ static uint64_t bits(double v) { return (uint64_t)__double_as_longlong(v); }
-  __device__ static uint64_t below(int k) { return kCnatF64Below[k - kKMin]; }
-  __device__ static uint64_t above(int k) { return kCnatF64Above[k - kKMin]; }
+  static constexpr int kBands = kCnatF64KMax - kCnatF64KMin + 1;
+  __device__ static const uint16_t* below_tab() { return kCnatF64Below; }
+  __device__ static const uint16_t* above_tab() { return kCnatF64Above; }
 };
 
 // torch's fp -> uint8 / int8 conversion on x86: truncate to int32 (NaN / out of range -> INT32_MIN, low
@@ -114,9 +117,16 @@ __device__ __forceinline__ void stream4(uint64_t seed, uint64_t counter, int64_t
   }
 }
 
+// The band tables of T, copied into LDS by the CNAT kernel (a lookup per element from the __constant__ arrays
+// was a global load in every element's dependency chain).
+struct Bands {
+  const uint16_t* below;
+  const uint16_t* above;
+};
+
 // CNAT's floor / ceil of fl(log2 v) for v = R(|x| + eps) (>= eps: normal), by the band rule.
 template <typename T>
-__device__ __forceinline__ void cnat_bounds(typename T::C v, typename T::C& f, typename T::C& c) {
+__device__ __forceinline__ void cnat_bounds(typename T::C v, typename T::C& f, typename T::C& c, const Bands& tb) {
   using C = typename T::C;
   if (!(v == v)) {
     f = c = v;  // NaN
@@ -131,10 +141,11 @@ __device__ __forceinline__ void cnat_bounds(typename T::C v, typename T::C& f, t
   const B one = (B)1 << T::kMBits;  // 2^mantissa bits: ulps per binade
   const int e = (int)(b >> T::kMBits) - T::kBias;
   const B m = b & (one - 1);
+  const B ab = tb.above[e - T::kKMin], bb = tb.below[e + 1 - T::kKMin];  // both read: no branch on the lookups
   int lo = e, hi = e + 1;
-  if (m <= T::above(e)) {
+  if (m <= ab) {
     hi = e;
-  } else if (one - m <= T::below(e + 1)) {
+  } else if (one - m <= bb) {
     lo = e + 1;
   }
   f = (C)lo;
@@ -153,7 +164,7 @@ __device__ __forceinline__ C pow2(C k) {  // 2^k for integral k (inf past the ra
 // One element -> (level / exponent byte, sign byte). KIND: 0 QSGD / 1 RQSGD (levels), 2 CNAT (exponents).
 template <typename T, int KIND>
 __device__ __forceinline__ uint32_t encode_elem(typename T::C x, typename T::C u, typename T::C norm, int bits,
-                                                uint32_t& sg) {
+                                                uint32_t& sg, const Bands& tb) {
   using C = typename T::C;
   const C xa = __builtin_fabs(x);
   sg = sign_byte(x);
@@ -173,7 +184,7 @@ __device__ __forceinline__ uint32_t encode_elem(typename T::C x, typename T::C u
     } else {
       const C v = T::rn(xa + (C)T::kEps);
       C f, c;
-      cnat_bounds<T>(v, f, c);
+      cnat_bounds<T>(v, f, c, tb);
       const C prob = T::rn(T::rn(T::rn(pow2(c)) - xa) / T::rn(pow2(f)));
       r = u < prob ? f : c;
       if (r == r) r = r < min_e ? min_e : (r > max_e ? max_e : r);  // clamp_ keeps NaN
@@ -214,6 +225,28 @@ __device__ __forceinline__ typename T::C stream1(uint64_t seed, uint64_t counter
 // ------------------------------------------------------------------------------------------------
 // kernels
 // ------------------------------------------------------------------------------------------------
+// The chunk's whole 16-byte vectors, thread t taking vectors t, t + 256, ... in order: kBatch loads issued
+// (index clamped to the last vector) before the first is used. One load per step left every step waiting
+// on its own load's latency.
+constexpr int kBatch = 4;
+
+template <class F>
+__device__ __forceinline__ void for_vectors(const uint4* __restrict__ xv, int64_t nv, F&& f) {
+  for (int64_t i0 = threadIdx.x; i0 < nv; i0 += kBatch * kBlock) {
+    uint4 w[kBatch];
+#pragma unroll
+    for (int b = 0; b < kBatch; ++b) {
+      const int64_t i = i0 + b * kBlock;
+      w[b] = xv[i < nv ? i : nv - 1];
+    }
+#pragma unroll
+    for (int b = 0; b < kBatch; ++b) {
+      const int64_t i = i0 + b * kBlock;
+      if (i < nv) f(i, w[b]);
+    }
+  }
+}
+
 __device__ __forceinline__ double block_sum(double v) {
   __shared__ double red[kWaves];
 #pragma unroll
@@ -270,14 +303,12 @@ __global__ __launch_bounds__(kBlock) void k_dt_norm_partials(const typename T::S
     }
   };
   for (int64_t g = c.start + threadIdx.x; g < sp.b0; g += kBlock) visit(x[g]);
-  const uint4* xv = reinterpret_cast<const uint4*>(x + sp.b0);
-  for (int64_t i = threadIdx.x; i < sp.nv; i += kBlock) {
-    const uint4 w = xv[i];
+  for_vectors(reinterpret_cast<const uint4*>(x + sp.b0), sp.nv, [&](int64_t, const uint4& w) {
     S vals[V];
     __builtin_memcpy(vals, &w, 16);
 #pragma unroll
     for (int j = 0; j < V; ++j) visit(vals[j]);
-  }
+  });
   for (int64_t g = sp.b1 + threadIdx.x; g < sp.end; g += kBlock) visit(x[g]);
   if (MODE == ADFL_NORM_L2) {
     acc = block_sum(acc);
@@ -302,9 +333,20 @@ __global__ __launch_bounds__(kBlock) void k_dt_norm_finalize(const adfl_slq_chun
                                                              double* __restrict__ norms, double* __restrict__ mins) {
   const adfl_slq_chunk c = chunks[blockIdx.x];
   if (c.first_chunk != (int32_t)blockIdx.x) return;  // block-uniform
+  // Each thread's slots k = t, t + 256, ... in order, kU loads in flight (index clamped to the last slot,
+  // absent slots masked): a plain `k < nchunks` loop waits on every load.
+  constexpr int kU = 8;
+  const int last = c.nchunks - 1;
+  const double* p0 = partials + 2 * (int64_t)c.first_chunk;
   if (MODE == ADFL_NORM_L2) {
     double s = 0.0;
-    for (int k = threadIdx.x; k < c.nchunks; k += kBlock) s += partials[2 * (c.first_chunk + k)];
+    for (int k0 = threadIdx.x; k0 <= last; k0 += kU * kBlock) {
+      double p[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) p[u] = p0[2 * min(k0 + u * kBlock, last)];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) s += k0 + u * kBlock <= last ? p[u] : 0.0;  // sums >= +0: adding +0 is exact
+    }
     s = block_sum(s);
     if (threadIdx.x == 0) {
       if constexpr (sizeof(typename T::C) == 4) {
@@ -316,11 +358,20 @@ __global__ __launch_bounds__(kBlock) void k_dt_norm_finalize(const adfl_slq_chun
     }
   } else {
     double mx = 0.0, mn = __builtin_inf(), nan = 0.0;
-    for (int k = threadIdx.x; k < c.nchunks; k += kBlock) {
-      const double a = partials[2 * (c.first_chunk + k)], b = partials[2 * (c.first_chunk + k) + 1];
-      if (a != a) nan = 1.0;
-      mx = fmax(mx, a);
-      mn = fmin(mn, b);
+    for (int k0 = threadIdx.x; k0 <= last; k0 += kU * kBlock) {
+      double a[kU], b[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int k = min(k0 + u * kBlock, last);  // repeats of the last slot are idempotent here
+        a[u] = p0[2 * k];
+        b[u] = p0[2 * k + 1];
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        if (a[u] != a[u]) nan = 1.0;
+        mx = fmax(mx, a[u]);
+        mn = fmin(mn, b[u]);
+      }
     }
     mx = block_max(mx);
     mn = block_min(mn);
@@ -335,19 +386,23 @@ __global__ __launch_bounds__(kBlock) void k_dt_norm_finalize(const adfl_slq_chun
 // Levels / exponents + signs from given per-tensor norms. Whole 16-byte vectors of x (V elements) per thread
 // step, their V level bytes and V sign bytes stored together (8 B for fp16 / bf16, 2 B for fp64); the
 // uniforms of a vector are one (fp64) or two (fp16 / bf16) Philox blocks. Head / tail elements one by one.
+// CNAT's exponents do not depend on the norm: with `partials` set (CNAT only) the kernel takes no norms and
+// writes the chunk's L2 partial instead, visiting the elements in k_dt_norm_partials' order (same sum), so the
+// encode reads x once; k_dt_zero_fixup then applies the norm == 0 branch.
 template <typename T, int KIND>
 __global__ __launch_bounds__(kBlock) void k_dt_quantize(const typename T::S* __restrict__ x,
                                                         const adfl_slq_chunk* __restrict__ chunks, int bits,
                                                         const double* __restrict__ norms,
                                                         const typename T::S* __restrict__ inj, uint64_t seed,
                                                         uint64_t counter, uint8_t* __restrict__ levels,
-                                                        int8_t* __restrict__ signs) {
+                                                        int8_t* __restrict__ signs, double* __restrict__ partials) {
   using C = typename T::C;
   using S = typename T::S;
   constexpr int V = kVec<T>;
   const adfl_slq_chunk c = chunks[blockIdx.x];
-  const C norm = (C)norms[c.tensor];
   const Span sp = split_chunk<T>(c);
+  const bool fused = KIND == 2 && partials != nullptr;
+  const C norm = fused ? (C)1 : (C)norms[c.tensor];
   if (norm == (C)0) {  // quant.py:227-228 / :368-369 / :513-514: u8 zeros, int8 ones
     for (int64_t g = c.start + threadIdx.x; g < sp.end; g += kBlock) {
       levels[g] = 0;
@@ -355,17 +410,28 @@ __global__ __launch_bounds__(kBlock) void k_dt_quantize(const typename T::S* __r
     }
     return;
   }
+  constexpr int kTab = KIND == 2 ? T::kBands : 1;
+  __shared__ uint16_t s_below[kTab], s_above[kTab];
+  if constexpr (KIND == 2) {
+    for (int i = threadIdx.x; i < kTab; i += kBlock) {
+      s_below[i] = T::below_tab()[i];
+      s_above[i] = T::above_tab()[i];
+    }
+    __syncthreads();
+  }
+  const Bands tb{s_below, s_above};
+  double acc = 0.0;
   auto one = [&](int64_t g) {
     const C u = inj ? T::load(inj[g]) : stream1<T>(seed, counter, g);
+    const C v = T::load(x[g]);
     uint32_t sg;
-    levels[g] = (uint8_t)encode_elem<T, KIND>(T::load(x[g]), u, norm, bits, sg);
+    levels[g] = (uint8_t)encode_elem<T, KIND>(v, u, norm, bits, sg, tb);
     signs[g] = (int8_t)sg;
+    if (fused) acc += (double)(v * v);
   };
   for (int64_t g = c.start + threadIdx.x; g < sp.b0; g += kBlock) one(g);
-  const uint4* xv = reinterpret_cast<const uint4*>(x + sp.b0);
-  for (int64_t i = threadIdx.x; i < sp.nv; i += kBlock) {
+  for_vectors(reinterpret_cast<const uint4*>(x + sp.b0), sp.nv, [&](int64_t i, const uint4& w) {
     const int64_t g0 = sp.b0 + i * V;
-    const uint4 w = xv[i];
     S vals[V];
     __builtin_memcpy(vals, &w, 16);
     C u[V];
@@ -389,10 +455,12 @@ __global__ __launch_bounds__(kBlock) void k_dt_quantize(const typename T::S* __r
     uint64_t lw = 0, sw = 0;
 #pragma unroll
     for (int j = 0; j < V; ++j) {
+      const C v = T::load(vals[j]);
       uint32_t sg;
-      const uint32_t lb = encode_elem<T, KIND>(T::load(vals[j]), u[j], norm, bits, sg);
+      const uint32_t lb = encode_elem<T, KIND>(v, u[j], norm, bits, sg, tb);
       lw |= (uint64_t)lb << (8 * j);
       sw |= (uint64_t)sg << (8 * j);
+      if (fused) acc += (double)(v * v);
     }
     if constexpr (V == 8) {
       *reinterpret_cast<uint64_t*>(levels + g0) = lw;
@@ -401,8 +469,31 @@ __global__ __launch_bounds__(kBlock) void k_dt_quantize(const typename T::S* __r
       *reinterpret_cast<uint16_t*>(levels + g0) = (uint16_t)lw;
       *reinterpret_cast<uint16_t*>(signs + g0) = (uint16_t)sw;
     }
-  }
+  });
   for (int64_t g = sp.b1 + threadIdx.x; g < sp.end; g += kBlock) one(g);
+  if (fused) {  // block-uniform
+    acc = block_sum(acc);
+    if (threadIdx.x == 0) partials[2 * blockIdx.x] = acc;
+  }
+}
+
+// CNAT norm == 0 after the fused encode (quant.py:513-514): one thread per chunk reads its tensor's norm; the
+// wave then fills its zero-norm chunks one at a time, all 64 lanes on each (k_cnat_zero_fixup's shape).
+__global__ __launch_bounds__(kBlock) void k_dt_zero_fixup(const adfl_slq_chunk* __restrict__ chunks, int64_t nchunks,
+                                                          const double* __restrict__ norms,
+                                                          uint8_t* __restrict__ levels, int8_t* __restrict__ signs) {
+  const int64_t wave0 = (int64_t)blockIdx.x * kBlock + (threadIdx.x & ~63);
+  const int64_t ci = wave0 + (threadIdx.x & 63);
+  uint64_t m = __ballot(ci < nchunks && norms[chunks[ci].tensor] == 0.0);
+  while (m) {  // wave-uniform
+    const int l = __builtin_ctzll(m);
+    m &= m - 1;
+    const adfl_slq_chunk c = chunks[wave0 + l];
+    for (int64_t i = c.start + (threadIdx.x & 63); i < c.start + c.len; i += 64) {
+      levels[i] = 0;
+      signs[i] = 1;
+    }
+  }
 }
 
 // The stream's uniforms for elements start .. start+n-1, stored in the dtype (tests).
@@ -455,11 +546,29 @@ int quantize_t(int codec, const void* d_x, const adfl_slq_chunk* d_chunks, int64
   const auto* inj = static_cast<const typename T::S*>(d_u);
   if (codec == ADFL_CODEC_CNAT) {
     hipLaunchKernelGGL((k_dt_quantize<T, 2>), dim3((unsigned)nchunks), dim3(kBlock), 0, st, x, d_chunks, bits, d_norms,
-                       inj, seed, counter, d_levels, d_signs);
+                       inj, seed, counter, d_levels, d_signs, (double*)nullptr);
   } else {
     hipLaunchKernelGGL((k_dt_quantize<T, 0>), dim3((unsigned)nchunks), dim3(kBlock), 0, st, x, d_chunks, bits, d_norms,
-                       inj, seed, counter, d_levels, d_signs);
+                       inj, seed, counter, d_levels, d_signs, (double*)nullptr);
   }
+  return launch_status();
+}
+
+// CNAT encode, x read once: exponents + signs + chunk partials, the per-tensor L2 finalize, the norm == 0 fix-up.
+template <typename T>
+int cnat_encode_t(const void* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, int bits, const void* d_u,
+                  uint64_t seed, uint64_t counter, void* d_ws, uint8_t* d_levels, int8_t* d_signs, double* d_norms,
+                  hipStream_t st) {
+  const auto* x = static_cast<const typename T::S*>(d_x);
+  const auto* inj = static_cast<const typename T::S*>(d_u);
+  double* part = static_cast<double*>(d_ws);
+  const dim3 grid((unsigned)nchunks);
+  hipLaunchKernelGGL((k_dt_quantize<T, 2>), grid, dim3(kBlock), 0, st, x, d_chunks, bits, (const double*)nullptr, inj,
+                     seed, counter, d_levels, d_signs, part);
+  hipLaunchKernelGGL((k_dt_norm_finalize<T, ADFL_NORM_L2>), grid, dim3(kBlock), 0, st, d_chunks, part, d_norms,
+                     (double*)nullptr);
+  hipLaunchKernelGGL(k_dt_zero_fixup, dim3((unsigned)((nchunks + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, d_chunks,
+                     nchunks, d_norms, d_levels, d_signs);
   return launch_status();
 }
 
@@ -513,6 +622,24 @@ int adfl_stoch_encode_batched_dt(int32_t codec, int32_t dtype, const void* d_x, 
                                  void* d_workspace, int64_t workspace_bytes, uint8_t* d_levels, int8_t* d_signs,
                                  double* d_norms, double* d_mins, void* stream) {
   if (codec == ADFL_CODEC_RQSGD && !d_mins) return ADFL_E_ARG;
+  if (codec == ADFL_CODEC_CNAT) {  // the argument checks of the two calls below, then one read of x
+    if (const int r = check_common(dtype, d_x, d_chunks, nchunks)) return r;
+    if (bits < 1 || bits > 16) return ADFL_E_BITS;
+    if (!d_norms || !d_workspace || !d_levels || !d_signs) return ADFL_E_ARG;
+    if (workspace_bytes < adfl_stoch_workspace_bytes(nchunks)) return ADFL_E_WORKSPACE;
+    if (!aligned16(d_workspace) || (d_uniforms && !aligned16(d_uniforms)) || !aligned16(d_levels) ||
+        !aligned16(d_signs))
+      return ADFL_E_ALIGN;
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == ADFL_DTYPE_F16)
+      return cnat_encode_t<DtF16>(d_x, d_chunks, nchunks, bits, d_uniforms, seed, counter, d_workspace, d_levels,
+                                  d_signs, d_norms, st);
+    if (dtype == ADFL_DTYPE_BF16)
+      return cnat_encode_t<DtBF16>(d_x, d_chunks, nchunks, bits, d_uniforms, seed, counter, d_workspace, d_levels,
+                                   d_signs, d_norms, st);
+    return cnat_encode_t<DtF64>(d_x, d_chunks, nchunks, bits, d_uniforms, seed, counter, d_workspace, d_levels,
+                                d_signs, d_norms, st);
+  }
   const int mode = codec == ADFL_CODEC_RQSGD ? ADFL_NORM_LINF : ADFL_NORM_L2;
   if (const int r = adfl_stoch_norms_batched_dt(dtype, d_x, d_chunks, nchunks, mode, d_workspace, workspace_bytes,
                                                 d_norms, d_mins, stream))

@@ -140,7 +140,8 @@ int adfl_stoch_norms_batched_dt(int32_t dtype, const void* d_x, const adfl_slq_c
 int adfl_stoch_quantize_batched_dt(int32_t codec, int32_t dtype, const void* d_x, const adfl_slq_chunk* d_chunks,
                                    int64_t nchunks, int bits, const double* d_norms, const void* d_uniforms,
                                    uint64_t seed, uint64_t counter, uint8_t* d_levels, int8_t* d_signs, void* stream);
-/* norms (L2; RQSGD: LINF with d_mins) + quantize. */
+/* norms (L2; RQSGD: LINF with d_mins) + quantize. CNAT reads x once (its exponents do not depend on the norm:
+ * exponents, signs and chunk partials in one pass, then the norms and the norm == 0 fill). */
 int adfl_stoch_encode_batched_dt(int32_t codec, int32_t dtype, const void* d_x, const adfl_slq_chunk* d_chunks,
                                  int64_t nchunks, int bits, const void* d_uniforms, uint64_t seed, uint64_t counter,
                                  void* d_workspace, int64_t workspace_bytes, uint8_t* d_levels, int8_t* d_signs,

@@ -637,7 +637,8 @@ def mode_stoch(args, world, rank, dev):
                     ev[1].record()
             _, evs = timed(step_dt, args.steps, args.warmup, world, 2)
             enc = seg_ms(evs, 0, 1)
-            eb = (2 * xd.element_size() + 2) * lay.total   # x read twice (norm pass, quantize) + 2 planes
+            # QSGD: x read twice (norm pass, quantize) + 2 planes; CNAT: x once (exponents + partials) + 2 planes
+            eb = ((1 if codec == "cnat" else 2) * xd.element_size() + 2) * lay.total
             res[f"c3_bucket_{str(dtype).replace('torch.', '')}_{codec}_flushed"] = {
                 "encode_ms": round(enc, 4), "encode_GBs": round(eb / enc / 1e6, 1),
                 "encode_frac": round(eb / enc / 1e6 / HBM_PEAK_GBS, 3)}
