@@ -124,40 +124,32 @@ struct Bands {
   const uint16_t* above;
 };
 
-// CNAT's floor / ceil of fl(log2 v) for v = R(|x| + eps) (>= eps: normal), by the band rule.
+// CNAT's floor / ceil of fl(log2 v) for a finite v = R(|x| + eps) (>= eps: normal), by the band rule.
 template <typename T>
-__device__ __forceinline__ void cnat_bounds(typename T::C v, typename T::C& f, typename T::C& c, const Bands& tb) {
-  using C = typename T::C;
-  if (!(v == v)) {
-    f = c = v;  // NaN
-    return;
-  }
-  if (__builtin_isinf(v)) {
-    f = c = v;  // +inf: log2 inf = inf
-    return;
-  }
+__device__ __forceinline__ void cnat_bounds(typename T::C v, int& lo, int& hi, const Bands& tb) {
   const auto b = T::bits(v);
   using B = decltype(b);
   const B one = (B)1 << T::kMBits;  // 2^mantissa bits: ulps per binade
   const int e = (int)(b >> T::kMBits) - T::kBias;
   const B m = b & (one - 1);
   const B ab = tb.above[e - T::kKMin], bb = tb.below[e + 1 - T::kKMin];  // both read: no branch on the lookups
-  int lo = e, hi = e + 1;
+  lo = e;
+  hi = e + 1;
   if (m <= ab) {
     hi = e;
   } else if (one - m <= bb) {
     lo = e + 1;
   }
-  f = (C)lo;
-  c = (C)hi;
 }
 
+// 2^k in C, exact, for the band range of every dtype (fp32: k in [-126, 128], 128 -> inf; fp64: k in
+// [-1022, 1024], 1024 -> inf), built from the exponent field.
 template <typename C>
-__device__ __forceinline__ C pow2(C k) {  // 2^k for integral k (inf past the range)
+__device__ __forceinline__ C pow2i(int k) {
   if constexpr (sizeof(C) == 4) {
-    return ldexpf(1.0f, (int)fmaxf(fminf(k, 300.0f), -300.0f));
+    return __uint_as_float((uint32_t)(k + 127) << 23);
   } else {
-    return ldexp(1.0, (int)fmax(fmin(k, 3000.0), -3000.0));
+    return __longlong_as_double((long long)(k + 1023) << 52);
   }
 }
 
@@ -177,19 +169,19 @@ __device__ __forceinline__ uint32_t encode_elem(typename T::C x, typename T::C u
     const C lev = l + (u < prob ? (C)1 : (C)0);
     return low_byte(lev);
   } else {
-    const C min_e = (C)(-(1 << (bits - 1))), max_e = (C)((1 << (bits - 1)) - 1);
-    C r;
-    if (x == (C)0) {
-      r = min_e;
-    } else {
-      const C v = T::rn(xa + (C)T::kEps);
-      C f, c;
-      cnat_bounds<T>(v, f, c, tb);
-      const C prob = T::rn(T::rn(T::rn(pow2(c)) - xa) / T::rn(pow2(f)));
-      r = u < prob ? f : c;
-      if (r == r) r = r < min_e ? min_e : (r > max_e ? max_e : r);  // clamp_ keeps NaN
-    }
-    return low_byte(r);
+    // The exponent is integral from here on. NaN x: ceil NaN, clamp_ keeps it, int8(NaN) = 0; inf x (the
+    // only way v is inf): log2 inf = inf, prob = NaN, so ceil = inf, clamped to max_exp.
+    const int min_e = -(1 << (bits - 1)), max_e = (1 << (bits - 1)) - 1;
+    if (x == (C)0) return (uint32_t)min_e & 0xffu;
+    const C v = T::rn(xa + (C)T::kEps);
+    if (!(v == v)) return 0u;
+    if (__builtin_isinf(v)) return (uint32_t)max_e & 0xffu;
+    int lo, hi;
+    cnat_bounds<T>(v, lo, hi, tb);
+    // the reference's (2^c - |x|) / 2^f, each op rounded to the dtype (2^16 is inf in fp16: prob NaN, ceil)
+    const C prob = T::rn(T::rn(T::rn(pow2i<C>(hi)) - xa) / T::rn(pow2i<C>(lo)));
+    const int r = u < prob ? lo : hi;
+    return (uint32_t)min(max(r, min_e), max_e) & 0xffu;
   }
 }
 
