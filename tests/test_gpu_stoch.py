@@ -184,6 +184,30 @@ def test_seeded_encode_matches_oracle_on_philox_uniforms(codec, sizes):
             assert mh[i] == so.lminf_norm(flat[o:o + n]) and nh[i] == so.linf_norm(flat[o:o + n])
 
 
+@pytest.mark.parametrize("mode", ["l2", "linf"])
+def test_norm_finalize_many_chunks(mode):
+    """A tensor of 16,387 chunks between two small ones: the finalize's large-tensor role sums it in two
+    batches of 16 loads per thread, the second one partial (clamped index, masked slots). A duplicated or
+    dropped slot moves the L2 norm by ~1/16,387 (thousands of ulps); the fp64 sum's order may move it by 1."""
+    n_big = (16 * 1024 + 3) * 8192 + 77   # ADFL_SLQ_CHUNK_ELEMS = 8192
+    sizes = [5, n_big, 9000]
+    lay = ops.BucketLayout(sizes, align=1)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    xd = torch.randn(lay.total, device=DEV, generator=g) * 1e-3
+    assert lay.nchunks > 16 * 1024 + 3
+    nrm, mins = stoch.norms_batched(xd, lay, stoch.NORM_L2 if mode == "l2" else stoch.NORM_LINF)
+    flat, nh = h(xd), h(nrm)
+    for i, n in enumerate(sizes):
+        o = int(lay.offsets[i])
+        x = flat[o:o + n]
+        if mode == "l2":
+            s = np.sum((x * x).astype(np.float64))     # fp32 squares, fp64 sum
+            want = np.float32(np.sqrt(np.float64(np.float32(s))))
+            assert ulp_diff(nh[i], want) <= 1, (i, nh[i], want)
+        else:
+            assert nh[i] == np.abs(x).max() and h(mins)[i] == np.abs(x).min()
+
+
 def test_philox_uniform_statistics():
     n = 1 << 24
     u = stoch.philox_uniforms(n, 42, 0, device=DEV).double()

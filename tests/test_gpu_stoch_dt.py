@@ -171,21 +171,25 @@ def test_channel_mixed_dtype_dict(codec):
         assert same_f32(dec[name].numpy().reshape(-1), want.reshape(-1)), name
 
 
-@pytest.mark.parametrize("dtname,n", [("float16", 1 << 24), ("bfloat16", (1 << 23) + 5), ("float64", (1 << 22) + 3)])
+@pytest.mark.parametrize("dtname,n", [("float16", (1 << 24) + 3 * 8192 + 11), ("bfloat16", (1 << 23) + 5),
+                                       ("float64", (1 << 22) + 3)])
 def test_large_tensor_multichunk_norm_and_bytes(dtname, n):
     """One large tensor (thousands of chunks: the per-tensor norm is reduced by a block over its chunk
-    partials): the norm equals the oracle's (fp64 within a few ulps) and every byte equals the oracle on the
-    kernel's norm with the same Philox stream."""
+    partials; fp16's 2,052 chunks take the finalize's per-thread loop twice, the second batch partial): the
+    norm equals the oracle's (fp64 within a few ulps), RQSGD's max / min exactly, and every byte equals the
+    oracle on the kernel's norm with the same Philox stream."""
     dt = DT[dtname]
     g = torch.Generator().manual_seed(n)
     xt = (torch.randn(n, generator=g, dtype=torch.float64) * 1e-2).to(TDT[dtname])
     raw = xt.numpy() if dtname == "float64" else xt.view(torch.int16).numpy().view(np.uint16)
     lay = ops.BucketLayout([n], align=1)
-    for codec in ("qsgd", "cnat"):
-        q, s, norms, _ = stoch.encode_batched_dt(codec, xt.to(DEV), lay, 8, seed=77, counter=0)
+    for codec in ("qsgd", "rqsgd", "cnat"):
+        q, s, norms, mins = stoch.encode_batched_dt(codec, xt.to(DEV), lay, 8, seed=77, counter=0)
         norm = float(norms.cpu()[0])
-        want = do.l2_norm(raw, dt)
-        if dt == do.DT_F64:
+        want = do.linf_norm(raw, dt) if codec == "rqsgd" else do.l2_norm(raw, dt)
+        if codec == "rqsgd":
+            assert norm == want and float(mins.cpu()[0]) == do.lminf_norm(raw, dt)
+        elif dt == do.DT_F64:
             assert abs(norm - want) <= 64 * 2.0 ** -52 * want
         else:
             assert norm == want
