@@ -38,7 +38,7 @@ from .. import hostcopy
 from .. import stoch as sops
 from ..model import CompressedParameters, Parameters, QuantParameter, QuantParameters, get_parameter_info
 from .channel import Channel, IdentityChannel
-from .quant import _PendingD2H, _hand_out, _serialized, _stage_in, _staging
+from .quant import _PendingD2H, _aggregate_entries, _hand_out, _serialized, _stage_in, _stage_rows, _staging
 
 _CODECS = ("qsgd", "rqsgd", "cnat")
 
@@ -219,6 +219,28 @@ def _decode_stoch(items: List[Tuple[str, QuantParameter]], codec: str, bits: int
     return {name: t for (name, _), t in zip(items, decoded)}
 
 
+@_serialized
+def _decode_mean_stoch(all_c_params: List[QuantParameters], names: List[str], codec: str,
+                       bits: int) -> List[torch.Tensor]:
+    """simple_aggregate over K payloads of the entries `names` (every client's entry decodable by
+    _decode_stoch, one shape): both byte planes of every client staged as device rows, one launch of
+    adfl_stoch_dequantize_mean_batched, one owned fp32 tensor per entry (CPU when the payloads are)."""
+    st = _staging()
+    dev = st.device
+    first = all_c_params[0].params
+    lay = st.layout(tuple(int(first[n].data.numel()) for n in names))
+    lv_rows = _stage_rows([[c.params[n].data for n in names] for c in all_c_params], lay, st, "sm_levels")
+    sg_rows = _stage_rows([[c.params[n].signs for n in names] for c in all_c_params], lay, st, "sm_signs")
+    norms = torch.tensor([[float(c.params[n].scale) for n in names] for c in all_c_params],
+                         dtype=torch.float32).to(dev, non_blocking=True)
+    mins = (torch.tensor([[float(c.params[n].scale_2) for n in names] for c in all_c_params],
+                         dtype=torch.float32).to(dev, non_blocking=True) if codec == "rqsgd" else None)
+    out_dev = sops.dequantize_mean_batched(codec, lv_rows, sg_rows, norms, lay, bits, mins=mins,
+                                           out=st.buf("sm_out", lay.total, torch.float32))
+    on_cpu = [not any(c.params[n].data.is_cuda for c in all_c_params) for n in names]
+    return _hand_out(out_dev, lay, [first[n].data.shape for n in names], on_cpu, st, "sm_out")
+
+
 class _StochChannel(Channel):
     """Shared body of the three bi-directional stochastic channels."""
 
@@ -278,6 +300,42 @@ class _StochChannel(Channel):
             else:
                 params[name] = p.data.data  # passthrough
         return params, time.perf_counter() - s_time
+
+    def receive_mean(self, all_c_params: List[CompressedParameters]) -> Tuple[Parameters, float]:
+        """``simple_aggregate([self.on_server_receive(c)[0] for c in all_c_params])`` — a synchronous server
+        decoding K client updates and averaging them (Src/ADFL/Strategy/simple.py:83-89 over
+        Src/ADFL/model.py:221-234). Returns (aggregate, seconds).
+
+        Entries encoded in every update are decoded and averaged on the device in one launch (each client's
+        level and sign planes read once, no decoded copy materialised): the fp32 sum in client order from
+        zero, then / K, bit-identical to simple_aggregate of the decoded CPU tensors for K <= 4 (torch's CPU
+        sum regroups from K = 5: fp32 summation error). Everything else (biases, running statistics, empty
+        tensors) is decoded and aggregated as the reference does, on the host."""
+        if not all_c_params:
+            raise AssertionError("receive_mean: no updates")   # simple_aggregate asserts len > 0
+        for c in all_c_params:
+            assert isinstance(c, QuantParameters)
+        s_time = time.perf_counter()
+        names = list(all_c_params[0].params.keys())
+        fused = [n for n in names if all(n in c.params and self._fusable(c.params[n]) for c in all_c_params)
+                 and len({tuple(c.params[n].data.shape) for c in all_c_params}) == 1]
+        out: Parameters = {}
+        if fused:
+            out.update(zip(fused, _decode_mean_stoch(all_c_params, fused, self.CODEC, self.bits)))
+        rest = [n for n in names if n not in out]
+        if rest:
+            parts = [self._receive(QuantParameters({n: c.params[n] for n in rest}, 0))[0] for c in all_c_params]
+            out.update(_aggregate_entries(rest, parts))
+        return {n: out[n] for n in names}, time.perf_counter() - s_time
+
+    @staticmethod
+    def _fusable(p: QuantParameter) -> bool:
+        """An entry _receive decodes (_decode_stoch's inputs: byte planes of one size, a numeric norm)."""
+        d, g = p.data, p.signs
+        return (isinstance(d, torch.Tensor) and isinstance(g, torch.Tensor) and d.ndim > 1 and d.numel() > 0
+                and d.element_size() == 1 and not d.is_quantized and not d.is_floating_point()
+                and g.numel() == d.numel() and g.element_size() == 1 and not g.is_floating_point()
+                and d.is_cuda == g.is_cuda)
 
     def _quantize_params(self, params: Parameters, bits: int, uniforms=None, seed=None) -> QuantParameters:
         """Biases and running metrics (ndim <= 1) are not quantized."""

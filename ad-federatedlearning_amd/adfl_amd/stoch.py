@@ -29,7 +29,7 @@ from .ops import BucketLayout, _dev, _stream
 __all__ = ["RngStream", "norms_batched", "qsgd_quantize_batched", "qsgd_encode_batched", "rqsgd_encode_batched",
            "qsgd_decode_batched", "rqsgd_decode_batched", "cnat_encode_batched", "cnat_decode_batched",
            "philox_uniforms", "workspace", "NORM_L2", "NORM_LINF", "NORM_L2_TORCH", "DT_DTYPES", "encode_batched_dt",
-           "quantize_batched_dt", "norms_batched_dt", "philox_uniforms_dt"]
+           "quantize_batched_dt", "norms_batched_dt", "philox_uniforms_dt", "dequantize_mean_batched"]
 
 
 class RngStream:
@@ -239,6 +239,39 @@ def philox_uniforms(n: int, seed: int, counter: int, start: int = 0, *, device=N
 
 
 # ------------------------------------------------------------------------------------------------
+def dequantize_mean_batched(codec: str, levels: torch.Tensor, signs: torch.Tensor, norms: torch.Tensor,
+                            layout: BucketLayout, bits: int, *, mins: Optional[torch.Tensor] = None,
+                            out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """simple_aggregate of K clients' decodes in one launch (adfl_stoch_dequantize_mean_batched): levels /
+    signs are [K, row] byte planes (uint8 / int8; row >= layout.total, a multiple of 16), norms (RQSGD: mins)
+    [K, ntensors] fp32. Returns the fp32 mean bucket."""
+    if codec not in _CODEC_IDS:
+        raise ValueError(f"adfl_amd.stoch: codec must be one of {sorted(_CODEC_IDS)}, got {codec!r}")
+    levels, signs, norms = _dev(levels, "levels"), _dev(signs, "signs"), _dev(norms, "norms")
+    if levels.dim() != 2 or signs.shape != levels.shape or levels.element_size() != 1 or signs.element_size() != 1:
+        raise ValueError("adfl_amd.stoch: levels / signs must be [K, row] byte planes of one shape")
+    k, row = levels.shape
+    if row < layout.total or not levels.is_contiguous() or not signs.is_contiguous():
+        raise ValueError(f"adfl_amd.stoch: rows of {row} bytes cannot hold the {layout.total}-element bucket")
+    if norms.shape != (k, layout.ntensors) or norms.dtype != torch.float32 or not norms.is_contiguous():
+        raise ValueError(f"adfl_amd.stoch: norms must be contiguous fp32 [{k}, {layout.ntensors}]")
+    if codec == "rqsgd":
+        if mins is None:
+            raise ValueError("adfl_amd.stoch: RQSGD needs mins")
+        mins = _dev(mins, "mins")
+        if mins.shape != norms.shape or mins.dtype != torch.float32 or not mins.is_contiguous():
+            raise ValueError("adfl_amd.stoch: mins must match norms")
+    dev = levels.device
+    out = torch.empty(layout.total, dtype=torch.float32, device=dev) if out is None else out
+    if out.dtype != torch.float32 or out.numel() < layout.total or not out.is_contiguous() or out.device != dev:
+        raise ValueError(f"adfl_amd.stoch: out must be a contiguous fp32 device tensor of >= {layout.total}")
+    check(_lib.load().adfl_stoch_dequantize_mean_batched(
+        _CODEC_IDS[codec], levels.data_ptr(), signs.data_ptr(), row, k, layout.device_chunks(dev).data_ptr(),
+        layout.nchunks, bits, norms.data_ptr(), mins.data_ptr() if mins is not None else None, layout.ntensors,
+        out.data_ptr(), _stream(dev)))
+    return out
+
+
 # fp16 / bf16 / fp64 buckets (include/adfl_stoch.h *_dt): the reference's arithmetic in the tensor's dtype
 # ------------------------------------------------------------------------------------------------
 DT_DTYPES = {torch.float16: DTYPE_F16, torch.bfloat16: DTYPE_BF16, torch.float64: DTYPE_F64}

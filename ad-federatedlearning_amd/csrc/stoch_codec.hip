@@ -1129,6 +1129,74 @@ __global__ __launch_bounds__(kBlock) void k_stoch_dequantize(const uint8_t* __re
   if (i >= 0) oc[i] = decode_exact<KIND>(lv[i], sg[i], norm, mn, s);
 }
 
+// Server-side mean of K clients' payloads: simple_aggregate (Src/ADFL/model.py:221-234) over the K decodes
+// (quant.py:243-252 / :385-398 / :537-545), the synchronous server's aggregate of K updates:
+//   out[i] = fp32(((0 + d_0[i]) + d_1[i]) + ... + d_{K-1}[i]) / K   (the division correctly rounded)
+// with d_r the decode of row r's level / exponent and sign bytes under row r's norm (+0 where that norm is 0,
+// as the decoder returns zeros). Row r's planes are levels / signs + r * row_stride (one bucket payload each,
+// one chunk table), its norms norms + r * norm_stride (RQSGD's minima likewise). The sum starts from +0 as
+// torch's does, so a column of -0 decodes (level 0, sign -1) sums to +0. One block per chunk; each thread's
+// dword groups (after the < 4-element head), all of a row's loads issued before its decodes; the exact
+// decode forms throughout (K decodes per output element; the loads dominate).
+template <int KIND>
+__device__ __forceinline__ float mean_term(uint32_t l, uint32_t g, float norm, float mn, float s) {
+  return norm == 0.0f ? 0.0f : decode_exact<KIND>(l, g, norm, mn, s);
+}
+
+template <int KIND>
+__global__ __launch_bounds__(kBlock) void k_stoch_dequantize_mean(const uint8_t* __restrict__ levels,
+                                                                  const uint8_t* __restrict__ signs,
+                                                                  int64_t row_stride, int k,
+                                                                  const adfl_slq_chunk* __restrict__ chunks,
+                                                                  const float* __restrict__ norms,
+                                                                  const float* __restrict__ mins, int64_t norm_stride,
+                                                                  float s, float* __restrict__ out) {
+  const adfl_slq_chunk c = chunks[blockIdx.x];
+  const int head = chunk_head4(c.start, c.len);
+  const int n4 = (c.len - head) >> 2;
+  const int ie = edge_elem(head, head + (n4 << 2), c.len);
+  float4 acc[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) acc[j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  float acc_e = 0.0f;
+  for (int r = 0; r < k; ++r) {
+    const float norm = norms[r * norm_stride + c.tensor];
+    const float mn = KIND == 1 ? mins[r * norm_stride + c.tensor] : 0.0f;
+    const uint8_t* lv = levels + r * row_stride + c.start;
+    const uint8_t* sg = signs + r * row_stride + c.start;
+    const uint32_t* l4 = reinterpret_cast<const uint32_t*>(lv + head);
+    const uint32_t* g4 = reinterpret_cast<const uint32_t*>(sg + head);
+    uint32_t L[kPer], G[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int q = threadIdx.x + j * kBlock;
+      L[j] = q < n4 ? l4[q] : 0u;
+      G[j] = q < n4 ? g4[q] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      if ((int)threadIdx.x + j * kBlock < n4) {
+        acc[j].x += mean_term<KIND>(L[j] & 0xffu, G[j] & 0xffu, norm, mn, s);
+        acc[j].y += mean_term<KIND>((L[j] >> 8) & 0xffu, (G[j] >> 8) & 0xffu, norm, mn, s);
+        acc[j].z += mean_term<KIND>((L[j] >> 16) & 0xffu, (G[j] >> 16) & 0xffu, norm, mn, s);
+        acc[j].w += mean_term<KIND>(L[j] >> 24, G[j] >> 24, norm, mn, s);
+      }
+    }
+    if (ie >= 0) acc_e += mean_term<KIND>(lv[ie], sg[ie], norm, mn, s);
+  }
+  const double dk = (double)k;
+  float* oc = out + c.start;
+  float4* o4 = reinterpret_cast<float4*>(oc + head);
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int q = threadIdx.x + j * kBlock;
+    if (q < n4)
+      store4_nt(o4 + q, make_float4((float)((double)acc[j].x / dk), (float)((double)acc[j].y / dk),
+                                    (float)((double)acc[j].z / dk), (float)((double)acc[j].w / dk)));
+  }
+  if (ie >= 0) oc[ie] = (float)((double)acc_e / dk);
+}
+
 __global__ __launch_bounds__(kBlock) void k_philox_uniforms(float* __restrict__ out, int64_t n, int64_t start,
                                                             Uniforms U) {
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
@@ -1349,6 +1417,34 @@ int adfl_cnat_encode_batched_work(const float* d_x, const adfl_slq_chunk* d_chun
                                     workspace_bytes, d_exps, d_signs, d_norms, stream);
   return launch_resident<2>(d_x, d_chunks, nchunks, d_work, nwork, bits, d_uniforms, seed, counter,
                             reinterpret_cast<uint8_t*>(d_exps), d_signs, d_norms, nullptr, stream);
+}
+
+int adfl_stoch_dequantize_mean_batched(int32_t codec, const uint8_t* d_levels, const int8_t* d_signs,
+                                       int64_t row_stride_bytes, int32_t k, const adfl_slq_chunk* d_chunks,
+                                       int64_t nchunks, int bits, const float* d_norms, const float* d_mins,
+                                       int64_t norm_stride, float* d_out, void* stream) {
+  if (codec != ADFL_CODEC_QSGD && codec != ADFL_CODEC_RQSGD && codec != ADFL_CODEC_CNAT) return ADFL_E_ARG;
+  if (!d_levels || !d_signs || !d_norms || !d_out || (codec == ADFL_CODEC_RQSGD && !d_mins) ||
+      bad_table(d_chunks, nchunks) || k < 1 || row_stride_bytes < 0 || norm_stride < 0 ||
+      (k > 1 && (row_stride_bytes == 0 || norm_stride == 0)))
+    return ADFL_E_ARG;
+  if (codec != ADFL_CODEC_CNAT)
+    if (int s = check_bits(bits)) return s;
+  if (!aligned16(d_levels) || !aligned16(d_signs) || !aligned16(d_out) || (row_stride_bytes & 15)) return ADFL_E_ALIGN;
+  const float s = codec == ADFL_CODEC_CNAT ? 1.0f : levels_f(bits);
+  const auto* sg = reinterpret_cast<const uint8_t*>(d_signs);
+  const dim3 grid((unsigned)nchunks), block(kBlock);
+  hipStream_t st = (hipStream_t)stream;
+  if (codec == ADFL_CODEC_QSGD)
+    hipLaunchKernelGGL(k_stoch_dequantize_mean<0>, grid, block, 0, st, d_levels, sg, row_stride_bytes, k, d_chunks,
+                       d_norms, d_mins, norm_stride, s, d_out);
+  else if (codec == ADFL_CODEC_RQSGD)
+    hipLaunchKernelGGL(k_stoch_dequantize_mean<1>, grid, block, 0, st, d_levels, sg, row_stride_bytes, k, d_chunks,
+                       d_norms, d_mins, norm_stride, s, d_out);
+  else
+    hipLaunchKernelGGL(k_stoch_dequantize_mean<2>, grid, block, 0, st, d_levels, sg, row_stride_bytes, k, d_chunks,
+                       d_norms, d_mins, norm_stride, s, d_out);
+  return launch_status();
 }
 
 int adfl_philox_uniforms(float* d_out, int64_t n, int64_t start, uint64_t seed, uint64_t counter, void* stream) {

@@ -96,6 +96,18 @@ int adfl_cnat_encode_batched(const float* d_x, const adfl_slq_chunk* d_chunks, i
 int adfl_cnat_dequantize_batched(const int8_t* d_exps, const int8_t* d_signs, const adfl_slq_chunk* d_chunks,
                                  int64_t nchunks, const float* d_norms, float* d_out, void* stream);
 
+/* simple_aggregate (Src/ADFL/model.py:221-234) of K clients' decodes, one launch: out[i] =
+ * fp32(((0 + d_0[i]) + ... + d_{K-1}[i]) / K), d_r the codec's decode (above) of row r's level / exponent
+ * and sign bytes (d_levels / d_signs + r * row_stride_bytes, each a bucket payload over d_chunks) under row
+ * r's norms d_norms + r * norm_stride (RQSGD: d_mins likewise; +0 where a norm is 0). codec: ADFL_CODEC_*
+ * (bits unused for CNAT). Bases 16-byte aligned, row_stride_bytes a multiple of 16. Bit-identical to torch's
+ * CPU sum for K <= 4 (it adds rows in order from zero); from K = 5 torch regroups, within fp32 summation
+ * error. */
+int adfl_stoch_dequantize_mean_batched(int32_t codec, const uint8_t* d_levels, const int8_t* d_signs,
+                                       int64_t row_stride_bytes, int32_t k, const adfl_slq_chunk* d_chunks,
+                                       int64_t nchunks, int bits, const float* d_norms, const float* d_mins,
+                                       int64_t norm_stride, float* d_out, void* stream);
+
 /* One-launch encodes (same outputs, bit for bit) for a bucket whose tensors ALL have at most
  * ADFL_SLQ_RESIDENT_CHUNKS chunks: d_work / nwork is the work list of adfl_slq_build_encode_work (the first
  * chunk of every tensor; nwork == 0 when some tensor is larger). A 1024-thread block holds one whole tensor

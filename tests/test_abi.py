@@ -132,6 +132,17 @@ def test_dtype_and_bucket_mean_argument_errors_return_codes_without_launching():
     assert lib.adfl_slq_dequantize_mean_batched_int4(16, 32, 2, 16, 1, 16, 1, 0, None, 16, None) == -1
     assert lib.adfl_slq_dequantize_mean_batched_int4(20, 32, 2, 16, 1, 16, 1, -1, None, 16, None) == -3
     assert lib.adfl_slq_dequantize_mean_batched_int4(16, 32, 0, 16, 1, 16, 1, -1, None, 16, None) == -1
+    # stochastic server mean: codec, minima for RQSGD, K, strides, bits, alignment
+    m = lib.adfl_stoch_dequantize_mean_batched
+    assert m(9, 16, 16, 32, 2, 16, 1, 8, 16, None, 1, 16, None) == -1
+    assert m(_lib.CODEC_RQSGD, 16, 16, 32, 2, 16, 1, 8, 16, None, 1, 16, None) == -1
+    assert m(QSGD, 16, 16, 32, 0, 16, 1, 8, 16, None, 1, 16, None) == -1
+    assert m(QSGD, 16, 16, 0, 2, 16, 1, 8, 16, None, 1, 16, None) == -1
+    assert m(QSGD, 16, 16, 32, 2, 16, 1, 8, 16, None, 0, 16, None) == -1
+    assert m(QSGD, 16, 16, 32, 2, 16, 1, 0, 16, None, 1, 16, None) == -2
+    assert m(QSGD, 16, 16, 24, 2, 16, 1, 8, 16, None, 1, 16, None) == -3
+    assert m(CNAT, 20, 16, 32, 2, 16, 1, 0, 16, None, 1, 16, None) == -3
+    assert m(CNAT, 16, 16, 32, 2, 16, 1, 0, 16, None, 1, 24, None) == -3
 
 
 def test_build_chunks_host_planning():
