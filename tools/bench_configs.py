@@ -551,7 +551,51 @@ def mode_channel_stoch(args, world, rank, dev):
                      "reference_encode_ms": round(best(r, 0), 3), "reference_decode_ms": round(best(r, 1), 3),
                      "ours_GiB_s": round(gib / ((best(o, 0) + best(o, 1)) * 1e-3), 2),
                      "reference_GiB_s": round(gib / ((best(r, 0) + best(r, 1)) * 1e-3), 3)}
+        res[name]["aggregate_k4"] = _stoch_aggregate_k4(name, ch, params, args)
     return res
+
+
+def _stoch_aggregate_k4(codec, ch, params, args):
+    """Synchronous server aggregate of K = 4 updates (Src/ADFL/Strategy/simple.py:83-89): receive_mean (one
+    decode-mean launch) against the reference's per-tensor decode ops (quant.py:243-252 / 385-398 / 537-545)
+    + simple_aggregate (Src/ADFL/model.py:221-234) on the host, over the same payloads; the output is checked
+    against simple_aggregate of the channel's own decodes (bit-identical for K <= 4)."""
+    s = float(2 ** ch.bits - 1)
+    ups = []
+    for ci in range(4):
+        gr = torch.Generator().manual_seed(10 + ci)
+        ups.append(ch.on_client_send({k: torch.randn(v.shape, generator=gr) * 1e-3 for k, v in params.items()})[0])
+
+    def ref_decode(p):
+        if p.data.ndim <= 1:
+            return p.data.data
+        norm, sf = float(p.scale), p.signs.float()
+        if codec == "qsgd":
+            return (norm * p.data.float()) / s * sf
+        if codec == "rqsgd":
+            r = ((norm * sf) * p.data.float()) / s
+            z = p.data == 0
+            r[z] = float(p.scale_2) * sf[z]
+            return r
+        return (norm * sf) * (2 ** p.data.float())
+
+    def aggregate(dec):
+        return {k: torch.sum(torch.stack([d[k] for d in dec], dim=0), dim=0) / len(dec) for k in dec[0]}
+
+    def ref_aggregate():
+        t0 = time.perf_counter()
+        agg = aggregate([{k: ref_decode(p) for k, p in u.params.items()} for u in ups])
+        return time.perf_counter() - t0, agg
+
+    for _ in range(args.warmup):
+        ch.receive_mean(ups)
+        ref_aggregate()
+    om = min(ch.receive_mean(ups)[1] for _ in range(args.steps))
+    rm = min(ref_aggregate()[0] for _ in range(max(3, args.steps // 4)))
+    mine = ch.receive_mean(ups)[0]
+    want = aggregate([ch.on_server_receive(u)[0] for u in ups])
+    return {"ours_receive_mean_ms": round(om * 1e3, 3), "reference_decode_simple_aggregate_ms": round(rm * 1e3, 3),
+            "identical_to_own_decodes_aggregated": all(torch.equal(mine[k], want[k]) for k in want)}
 
 
 def mode_stoch(args, world, rank, dev):
