@@ -199,6 +199,30 @@ def _payloads(names, datas, signs, nm, ntensors: int, codec: str, dtype: torch.d
 def _decode_stoch(items: List[Tuple[str, QuantParameter]], codec: str, bits: int) -> Dict[str, torch.Tensor]:
     """Decode (levels, signs, norm[, min]) payloads of ndim > 1 tensors in one bucketed pass."""
     st = _staging()
+    lay, out_dev = _decode_stoch_bucket(st, items, codec, bits)
+    on_cpu = [not p.data.is_cuda for _, p in items]
+    decoded = _hand_out(out_dev, lay, [p.data.shape for _, p in items], on_cpu, st, "d_out")
+    return {name: t for (name, _), t in zip(items, decoded)}
+
+
+@_serialized
+def _decode_add_stoch(items: List[Tuple[str, QuantParameter]], codec: str, bits: int,
+                      targets: List[List[torch.Tensor]]) -> None:
+    """Decode the payloads once into the device bucket and add it into every model (targets[k][j] += decode of
+    item j, fp32 adds: add_parameters_inpace's mul_(1).add_(d, alpha=1), model.py:337-347)."""
+    st = _staging()
+    lay, out_dev = _decode_stoch_bucket(st, items, codec, bits)
+    views = [out_dev[o:o + n].view(p.data.shape)
+             for o, n, (_, p) in zip(lay.offsets.tolist(), lay.sizes.tolist(), items)]
+    with torch.no_grad():
+        for model in targets:
+            torch._foreach_add_(model, views)
+    # the next call's staging rewrites the pinned buffers this call's H2D read and the bucket it decoded into
+    torch.cuda.current_stream(st.device).synchronize()
+
+
+def _decode_stoch_bucket(st, items: List[Tuple[str, QuantParameter]], codec: str, bits: int):
+    """Both planes staged as one bucket on the device and decoded by one launch: (layout, fp32 bucket)."""
     dev = st.device
     lay = st.layout(tuple(int(p.data.numel()) for _, p in items))
     lv_dev = _stage_in([p.data.view(torch.uint8) for _, p in items], lay, st, "d_levels", torch.uint8)
@@ -214,9 +238,7 @@ def _decode_stoch(items: List[Tuple[str, QuantParameter]], codec: str, bits: int
         sops.rqsgd_decode_batched(lv_dev, sg_dev, sc[:ntens], sc[ntens:], lay, bits, out=out_dev)
     else:
         sops.cnat_decode_batched(lv_dev.view(torch.int8), sg_dev, sc[:ntens], lay, out=out_dev)
-    on_cpu = [not p.data.is_cuda for _, p in items]
-    decoded = _hand_out(out_dev, lay, [p.data.shape for _, p in items], on_cpu, st, "d_out")
-    return {name: t for (name, _), t in zip(items, decoded)}
+    return lay, out_dev
 
 
 @_serialized
@@ -327,6 +349,37 @@ class _StochChannel(Channel):
             parts = [self._receive(QuantParameters({n: c.params[n] for n in rest}, 0))[0] for c in all_c_params]
             out.update(_aggregate_entries(rest, parts))
         return {n: out[n] for n in names}, time.perf_counter() - s_time
+
+    def receive_add_(self, c_params: CompressedParameters, targets: List[Parameters]) -> float:
+        """``on_client_receive(c_params)`` followed by ``add_parameters_inpace(t, decoded, 1, 1, False)`` for
+        every ``t`` in ``targets`` — the client pool's ``add_to_model`` / ``add_to_model_all``
+        (Src/ADFL/Client/pool.py:62-75) and QAFeL's hidden-state update (Src/ADFL/Server/qafel.py:176-179),
+        bit-identical to them. Returns the seconds spent.
+
+        Encoded tensors whose targets are all fp32 device tensors are decoded once, into device memory, and
+        added into every model there (no decoded tensor crosses PCIe). Everything else takes the reference's
+        route: decode, then ``mul_(1).add_(decoded, alpha=1)``."""
+        assert isinstance(c_params, QuantParameters)
+        for t in targets:
+            assert set(t.keys()) == set(c_params.params.keys())  # add_parameters_inpace, model.py:340
+        s_time = time.perf_counter()
+        fused = [n for n, p in c_params.params.items()
+                 if self._fusable(p) and all(t[n].is_cuda and t[n].dtype == torch.float32 for t in targets)]
+        if fused and targets:
+            dev = targets[0][fused[0]].device   # the staging's device (the current one) for the whole set
+            if dev.index == torch.cuda.current_device() and all(t[n].device == dev for t in targets for n in fused):
+                _decode_add_stoch([(n, c_params.params[n]) for n in fused], self.CODEC, self.bits,
+                                  [[t[n] for n in fused] for t in targets])
+            else:
+                fused = []
+        rest = QuantParameters({n: p for n, p in c_params.params.items() if n not in fused}, 0)
+        if rest.params:
+            decoded, _ = self.on_client_receive(rest)
+            with torch.no_grad():
+                for t in targets:
+                    for n, d in decoded.items():
+                        t[n].mul_(1).add_(d.to(t[n].device), alpha=1)
+        return time.perf_counter() - s_time
 
     @staticmethod
     def _fusable(p: QuantParameter) -> bool:

@@ -9,7 +9,9 @@ averaged in one HIP launch (adfl_stoch_dequantize_mean_batched).
 * the encoded tensors bit for bit against the oracle's decodes (oracle/stoch_oracle.py) summed in client
   order from zero, then / K, for every K;
 * all-zero tensors (the reference's norm == 0 payload), fp16 tensors (decoded to fp32), biases and int64
-  counters (aggregated as simple_aggregate does), device-resident payloads."""
+  counters (aggregated as simple_aggregate does), device-resident payloads;
+* receive_add_ (the client pool's add_to_model_all, QAFeL's hidden-state update): bit-identical to
+  on_client_receive + add_parameters_inpace (Src/ADFL/model.py:337-347) for device and host models."""
 
 import numpy as np
 import pytest
@@ -134,3 +136,33 @@ def test_receive_mean_errors():
     u2 = ch.on_client_send({"w": torch.randn(4, 5)})[0]
     with pytest.raises(RuntimeError):   # torch.stack of unequal shapes, as simple_aggregate raises
         ch.receive_mean([u1, u2])
+
+
+def add_parameters_inpace(model, delta):
+    """Src/ADFL/model.py:337-347 with alpha = beta = 1, to_float=False."""
+    with torch.no_grad():
+        for n in model:
+            model[n].mul_(1).add_(delta[n].to(model[n].device), alpha=1)
+
+
+@pytest.mark.parametrize("codec", list(CHANNELS))
+@pytest.mark.parametrize("where", ["cuda", "cpu"])
+def test_receive_add_matches_decode_then_add(codec, where):
+    cls, bits = CHANNELS[codec]
+    ch = cls(bits)
+    c_params = ch.on_server_send(_client(0))[0]
+    base = [_client(10 + m) for m in range(2)]
+    for m in base:
+        m["half.weight"] = m["half.weight"].float()   # models in fp32; the update was encoded from fp16
+    dev = torch.device(where, 0) if where == "cuda" else torch.device("cpu")
+    mine = [{n: t.clone().to(dev) if t.ndim > 1 else t.clone() for n, t in m.items()} for m in base]
+    ref = [{n: t.clone() for n, t in m.items()} for m in base]
+    t = ch.receive_add_(c_params, mine)
+    decoded = ch.on_client_receive(c_params)[0]
+    for m in ref:
+        add_parameters_inpace(m, decoded)
+    assert t > 0
+    for a, b in zip(mine, ref):
+        for n in b:
+            assert a[n].device.type == (where if b[n].ndim > 1 else "cpu"), n
+            assert np.array_equal(a[n].cpu().numpy().reshape(-1).view(np.uint8), b[n].numpy().reshape(-1).view(np.uint8)), n
