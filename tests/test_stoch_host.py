@@ -116,3 +116,23 @@ def test_rng_stream_is_seeded_from_torch():
     b = stoch.RngStream()
     assert a.seed == b.seed
     assert a.take(10) == (a.seed, 0) and a.take(1) == (a.seed, 3) and a.counter == 4
+
+
+@pytest.mark.parametrize("cls", [QSGDChannel, RQSGDChannel, CNATChannel], ids=lambda c: c.__name__)
+def test_receive_mean_and_add_without_encoded_entries_need_no_device(cls):
+    """Passthrough entries and empty matrices (the zero branch) aggregate and accumulate on the host as
+    simple_aggregate / add_parameters_inpace do (Src/ADFL/model.py:221-234, 337-347); no updates asserts."""
+    ch = cls(8)
+    ups = [ch.on_client_send({"b": torch.arange(5, dtype=torch.float32) * (k + 1), "w": torch.empty(0, 4),
+                              "n": torch.tensor(3 + k)})[0] for k in range(3)]
+    got, t = ch.receive_mean(ups)
+    assert t > 0 and list(got) == ["b", "w", "n"]
+    assert torch.equal(got["b"], torch.arange(5, dtype=torch.float32) * 2)
+    assert got["w"].shape == (0, 4) and got["w"].dtype == torch.float32
+    want_n = torch.sum(torch.stack([torch.tensor(3 + k) for k in range(3)]), dim=0) / 3   # true division: fp32
+    assert torch.equal(got["n"], want_n) and got["n"].dtype == want_n.dtype
+    with pytest.raises(AssertionError):
+        ch.receive_mean([])
+    model = {"b": torch.ones(5), "w": torch.zeros(0, 4), "n": torch.tensor(1)}
+    ch.receive_add_(ups[0], [model])
+    assert torch.equal(model["b"], torch.arange(5, dtype=torch.float32) + 1) and model["n"].item() == 4
