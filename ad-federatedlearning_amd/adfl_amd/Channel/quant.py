@@ -162,7 +162,13 @@ def _stage_in(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _DeviceSta
             _gather(tensors, lay, host)
             dev_buf.copy_(host, non_blocking=True)
     elif kinds == {True}:
-        _gather([t.to(st.device) for t in tensors], lay, dev_buf)
+        es = dev_buf.element_size()
+        if all(t.device == st.device and t.is_contiguous() and t.element_size() == es and t.numel() == n
+               for t, n in zip(tensors, lay.sizes.tolist())):
+            # one launch; quantized payloads read from their storage (checked just above)
+            ops.bucket_gather(tensors, lay, dev_buf, checked=False)
+        else:
+            _gather([t.to(st.device) for t in tensors], lay, dev_buf)
     else:  # mixed host / device dict: per-tensor copies (rare)
         for t, off, n in zip(tensors, lay.offsets.tolist(), lay.sizes.tolist()):
             dev_buf[off:off + n].view(t.shape).copy_(t)
@@ -220,6 +226,12 @@ def _hand_out(out_dev: torch.Tensor, lay: ops.BucketLayout, shapes: List[torch.S
         hostcopy.advise_huge(host_outs)
         pending.finish(host_outs)
         return host_outs
+    if not any(on_cpu) and out_dev.device == st.device:
+        # device dict: fresh owned tensors filled from the bucket by one launch (not one clone per tensor)
+        dev_outs = [torch.empty(s, dtype=out_dev.dtype, device=st.device) for s in shapes]
+        ops.bucket_scatter(out_dev, lay, dev_outs, checked=False)
+        torch.cuda.current_stream(st.device).synchronize()
+        return dev_outs
     for i, (off, n, s) in enumerate(zip(lay.offsets.tolist(), lay.sizes.tolist(), shapes)):
         if on_cpu[i]:  # mixed host / device dict (rare): per-tensor copies
             outs[i] = torch.empty(s, dtype=out_dev.dtype)
@@ -265,6 +277,13 @@ def _encode_dict(params: Parameters, names: List[str], bits: int, stats: Optiona
         return {name: (qt, sc) for name, qt, sc in zip(names, qs, scales)}
     torch.cuda.current_stream(dev).synchronize()
     scales = scales_host.tolist()
+    if not any(on_cpu) and all(t.device == dev for t in tensors):
+        # device dict: the qint8 payloads allocated (no launch each) and filled from the bucket by one launch
+        qs = [torch._empty_affine_quantized(t.shape, scale=sc, zero_point=0, dtype=torch.qint8, device=dev)
+              for t, sc in zip(tensors, scales)]
+        ops.bucket_scatter(q_dev, lay, qs, checked=False)
+        torch.cuda.current_stream(dev).synchronize()
+        return {name: (qt, sc) for name, qt, sc in zip(names, qs, scales)}
     out = {}
     offs, sizes = lay.offsets.tolist(), lay.sizes.tolist()
     for i, (name, t) in enumerate(zip(names, tensors)):
@@ -293,7 +312,10 @@ def _decode_dict(items: List[Tuple[str, torch.Tensor]]) -> Dict[str, torch.Tenso
     lay = st.layout(tuple(int(q.numel()) for _, q in items))
     # CPU qint8 payloads are gathered byte-wise straight from their storage; device ones through int8 views
     all_host = all(not q.is_cuda and q.is_contiguous() for _, q in items)
-    qs = [q if all_host else _int8_view(q) for _, q in items]
+    all_dev = all(q.is_cuda and q.device == dev and q.is_contiguous() for _, q in items)
+    # host payloads are gathered byte-wise from their storages, device ones by one gather launch: neither
+    # needs an int8 view object per tensor
+    qs = [q if all_host or all_dev else _int8_view(q) for _, q in items]
     q_dev = _stage_in(qs, lay, st, "dq", torch.int8)
     # q_scale() is a double; fbgemm's dequantize uses it as fp32 (quant.py:110), so round it the same way
     s_dev = torch.tensor([q.q_scale() for _, q in items], dtype=torch.float32).to(dev, non_blocking=True)

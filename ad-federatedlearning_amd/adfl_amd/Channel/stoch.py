@@ -34,7 +34,7 @@ from typing import Dict, List, Tuple
 
 import torch
 
-from .. import hostcopy
+from .. import hostcopy, ops
 from .. import stoch as sops
 from ..model import CompressedParameters, Parameters, QuantParameter, QuantParameters, get_parameter_info
 from .channel import Channel, IdentityChannel
@@ -58,6 +58,13 @@ def _owned(parts: List[torch.Tensor], shapes: List[torch.Size]) -> List[torch.Te
     """Per-tensor copies: each payload tensor owns its bytes (it is pickled on its own; the staging
     buffers are reused by the next call)."""
     return [p.view(s).clone() for p, s in zip(parts, shapes)]
+
+
+def _owned_dev(buf: torch.Tensor, lay, shapes: List[torch.Size]) -> List[torch.Tensor]:
+    """_owned for a device dict: fresh tensors filled from the bucket by one launch (ops.bucket_scatter)."""
+    outs = [torch.empty(s, dtype=buf.dtype, device=buf.device) for s in shapes]
+    ops.bucket_scatter(buf, lay, outs, checked=False)
+    return outs
 
 
 def _owned_host(buf: torch.Tensor, offsets, shapes: List[torch.Size]) -> List[torch.Tensor]:
@@ -132,8 +139,11 @@ def _encode_stoch(params: Parameters, names: List[str], codec: str, bits: int, u
     split = lambda buf: [p[:n] for p, n in zip(torch.split(buf, lay.padded.tolist()), sizes)]  # noqa: E731
     lv_parts = _owned_host(lv_h, lay.offsets, shapes) if any(on_cpu) else None
     sg_parts = _owned_host(sg_h, lay.offsets, shapes) if any(on_cpu) else None
-    lv_dev = _owned(split(lv), shapes) if not all(on_cpu) else None
-    sg_dev = _owned(split(sg), shapes) if not all(on_cpu) else None
+    if not any(on_cpu):   # device dict: one scatter launch per plane
+        lv_dev, sg_dev = _owned_dev(lv, lay, shapes), _owned_dev(sg, lay, shapes)
+    else:
+        lv_dev = _owned(split(lv), shapes) if not all(on_cpu) else None
+        sg_dev = _owned(split(sg), shapes) if not all(on_cpu) else None
     datas = [(lv_parts if cpu else lv_dev)[i] for i, cpu in enumerate(on_cpu)]
     signs = [(sg_parts if cpu else sg_dev)[i] for i, cpu in enumerate(on_cpu)]
     return _payloads(names, datas, signs, nm, lay.ntensors, codec)
@@ -172,8 +182,11 @@ def _encode_stoch_dt(params: Parameters, names: List[str], codec: str, bits: int
     split = lambda buf: [p[:n] for p, n in zip(torch.split(buf, lay.padded.tolist()), sizes)]  # noqa: E731
     lv_parts = _owned_host(lv_h, lay.offsets, shapes) if any(on_cpu) else None
     sg_parts = _owned_host(sg_h, lay.offsets, shapes) if any(on_cpu) else None
-    lv_dev = _owned(split(lv), shapes) if not all(on_cpu) else None
-    sg_dev = _owned(split(sg), shapes) if not all(on_cpu) else None
+    if not any(on_cpu):   # device dict: one scatter launch per plane
+        lv_dev, sg_dev = _owned_dev(lv, lay, shapes), _owned_dev(sg, lay, shapes)
+    else:
+        lv_dev = _owned(split(lv), shapes) if not all(on_cpu) else None
+        sg_dev = _owned(split(sg), shapes) if not all(on_cpu) else None
     datas = [(lv_parts if cpu else lv_dev)[i] for i, cpu in enumerate(on_cpu)]
     signs = [(sg_parts if cpu else sg_dev)[i] for i, cpu in enumerate(on_cpu)]
     return _payloads(names, datas, signs, nm, lay.ntensors, codec, dtype)

@@ -78,6 +78,8 @@ SIGNATURES = {
     "adfl_cnat_encode_batched": (INT, [P, P, I64, INT, P, U64, U64, P, I64, P, P, P, P]),
     "adfl_cnat_dequantize_batched": (INT, [P, P, P, I64, P, P, P]),
     "adfl_stoch_dequantize_mean_batched": (INT, [I32, P, P, I64, I32, P, I64, INT, P, P, I64, P, P]),
+    "adfl_bucket_gather": (INT, [P, P, I64, P, I32, P]),
+    "adfl_bucket_scatter": (INT, [P, P, I64, P, I32, P]),
     "adfl_qsgd_encode_batched_work": (INT, [P, P, I64, P, I64, INT, P, U64, U64, P, I64, P, P, P, P]),
     "adfl_rqsgd_encode_batched_work": (INT, [P, P, I64, P, I64, INT, P, U64, U64, P, I64, P, P, P, P, P]),
     "adfl_cnat_encode_batched_work": (INT, [P, P, I64, P, I64, INT, P, U64, U64, P, I64, P, P, P, P]),

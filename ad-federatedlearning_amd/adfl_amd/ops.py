@@ -319,6 +319,52 @@ def qerror_batched_int4(flat: torch.Tensor, packed: torch.Tensor, scales: torch.
     return tuple(partials.view(-1, 4).sum(0).tolist())
 
 
+def _bucket_ptr_table(tensors, layout: BucketLayout, bucket: torch.Tensor, what: str, checked: bool) -> torch.Tensor:
+    """Device int64 table of the tensors' data pointers, after checking them against the layout and bucket
+    (checked=False: tensors the caller has just allocated to match, as the Channel's outputs are)."""
+    dev = bucket.device
+    if len(tensors) != layout.ntensors:
+        raise ValueError(f"{what}: {len(tensors)} tensors for a layout of {layout.ntensors}")
+    if checked:
+        es = bucket.element_size()
+        for t, (x, n) in enumerate(zip(tensors, layout.sizes.tolist())):
+            if (not x.is_cuda or x.device != dev or not x.is_contiguous() or x.numel() != n
+                    or x.element_size() != es):
+                raise ValueError(f"{what}: tensor {t} must be a contiguous {es}-byte-element tensor of {n} "
+                                 f"elements on {dev}")
+    return torch.tensor([x.data_ptr() for x in tensors], dtype=torch.int64).to(dev, non_blocking=True)
+
+
+def _check_bucket(bucket: torch.Tensor, layout: BucketLayout, what: str) -> torch.Tensor:
+    bucket = _dev(bucket, "bucket")
+    if not bucket.is_contiguous() or bucket.numel() < layout.total or bucket.element_size() not in (1, 2, 4, 8):
+        raise ValueError(f"{what}: the bucket must be a contiguous device tensor of >= {layout.total} elements "
+                         "of 1, 2, 4 or 8 bytes")
+    return bucket
+
+
+def bucket_gather(tensors, layout: BucketLayout, bucket: torch.Tensor, *, checked: bool = True) -> torch.Tensor:
+    """Copy every tensor into its slot of the device bucket (tensor t at layout.offsets[t]), one launch
+    (adfl_bucket_gather). Tensors: contiguous, on the bucket's device, of its element size (any dtype,
+    quantized included); pads between slots are left as they are."""
+    bucket = _check_bucket(bucket, layout, "bucket_gather")
+    table = _bucket_ptr_table(tensors, layout, bucket, "bucket_gather", checked)
+    check(_lib.load().adfl_bucket_gather(bucket.data_ptr(), layout.device_chunks(bucket.device).data_ptr(),
+                                         layout.nchunks, table.data_ptr(), bucket.element_size(),
+                                         _stream(bucket.device)))
+    return bucket
+
+
+def bucket_scatter(bucket: torch.Tensor, layout: BucketLayout, tensors, *, checked: bool = True) -> None:
+    """Copy every slot of the device bucket into its own tensor (tensor t from layout.offsets[t]), one launch
+    (adfl_bucket_scatter): the owned per-tensor outputs of a bucketed decode or encode."""
+    bucket = _check_bucket(bucket, layout, "bucket_scatter")
+    table = _bucket_ptr_table(tensors, layout, bucket, "bucket_scatter", checked)
+    check(_lib.load().adfl_bucket_scatter(bucket.data_ptr(), layout.device_chunks(bucket.device).data_ptr(),
+                                          layout.nchunks, table.data_ptr(), bucket.element_size(),
+                                          _stream(bucket.device)))
+
+
 def dequantize_add_batched(q: torch.Tensor, scales: torch.Tensor, layout: BucketLayout, targets) -> None:
     """In place, for every model k and tensor t: targets[k][t] += fp32(scales[t] * q_t) (fp32 add) — decode
     once, accumulate into K device-resident models (Src/ADFL/Client/pool.py:62-75, model.py:337-347).

@@ -211,6 +211,17 @@ int adfl_slq_dequantize_add_batched(const int8_t* d_q, const adfl_slq_chunk* d_c
                                     const float* d_scales, float* const* d_targets, int32_t ntensors,
                                     int32_t ntargets, void* stream);
 
+/* Device staging of a state dict as one bucket (the gather / scatter around every bucketed entry above when
+ * the dict's tensors live on the device; the reference's per-tensor loop, quant.py:67-94, has one tensor per
+ * op): every tensor's elements copied between its own storage and its slot of the bucket, one launch for the
+ * whole dict. d_srcs / d_dsts[t] (a device array of nt pointers) is tensor t's first element, contiguous,
+ * elem_bytes (1, 2, 4 or 8) per element; the bucket holds tensor t at its chunks' offsets (elements).
+ * Bytes outside every chunk (an aligned bucket's pads) are neither read nor written. Any alignment. */
+int adfl_bucket_gather(void* d_bucket, const adfl_slq_chunk* d_chunks, int64_t nchunks, const void* const* d_srcs,
+                       int32_t elem_bytes, void* stream);
+int adfl_bucket_scatter(const void* d_bucket, const adfl_slq_chunk* d_chunks, int64_t nchunks, void* const* d_dsts,
+                        int32_t elem_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
