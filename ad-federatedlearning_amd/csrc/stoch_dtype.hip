@@ -16,9 +16,11 @@
 // rounded to the dtype; fp64 squares accumulated in fp64. Returned as fp64 (exactly the dtype's value).
 // Decode is the fp32 codecs' (the reference decodes to fp32 with scale = fp32(norm)).
 //
-// These tensors are rare in ADFL (models train in fp32), so the kernels are plain: one 256-thread block per
-// chunk, each thread one 16-byte vector of x per step (8 fp16 / bf16 or 2 fp64 elements; two Philox blocks
-// or one), kBatch steps' loads in flight, scalar head / tail elements around the vectors.
+// These tensors are rare in ADFL (models train in fp32), so the kernels keep one simple shape: one 256-thread
+// block per chunk, each thread one 16-byte vector of x per step (8 fp16 / bf16 or 2 fp64 elements; two
+// Philox blocks or one), kBatch steps' loads in flight, scalar head / tail elements around the vectors.
+// QSGD / RQSGD: norm partials, per-tensor finalize, quantize (x read twice). CNAT: quantize + partials in one
+// read of x, finalize, zero-norm fix-up; its band tables in LDS and its exponent carried as an integer.
 
 #include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
