@@ -361,3 +361,69 @@ def philox_uniforms_dt(dtype: torch.dtype, n: int, seed: int, counter: int, star
     check(_lib.load().adfl_philox_uniforms_dt(DT_DTYPES[dtype], out.data_ptr(), n, start, seed & (2 ** 64 - 1),
                                               counter, _stream(dev)))
     return out
+
+
+# ------------------------------------------------------------------------------------------------
+# torch.ops.adfl stochastic ops over caller-placed tensors (offsets / sizes: host int64, as the SLQ batched
+# ops take them, ops.layout_for): QSGDChannel / RQSGDChannel / CNATChannel's per-tensor loops
+# (quant.py:223-252, :364-398, :509-545) as traceable ops. Positions no tensor owns are zero.
+# ------------------------------------------------------------------------------------------------
+def _check_codec(codec: str) -> None:
+    if codec not in _CODEC_IDS:
+        raise ValueError(f"adfl stochastic ops: codec must be one of {sorted(_CODEC_IDS)}, got {codec!r}")
+
+
+@torch.library.custom_op("adfl::stoch_encode_batched", mutates_args=())
+def stoch_encode_batched_op(flat: torch.Tensor, offsets: torch.Tensor, sizes: torch.Tensor, codec: str, bits: int,
+                            seed: int, counter: int) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
+    """(levels — uint8, CNAT: int8 exponents —, signs int8, norms f32, mins f32 — RQSGD's min|x|, else 0) of
+    an fp32 flat buffer; uniforms from the Philox stream (seed, counter)."""
+    from .ops import _filled, layout_for
+    _check_codec(codec)
+    lay = layout_for(offsets, sizes)
+    flat = flat.reshape(-1)
+    if flat.numel() < lay.total:
+        raise ValueError("stoch_encode_batched: flat buffer smaller than the layout")
+    dev = flat.device
+    lv = _filled(flat.numel(), torch.int8 if codec == "cnat" else torch.uint8, dev, lay)
+    sg = _filled(flat.numel(), torch.int8, dev, lay)
+    mins = torch.zeros(lay.ntensors, dtype=torch.float32, device=dev)
+    if codec == "qsgd":
+        lv, sg, nr = qsgd_encode_batched(flat, lay, bits, seed=seed, counter=counter, levels=lv, signs=sg)
+    elif codec == "rqsgd":
+        lv, sg, nr, mins = rqsgd_encode_batched(flat, lay, bits, seed=seed, counter=counter, levels=lv, signs=sg,
+                                                mins=mins)
+    else:
+        lv, sg, nr = cnat_encode_batched(flat, lay, bits, seed=seed, counter=counter, exps=lv, signs=sg)
+    return lv, sg, nr, mins
+
+
+@stoch_encode_batched_op.register_fake
+def _(flat, offsets, sizes, codec, bits, seed, counter):
+    n, t = flat.numel(), sizes.numel()
+    return (flat.new_empty((n,), dtype=torch.int8 if codec == "cnat" else torch.uint8),
+            flat.new_empty((n,), dtype=torch.int8), flat.new_empty((t,), dtype=torch.float32),
+            flat.new_empty((t,), dtype=torch.float32))
+
+
+@torch.library.custom_op("adfl::stoch_decode_batched", mutates_args=())
+def stoch_decode_batched_op(levels: torch.Tensor, signs: torch.Tensor, norms: torch.Tensor, mins: torch.Tensor,
+                            offsets: torch.Tensor, sizes: torch.Tensor, codec: str, bits: int) -> torch.Tensor:
+    """fp32 decode of stoch_encode_batched's planes (mins used by RQSGD only)."""
+    from .ops import _filled, layout_for
+    _check_codec(codec)
+    lay = layout_for(offsets, sizes)
+    levels, signs = levels.reshape(-1), signs.reshape(-1)
+    if levels.numel() < lay.total or signs.numel() < lay.total:
+        raise ValueError("stoch_decode_batched: planes smaller than the layout")
+    out = _filled(levels.numel(), torch.float32, levels.device, lay)
+    if codec == "qsgd":
+        return qsgd_decode_batched(levels.view(torch.uint8), signs, norms, lay, bits, out=out)
+    if codec == "rqsgd":
+        return rqsgd_decode_batched(levels.view(torch.uint8), signs, norms, mins, lay, bits, out=out)
+    return cnat_decode_batched(levels.view(torch.int8), signs, norms, lay, out=out)
+
+
+@stoch_decode_batched_op.register_fake
+def _(levels, signs, norms, mins, offsets, sizes, codec, bits):
+    return levels.new_empty((levels.numel(),), dtype=torch.float32)

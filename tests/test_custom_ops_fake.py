@@ -13,7 +13,8 @@ from adfl_amd import ops
 A = torch.ops.adfl
 OPS = ["slq_absmax", "slq_encode", "slq_decode", "slq_encode_int4", "slq_decode_int4", "slq_encode_batched",
        "slq_decode_batched", "slq_encode_batched_int4", "slq_decode_batched_int4", "pack_int4", "unpack_int4",
-       "slq_dequantize_mean", "slq_dequantize_mean_batched", "slq_dequantize_mean_batched_int4"]
+       "slq_dequantize_mean", "slq_dequantize_mean_batched", "slq_dequantize_mean_batched_int4",
+       "stoch_encode_batched", "stoch_decode_batched"]
 
 
 def test_every_op_is_registered():
@@ -51,6 +52,12 @@ def test_fake_shapes_and_dtypes():
         prow = mode.from_tensor(torch.empty(4, 64, dtype=torch.uint8))
         mb4 = A.slq_dequantize_mean_batched_int4(prow, mode.from_tensor(torch.empty(4, 3)), off, siz, 107, -1, None)
         assert mb4.shape == (107,) and mb4.dtype == torch.float32
+        for codec in ("qsgd", "rqsgd", "cnat"):
+            lv, sg, nr, mn = A.stoch_encode_batched(flat, off, siz, codec, 8, 7, 0)
+            assert lv.shape == (107,) and lv.dtype == (torch.int8 if codec == "cnat" else torch.uint8)
+            assert sg.dtype == torch.int8 and nr.shape == (3,) and mn.shape == (3,)
+            d = A.stoch_decode_batched(lv, sg, nr, mn, off, siz, codec, 8)
+            assert d.shape == (107,) and d.dtype == torch.float32
 
 
 def test_caller_placed_layout():

@@ -194,6 +194,57 @@ def test_opcheck(case):
     torch.library.opcheck(op, args)
 
 
+@pytest.mark.parametrize("codec", ["qsgd", "rqsgd", "cnat"])
+@pytest.mark.parametrize("gap", [0, 3])
+def test_stoch_ops_match_the_bucket_api(codec, gap):
+    """torch.ops.adfl.stoch_encode_batched / stoch_decode_batched over caller-placed tensors equal the
+    adfl_amd.stoch bucket calls on the same layout and Philox stream byte for byte (those are pinned to the
+    reference's fixtures and the oracle in tests/test_gpu_stoch.py); positions no tensor owns are zero."""
+    from adfl_amd import ops, stoch
+    flat, off, siz = _bucket(21, [3, 4097, 900, 8192], gap)
+    x = torch.from_numpy(flat).to(DEV)
+    lv, sg, nr, mn = A.stoch_encode_batched(x, off, siz, codec, 8, 1234, 5)
+    lay = ops.layout_for(off, siz)
+    if codec == "qsgd":
+        want = stoch.qsgd_encode_batched(x, lay, 8, seed=1234, counter=5)
+        wdec = stoch.qsgd_decode_batched(want[0], want[1], want[2], lay, 8)
+    elif codec == "rqsgd":
+        want = stoch.rqsgd_encode_batched(x, lay, 8, seed=1234, counter=5)
+        wdec = stoch.rqsgd_decode_batched(want[0], want[1], want[2], want[3], lay, 8)
+    else:
+        want = stoch.cnat_encode_batched(x, lay, 8, seed=1234, counter=5)
+        wdec = stoch.cnat_decode_batched(want[0], want[1], want[2], lay)
+    d = A.stoch_decode_batched(lv, sg, nr, mn, off, siz, codec, 8)
+    owned = torch.zeros(x.numel(), dtype=torch.bool, device=DEV)
+    for o, n in zip(off.tolist(), siz.tolist()):
+        owned[o:o + n] = True
+    w = owned[:lay.total]                      # the bucket calls' planes end at the layout's last element
+    assert torch.equal(lv[owned].view(torch.uint8), want[0][w].view(torch.uint8))
+    assert torch.equal(sg[owned], want[1][w]) and torch.equal(nr, want[2])
+    assert torch.equal(d[owned].view(torch.int32), wdec[w].view(torch.int32))
+    if codec == "rqsgd":
+        assert torch.equal(mn, want[3])
+    if gap:
+        assert not lv[~owned].any() and not sg[~owned].any() and not d[~owned].any()
+
+
+@pytest.mark.parametrize("codec", ["qsgd", "rqsgd", "cnat"])
+def test_stoch_ops_opcheck_and_compile(codec):
+    flat, off, siz = _bucket(8, [3, 4097, 900], 2)
+    x = torch.from_numpy(flat).to(DEV)
+    torch.library.opcheck(A.stoch_encode_batched, (x, off, siz, codec, 8, 99, 0))
+    lv, sg, nr, mn = A.stoch_encode_batched(x, off, siz, codec, 8, 99, 0)
+    torch.library.opcheck(A.stoch_decode_batched, (lv, sg, nr, mn, off, siz, codec, 8))
+
+    def pipeline(x):
+        e = torch.ops.adfl.stoch_encode_batched(x, off, siz, codec, 8, 99, 0)
+        return torch.ops.adfl.stoch_decode_batched(*e, off, siz, codec, 8)
+
+    eager = pipeline(x)
+    compiled = torch.compile(pipeline, backend="aot_eager", fullgraph=True)(x)
+    assert torch.equal(eager.view(torch.int32), compiled.view(torch.int32))
+
+
 def test_codec_pipeline_under_torch_compile():
     """encode -> decode -> mean of a bucketed update traced by torch.compile (fullgraph: every op goes through
     its fake implementation at trace time, the HIP kernels at run time) equals eager bit for bit."""
