@@ -1,5 +1,5 @@
-"""cProfile of SLQChannel on a device-resident ResNet-18-sized state dict (what tools/prof_channel_device.py
-times): where the host-side time of a device round trip goes, by function."""
+"""cProfile of SLQChannel on a ResNet-18-sized state dict — device-resident (what tools/prof_channel_device.py
+times), or with --host a CPU dict (ADFL's own call pattern): where the host-side time goes, by function."""
 import cProfile
 import io
 import os
@@ -15,7 +15,7 @@ RESNET18 = 11_689_512
 
 
 def main():
-    dev = torch.device("cuda", 0)
+    dev = torch.device("cpu") if "--host" in sys.argv else torch.device("cuda", 0)
     base, rem = divmod(RESNET18, 256)
     params = {}
     for i in range(256):
@@ -24,14 +24,17 @@ def main():
     ch = SLQChannel(8)
     for _ in range(3):
         ch.on_server_receive(ch.on_client_send(params)[0])
-    pr = cProfile.Profile()
-    pr.enable()
-    for _ in range(10):
-        ch.on_server_receive(ch.on_client_send(params)[0])
-    pr.disable()
-    s = io.StringIO()
-    pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(18)
-    print(s.getvalue())
+    qp = ch.on_client_send(params)[0]
+    for what, fn in (("encode", lambda: ch.on_client_send(params)), ("decode", lambda: ch.on_server_receive(qp))):
+        pr = cProfile.Profile()
+        pr.enable()
+        for _ in range(10):
+            fn()
+        pr.disable()
+        s = io.StringIO()
+        pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(14)
+        print("==", what)
+        print(s.getvalue())
 
 
 if __name__ == "__main__":
