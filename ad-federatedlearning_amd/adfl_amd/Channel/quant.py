@@ -358,7 +358,11 @@ def _stage_rows(clients: List[List[torch.Tensor]], lay: ops.BucketLayout, st: _D
         for r, c in enumerate(clients):
             hostcopy.copy_pieces(*_range_copies(_ptrs(c), lay, host[r].data_ptr(), 1, 0, lay.total, to_bucket=True))
             dev[r].copy_(host[r], non_blocking=True)
-    else:  # device (or mixed) payloads: per-tensor copies into the device rows
+    elif all(t.device == st.device and t.is_contiguous() and t.element_size() == 1 and t.numel() == n
+             for c in clients for t, n in zip(c, lay.sizes.tolist())):
+        for r, c in enumerate(clients):   # device payloads: one gather launch per client row
+            ops.bucket_gather(c, lay, dev[r], checked=False)
+    else:  # mixed payloads: per-tensor copies into the device rows
         for r, c in enumerate(clients):
             for t, off, n in zip(c, lay.offsets.tolist(), lay.sizes.tolist()):
                 dev[r, off:off + n].copy_(_byte_view(t).reshape(-1).to(st.device))
