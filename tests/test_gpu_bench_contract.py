@@ -37,7 +37,7 @@ def test_bench_emits_one_contract_line():
     assert d["cpu_baseline"] is None  # --no-cpu-baseline
     # the receiver-side round trip: absmax + quantize + a decode whose payload is not in the Infinity Cache
     cr = d["cold_round_trip"]
-    assert abs(cr["kernel_ms"] - (d["kernels_ms"]["absmax"] + d["kernels_ms"]["quantize"] + d["decode_cold_ms"])) < 2e-4
+    assert abs(cr["kernel_ms"] - (d["kernels_ms"]["absmax"] + d["kernels_ms"]["quantize"] + d["decode_cold_ms"])) < 2.5e-4  # four 4-decimal roundings
     assert 0.0 < cr["frac"] < 1.0 and cr["GiB_per_s"] > 0
 
 
