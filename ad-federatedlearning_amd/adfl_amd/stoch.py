@@ -377,7 +377,10 @@ def _check_codec(codec: str) -> None:
 def stoch_encode_batched_op(flat: torch.Tensor, offsets: torch.Tensor, sizes: torch.Tensor, codec: str, bits: int,
                             seed: int, counter: int) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
     """(levels — uint8, CNAT: int8 exponents —, signs int8, norms f32, mins f32 — RQSGD's min|x|, else 0) of
-    an fp32 flat buffer; uniforms from the Philox stream (seed, counter)."""
+    a flat buffer; uniforms from the Philox stream (seed, counter). fp32 buffers take the fp32 kernels;
+    fp16 / bf16 / fp64 ones are encoded in their own dtype's arithmetic, as the reference computes them
+    (encode_batched_dt), and their norms / mins come back as the fp32 values the decode multiplies by (the
+    channels' Python-float norm as an fp32 scalar; exact for fp16 / bf16 norms)."""
     from .ops import _filled, layout_for
     _check_codec(codec)
     lay = layout_for(offsets, sizes)
@@ -388,6 +391,9 @@ def stoch_encode_batched_op(flat: torch.Tensor, offsets: torch.Tensor, sizes: to
     lv = _filled(flat.numel(), torch.int8 if codec == "cnat" else torch.uint8, dev, lay)
     sg = _filled(flat.numel(), torch.int8, dev, lay)
     mins = torch.zeros(lay.ntensors, dtype=torch.float32, device=dev)
+    if flat.dtype in DT_DTYPES:
+        lv, sg, nr, mn = encode_batched_dt(codec, flat, lay, bits, seed=seed, counter=counter, levels=lv, signs=sg)
+        return lv, sg, nr.float(), (mn.float() if mn is not None else mins)
     if codec == "qsgd":
         lv, sg, nr = qsgd_encode_batched(flat, lay, bits, seed=seed, counter=counter, levels=lv, signs=sg)
     elif codec == "rqsgd":

@@ -58,6 +58,10 @@ def test_fake_shapes_and_dtypes():
             assert sg.dtype == torch.int8 and nr.shape == (3,) and mn.shape == (3,)
             d = A.stoch_decode_batched(lv, sg, nr, mn, off, siz, codec, 8)
             assert d.shape == (107,) and d.dtype == torch.float32
+        for dt in (torch.float16, torch.bfloat16, torch.float64):   # encoded in their own dtype's arithmetic
+            lv, sg, nr, mn = A.stoch_encode_batched(mode.from_tensor(torch.empty(107, dtype=dt)), off, siz, "cnat",
+                                                    8, 7, 0)
+            assert lv.shape == (107,) and lv.dtype == torch.int8 and nr.dtype == torch.float32
 
 
 def test_caller_placed_layout():

@@ -229,6 +229,38 @@ def test_stoch_ops_match_the_bucket_api(codec, gap):
 
 
 @pytest.mark.parametrize("codec", ["qsgd", "rqsgd", "cnat"])
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16, torch.float64])
+def test_stoch_ops_dtype_buckets(codec, dtype):
+    """fp16 / bf16 / fp64 buffers through torch.ops.adfl.stoch_encode_batched are encoded in their own dtype's
+    arithmetic: planes equal adfl_amd.stoch.encode_batched_dt on the same layout and Philox stream (pinned to
+    the reference's fp16 / bf16 / fp64 fixtures in tests/test_gpu_stoch_dt.py); norms / mins come back as the
+    fp32 values the decode uses, and the decode op equals the fp32 decode with them."""
+    from adfl_amd import ops, stoch
+    flat, off, siz = _bucket(33, [3, 4097, 900, 8192], 3)
+    x = torch.from_numpy(flat).to(DEV).to(dtype)
+    lv, sg, nr, mn = A.stoch_encode_batched(x, off, siz, codec, 8, 4321, 2)
+    lay = ops.layout_for(off, siz)
+    wl, ws_, wn, wm = stoch.encode_batched_dt(codec, x, lay, 8, seed=4321, counter=2)
+    owned = torch.zeros(x.numel(), dtype=torch.bool, device=DEV)
+    for o, n in zip(off.tolist(), siz.tolist()):
+        owned[o:o + n] = True
+    w = owned[:lay.total]
+    assert torch.equal(lv[owned].view(torch.uint8), wl[w].view(torch.uint8)) and torch.equal(sg[owned], ws_[w])
+    assert nr.dtype == torch.float32 and torch.equal(nr, wn.float())
+    assert torch.equal(mn, wm.float()) if codec == "rqsgd" else not mn.any()
+    assert not lv[~owned].any() and not sg[~owned].any()
+    d = A.stoch_decode_batched(lv, sg, nr, mn, off, siz, codec, 8)
+    if codec == "qsgd":
+        wdec = stoch.qsgd_decode_batched(wl.view(torch.uint8), ws_, wn.float(), lay, 8)
+    elif codec == "rqsgd":
+        wdec = stoch.rqsgd_decode_batched(wl.view(torch.uint8), ws_, wn.float(), wm.float(), lay, 8)
+    else:
+        wdec = stoch.cnat_decode_batched(wl.view(torch.int8), ws_, wn.float(), lay)
+    assert torch.equal(d[owned].view(torch.int32), wdec[w].view(torch.int32))
+    torch.library.opcheck(A.stoch_encode_batched, (x, off, siz, codec, 8, 99, 0))
+
+
+@pytest.mark.parametrize("codec", ["qsgd", "rqsgd", "cnat"])
 def test_stoch_ops_opcheck_and_compile(codec):
     flat, off, siz = _bucket(8, [3, 4097, 900], 2)
     x = torch.from_numpy(flat).to(DEV)
