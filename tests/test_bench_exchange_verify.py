@@ -1,4 +1,4 @@
-"""CPU, world_size 2 (gloo): bench.py's self-check of the N > 1 exchange leg (exchange_verify) — the
+"""CPU, world_size 2 and 4 (gloo): bench.py's self-check of the N > 1 exchange leg (exchange_verify) — the
 fingerprints of every gathered row against its sender's, the own row byte for byte, and the
 exact_self=False mean bit-identical on every rank (Examples/ray_ad.py:188) — driven with the oracle codec
 in place of the HIP codec, plus a rank whose received row is corrupted: every rank must then report
@@ -8,6 +8,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -48,13 +49,13 @@ def _worker(rank, world, port, corrupt, q):
         q.put((rank, f"error {e!r}\n{traceback.format_exc()}"))
 
 
-def _run(corrupt):
+def _run(corrupt, world=2):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, corrupt, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, corrupt, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in procs)
@@ -65,14 +66,17 @@ def _run(corrupt):
     return res
 
 
-def test_exchange_verify_passes_on_a_clean_exchange():
-    res = _run(corrupt=False)
+@pytest.mark.parametrize("world", [2, 4])
+def test_exchange_verify_passes_on_a_clean_exchange(world):
+    res = _run(corrupt=False, world=world)
+    assert sorted(res) == list(range(world))
     for rank, checks in res.items():
         for c in checks:
             assert c["parity"] and c["own_row_equal"] and c["mean_identical_on_all_ranks"], (rank, c)
             assert c["rows_mismatched"] == []
-    # both ranks hold the identical exact_self=False mean
-    assert [c["mean_fingerprint"] for c in res[0]] == [c["mean_fingerprint"] for c in res[1]]
+    # every rank holds the identical exact_self=False mean
+    for r in range(1, world):
+        assert [c["mean_fingerprint"] for c in res[0]] == [c["mean_fingerprint"] for c in res[r]]
 
 
 def test_exchange_verify_flags_a_corrupted_row_on_every_rank():
