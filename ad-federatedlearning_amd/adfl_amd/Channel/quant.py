@@ -31,7 +31,7 @@ from typing import Dict, List, Optional, Tuple
 import numpy as np
 import torch
 
-from .. import hostcopy, ops
+from .. import hostcopy, ops, sum_order
 from ..model import (CompressedParameters, Parameters, QuantParameter, QuantParameters, get_parameter_info)
 from .channel import Channel, IdentityChannel
 
@@ -379,8 +379,8 @@ def _byte_view(t: torch.Tensor) -> torch.Tensor:
 @_serialized
 def _decode_mean(clients: List[List[torch.Tensor]], scales: List[List[float]], shapes: List[torch.Size],
                  packed: bool) -> List[torch.Tensor]:
-    """The fp32 mean over K clients of their decoded tensors, tensor by tensor, in client order, in ONE
-    launch (ops.dequantize_mean_batched): clients[k][j] is client k's payload for tensor j (a qint8 tensor,
+    """The fp32 mean over K clients of their decoded tensors, tensor by tensor, in torch's CPU summation
+    order for simple_aggregate (csrc/torch_sum_order.h), in ONE launch (ops.dequantize_mean_batched): clients[k][j] is client k's payload for tensor j (a qint8 tensor,
     or ceil(n/2) packed int8 bytes with packed=True), scales[k][j] its scale. Returns one
     owned tensor per entry (CPU when every client's payload is on the CPU)."""
     st = _staging()
@@ -405,40 +405,43 @@ def _simple_aggregate(values: List[torch.Tensor]) -> torch.Tensor:
         return torch.sum(torch.stack(values, dim=0), dim=0) / len(values)
 
 
-_SUM_GRAIN = 32768  # torch's intra-op grain size: smaller reductions run on one thread
-
-
 def _aggregate_entries(names: List[str], parts: List[Parameters]) -> Dict[str, torch.Tensor]:
     """simple_aggregate over the entries `names` of the K dicts `parts` (host tensors: biases, running
     statistics, counters), with the per-entry call's values but not its per-entry dispatch cost (256
-    biases: about 3 ms of stack / sum / div). Entries of one dtype are concatenated and summed with K
-    elementwise adds from zero, then divided and split into owned tensors, where that provably equals each
-    entry's own torch.sum(torch.stack(...), 0): int64 (integer sums are exact in any order), and fp32 entries
-    below torch's grain size for K <= 4 (one thread, and torch's CPU sum over dim 0 adds up to 4 rows in row
-    order from zero at every column, vector body and scalar tail alike; from 5 rows it regroups the tail
-    columns, so there each entry is summed on its own). A single concatenated torch.sum is no substitute:
-    its order depends on the combined size (and [4, 17000] took 40 ms on 8 threads)."""
+    biases: about 3 ms of stack / sum / div). Entries of one dtype are concatenated into K rows and summed
+    together: int64 with K elementwise adds (integer sums are exact in any order), fp32 in torch's own CPU
+    summation order (adfl_amd.sum_order: each entry's columns in the order its own
+    torch.sum(torch.stack(...), 0) takes, bit for bit; checked against torch once per process,
+    sum_order.self_check). Then one division and a split into owned tensors. One-element fp32 entries at
+    K >= 8 (torch's inner-sum kernel) and everything else go through simple_aggregate per entry."""
     k = len(parts)
     res: Dict[str, torch.Tensor] = {}
     groups: Dict[torch.dtype, List[str]] = {}
+    f32_ok = sum_order.self_check()
     for n in names:
         vals = [p[n] for p in parts]
         t0 = vals[0]
         if not all(isinstance(v, torch.Tensor) and not v.is_cuda and v.is_contiguous() and v.dtype == t0.dtype
                    and v.shape == t0.shape for v in vals):
             continue
-        if t0.dtype == torch.int64 or (t0.dtype == torch.float32 and k <= 4 and t0.numel() < _SUM_GRAIN):
+        if t0.dtype == torch.int64 or (t0.dtype == torch.float32 and f32_ok and t0.numel() > 0
+                                       and not (t0.numel() == 1 and k >= 8)):
             groups.setdefault(t0.dtype, []).append(n)
     with torch.no_grad():
-        for ns in groups.values():
+        for dt, ns in groups.items():
             if len(ns) < 2:
                 continue
-            rows = [torch.cat([t if t.dim() == 1 else t.reshape(-1) for t in (p[n] for n in ns)]) for p in parts]
-            acc = torch.zeros_like(rows[0])
-            for r in rows:
-                acc = acc + r
+            sizes = [parts[0][n].numel() for n in ns]
+            if dt == torch.int64:
+                rows = [torch.cat([p[n].reshape(-1) for n in ns]) for p in parts]
+                acc = torch.zeros_like(rows[0])
+                for r in rows:
+                    acc = acc + r
+            else:
+                stacked = torch.stack([torch.cat([p[n].reshape(-1) for n in ns]) for p in parts])
+                acc = sum_order.sum_rows(stacked, sizes)
             agg = acc / k
-            for n, piece in zip(ns, torch.split(agg, [parts[0][n].numel() for n in ns])):
+            for n, piece in zip(ns, torch.split(agg, sizes)):
                 shape = parts[0][n].shape
                 res[n] = (piece if piece.shape == shape else piece.view(shape)).clone()
     for n in names:
@@ -581,11 +584,12 @@ class SLQChannel(Channel):
 
         Tensors quantized in every update are decoded and averaged on the device in one launch: the K
         payloads are read once and no decoded copy is materialised (ops.dequantize_mean_batched). Their
-        mean is the fp32 sum in client order, then / K: bit-identical to simple_aggregate on CPU tensors
-        (as the reference runs it, model.py:195-197) for K <= 4; for K >= 5 torch's CPU sum regroups the
-        additions (multi-accumulator tails, cascade levels), and torch's GPU sum groups them its own way,
-        so there the two agree to fp32 summation error. Everything else (biases, running statistics,
-        non-quantized payloads) is decoded and aggregated as the reference does, on the host."""
+        mean is summed in torch's CPU order for ``torch.sum(torch.stack(...), dim=0)`` (csrc/torch_sum_order.h:
+        per tensor, a 16-row cascade over the SEQ columns, four interleaved partials over each tensor's last
+        n % 32 elements), then / K correctly rounded: bit-identical to simple_aggregate on CPU tensors (as
+        the reference runs it, model.py:195-197) for every K (tests/golden/aggregate.npz: the reference
+        executed at K = 1 .. 64). Everything else (biases, running statistics, non-quantized payloads) is
+        decoded and aggregated as the reference does, on the host, in the same order."""
         if not all_c_params:
             raise AssertionError("receive_mean: no updates")   # simple_aggregate asserts len > 0
         for c in all_c_params:

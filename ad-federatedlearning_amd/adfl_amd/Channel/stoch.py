@@ -342,9 +342,10 @@ class _StochChannel(Channel):
         Src/ADFL/model.py:221-234). Returns (aggregate, seconds).
 
         Entries encoded in every update are decoded and averaged on the device in one launch (each client's
-        level and sign planes read once, no decoded copy materialised): the fp32 sum in client order from
-        zero, then / K, bit-identical to simple_aggregate of the decoded CPU tensors for K <= 4 (torch's CPU
-        sum regroups from K = 5: fp32 summation error). Everything else (biases, running statistics, empty
+        level and sign planes read once, no decoded copy materialised): summed in torch's CPU order for
+        ``torch.sum(torch.stack(...), dim=0)`` (csrc/torch_sum_order.h), then / K, bit-identical to
+        simple_aggregate of the decoded CPU tensors at every K (tests/golden/aggregate.npz: the reference's
+        own payloads and aggregates at K = 5, 8, 16, 20). Everything else (biases, running statistics, empty
         tensors) is decoded and aggregated as the reference does, on the host."""
         if not all_c_params:
             raise AssertionError("receive_mean: no updates")   # simple_aggregate asserts len > 0

@@ -60,6 +60,48 @@ def _dev(t: torch.Tensor, what: str) -> torch.Tensor:
     return t
 
 
+def _f32_on(t: torch.Tensor, n: int, dev: torch.device, what: str) -> torch.Tensor:
+    """An fp32 tensor of >= n elements on `dev` as a contiguous, 16-byte aligned device view (scales, self_x):
+    a host tensor, another device, another dtype or a short tensor raises instead of reaching a kernel."""
+    if not isinstance(t, torch.Tensor) or not t.is_cuda or t.device != dev:
+        raise ValueError(f"adfl_amd.ops: {what} must be a device tensor on {dev}, got "
+                         f"{getattr(t, 'device', type(t).__name__)}")
+    if t.dtype != torch.float32:
+        raise ValueError(f"adfl_amd.ops: {what} must be float32, got {t.dtype}")
+    if t.numel() < n:
+        raise ValueError(f"adfl_amd.ops: {what} needs >= {n} elements, got {t.numel()}")
+    return _dev(t, what)
+
+
+def _scale_rows(scales: torch.Tensor, k: int, ncols: int, dev: torch.device, what: str) -> torch.Tensor:
+    """K rows of >= ncols fp32 scales with unit column stride (row r's scale for tensor t at [r, t])."""
+    if not isinstance(scales, torch.Tensor) or not scales.is_cuda or scales.device != dev:
+        raise ValueError(f"adfl_amd.ops: {what} must be a device tensor on {dev}")
+    if scales.dtype != torch.float32:
+        raise ValueError(f"adfl_amd.ops: {what} must be float32, got {scales.dtype}")
+    if scales.numel() % k:
+        raise ValueError(f"adfl_amd.ops: {what} has {scales.numel()} elements, not a multiple of K = {k}")
+    sc = scales.reshape(k, -1)
+    if sc.shape[1] < ncols:
+        raise ValueError(f"adfl_amd.ops: {what} must be [K, >= {ncols}] fp32")
+    if sc.stride(1) != 1 or sc.data_ptr() % 4:
+        sc = sc.contiguous()
+    return sc
+
+
+def _dst(out: Optional[torch.Tensor], n: int, dtype: torch.dtype, dev: torch.device, what: str,
+         zero: bool = False, align: int = 16) -> torch.Tensor:
+    """A caller's output tensor checked (contiguous, `align`-byte aligned, dtype, >= n elements, on dev), or a
+    new one."""
+    if out is None:
+        return (torch.zeros if zero else torch.empty)(n, dtype=dtype, device=dev)
+    if (not out.is_cuda or out.device != dev or out.dtype != dtype or not out.is_contiguous()
+            or out.numel() < n or out.data_ptr() % align):
+        raise ValueError(f"adfl_amd.ops: {what} must be a contiguous, {align}-byte aligned {dtype} tensor of "
+                         f">= {n} elements on {dev}")
+    return out
+
+
 def new_workspace(device) -> torch.Tensor:
     return torch.empty(_lib.workspace_bytes(), dtype=torch.uint8, device=device)
 
@@ -84,8 +126,9 @@ def encode(x: torch.Tensor, bits: int, *, q: Optional[torch.Tensor] = None, scal
     """quant.py:97-104 on the device: returns (int8 payload shaped like x, fp32 scale of shape [1])."""
     require_quantizable(x)
     x = _dev(x, "x")
-    q = torch.empty(x.shape, dtype=torch.int8, device=x.device) if q is None else q
-    scale = torch.empty(1, dtype=torch.float32, device=x.device) if scale is None else scale
+    q = torch.empty(x.shape, dtype=torch.int8, device=x.device) if q is None else \
+        _dst(q, x.numel(), torch.int8, x.device, "q")
+    scale = _dst(scale, 1, torch.float32, x.device, "scale", align=4)
     ws = new_workspace(x.device) if workspace is None else workspace
     check(_lib.load().adfl_slq_encode(x.data_ptr(), x.numel(), bits, q.data_ptr(), scale.data_ptr(), ws.data_ptr(),
                                       ws.numel(), _stream(x.device)))
@@ -97,7 +140,9 @@ def decode(q: torch.Tensor, scale: torch.Tensor, *, out: Optional[torch.Tensor] 
     q = _dev(q, "q")
     if q.dtype != torch.int8:
         raise TypeError(f"adfl_amd.ops.decode: payload must be int8, got {q.dtype}")
-    out = torch.empty(q.shape, dtype=torch.float32, device=q.device) if out is None else out
+    out = torch.empty(q.shape, dtype=torch.float32, device=q.device) if out is None else \
+        _dst(out, q.numel(), torch.float32, q.device, "out")
+    scale = _f32_on(scale, 1, q.device, "scale")
     check(_lib.load().adfl_slq_dequantize(q.data_ptr(), q.numel(), scale.data_ptr(), out.data_ptr(),
                                           _stream(q.device)))
     return out
@@ -110,8 +155,8 @@ def encode_int4(x: torch.Tensor, bits: int = 4, *, packed: Optional[torch.Tensor
     require_quantizable(x)
     x = _dev(x, "x")
     n = x.numel()
-    packed = torch.empty((n + 1) // 2, dtype=torch.uint8, device=x.device) if packed is None else packed
-    scale = torch.empty(1, dtype=torch.float32, device=x.device) if scale is None else scale
+    packed = _dst(packed, (n + 1) // 2, torch.uint8, x.device, "packed")
+    scale = _dst(scale, 1, torch.float32, x.device, "scale", align=4)
     ws = new_workspace(x.device) if workspace is None else workspace
     check(_lib.load().adfl_slq_encode_int4(x.data_ptr(), n, bits, packed.data_ptr(), scale.data_ptr(),
                                            ws.data_ptr(), ws.numel(), _stream(x.device)))
@@ -122,7 +167,10 @@ def decode_int4(packed: torch.Tensor, n: int, scale: torch.Tensor, *,
                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """unpack_4bit (compression.py:51-66) fused with dequantize: fp32 [n]."""
     packed = _dev(packed, "packed")
-    out = torch.empty(n, dtype=torch.float32, device=packed.device) if out is None else out
+    if packed.numel() * packed.element_size() < (n + 1) // 2:
+        raise ValueError(f"decode_int4: {n} elements need {(n + 1) // 2} packed bytes")
+    out = _dst(out, n, torch.float32, packed.device, "out")
+    scale = _f32_on(scale, 1, packed.device, "scale")
     check(_lib.load().adfl_slq_dequantize_int4(packed.data_ptr(), n, scale.data_ptr(), out.data_ptr(),
                                                _stream(packed.device)))
     return out
@@ -148,23 +196,30 @@ def unpack_int4(packed: torch.Tensor, shape: Sequence[int]) -> torch.Tensor:
 
 def dequantize_mean(q_rows: torch.Tensor, scales: torch.Tensor, n: int, *,
                     out: Optional[torch.Tensor] = None, self_row: int = -1,
-                    self_x: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Mean over K int8 payload rows (Examples/ray_ad.py:188): q_rows is [K, row_bytes] int8 (row_bytes >= n,
-    16-byte multiple), scales is [K] or [K, stride] fp32 (column 0 used). With self_row >= 0 that row is
-    replaced by the receiver's own fp32 update self_x, added last and exactly (async_peer.py:170-174)."""
-    if q_rows.dim() != 2 or q_rows.dtype != torch.int8 or not q_rows.is_contiguous():
-        raise ValueError("dequantize_mean: q_rows must be a contiguous [K, row_bytes] int8 tensor")
+                    self_x: Optional[torch.Tensor] = None, packed: bool = False) -> torch.Tensor:
+    """Mean over K payload rows of one n-element tensor (Examples/ray_ad.py:188; simple_aggregate,
+    Src/ADFL/model.py:221-234), summed in torch's CPU order (csrc/torch_sum_order.h), then / K: q_rows is
+    [K, row_bytes] int8 (row_bytes >= n, a 16-byte multiple) — or, packed=True, uint8 int4-packed rows
+    (row_bytes >= ceil(n/2), compression.py:35-48) — and scales is [K] or [K, stride] fp32 (column 0). With
+    self_row >= 0 that row is replaced by the receiver's own fp32 update self_x, added last and exactly
+    (async_peer.py:170-174)."""
+    dt = torch.uint8 if packed else torch.int8
+    if q_rows.dim() != 2 or q_rows.dtype != dt or not q_rows.is_contiguous() or not q_rows.is_cuda:
+        raise ValueError(f"dequantize_mean: q_rows must be a contiguous [K, row_bytes] {dt} device tensor")
     k, row = q_rows.shape
-    sc = scales.reshape(k, -1)
+    dev = q_rows.device
+    if row < ((n + 1) // 2 if packed else n):
+        raise ValueError("dequantize_mean: rows shorter than the tensor")
+    sc = _scale_rows(scales, k, 1, dev, "scales")
     xp = None
     if self_row >= 0:
-        self_x = _dev(self_x, "self_x")
-        if self_x.dtype != torch.float32 or self_x.numel() != n or not self_x.is_contiguous():
+        self_x = _f32_on(self_x, n, dev, "self_x")
+        if self_x.numel() != n:
             raise ValueError("dequantize_mean: self_x must be a contiguous fp32 tensor of n elements")
         xp = self_x.data_ptr()
-    out = torch.empty(n, dtype=torch.float32, device=q_rows.device) if out is None else out
-    check(_lib.load().adfl_slq_dequantize_mean_self(q_rows.data_ptr(), row, k, n, sc.data_ptr(), sc.stride(0),
-                                                    self_row, xp, out.data_ptr(), _stream(q_rows.device)))
+    out = _dst(out, n, torch.float32, dev, "out")
+    fn = _lib.load().adfl_slq_dequantize_mean_self_int4 if packed else _lib.load().adfl_slq_dequantize_mean_self
+    check(fn(q_rows.data_ptr(), row, k, n, sc.data_ptr(), sc.stride(0), self_row, xp, out.data_ptr(), _stream(dev)))
     return out
 
 
@@ -269,9 +324,9 @@ def encode_batched(flat: torch.Tensor, layout: BucketLayout, bits: int, *, q: Op
     if flat.numel() < layout.total:
         raise ValueError("encode_batched: flat buffer smaller than the layout")
     dev = flat.device
-    q = torch.empty(layout.total, dtype=torch.int8, device=dev) if q is None else q
-    scales = torch.empty(layout.ntensors, dtype=torch.float32, device=dev) if scales is None else scales
-    partials = torch.empty(layout.nchunks, dtype=torch.int32, device=dev) if partials is None else partials
+    q = _dst(q, layout.total, torch.int8, dev, "q")
+    scales = _dst(scales, layout.ntensors, torch.float32, dev, "scales", align=4)
+    partials = _dst(partials, layout.nchunks, torch.int32, dev, "partials", align=4)
     lib, st = _lib.load(), _stream(dev)
     nwork = 0 if _encode_mode() == "twopass" else layout.nwork
     check(lib.adfl_slq_encode_batched_work(flat.data_ptr(), layout.device_chunks(dev).data_ptr(),
@@ -286,7 +341,10 @@ def decode_batched(q: torch.Tensor, scales: torch.Tensor, layout: BucketLayout, 
     """Decode a bucketed int8 payload with per-tensor scales (quant.py:67-71)."""
     q = _dev(q, "q")
     dev = q.device
-    out = torch.empty(layout.total, dtype=torch.float32, device=dev) if out is None else out
+    if q.numel() * q.element_size() < layout.total:
+        raise ValueError("decode_batched: payload smaller than the layout")
+    out = _dst(out, layout.total, torch.float32, dev, "out")
+    scales = _f32_on(scales, layout.ntensors, dev, "scales")
     check(_lib.load().adfl_slq_dequantize_batched(q.data_ptr(), layout.device_chunks(dev).data_ptr(),
                                                   layout.nchunks, scales.data_ptr(), out.data_ptr(), _stream(dev)))
     return out
@@ -298,6 +356,7 @@ def qerror_batched(flat: torch.Tensor, q: torch.Tensor, scales: torch.Tensor,
     sums (synchronises: returns Python floats)."""
     flat, q = _dev(flat, "flat"), _dev(q, "q")
     dev = flat.device
+    scales = _f32_on(scales, layout.ntensors, dev, "scales")
     partials = torch.empty(layout.nchunks * 4, dtype=torch.float64, device=dev)
     check(_lib.load().adfl_slq_qerror_batched(flat.data_ptr(), q.data_ptr(), layout.device_chunks(dev).data_ptr(),
                                               layout.nchunks, scales.data_ptr(), partials.data_ptr(),
@@ -312,6 +371,7 @@ def qerror_batched_int4(flat: torch.Tensor, packed: torch.Tensor, scales: torch.
     if (layout.offsets % 2).any():
         raise ValueError("qerror_batched_int4: tensor offsets must be even (an int4 bucket layout)")
     dev = flat.device
+    scales = _f32_on(scales, layout.ntensors, dev, "scales")
     partials = torch.empty(layout.nchunks * 4, dtype=torch.float64, device=dev)
     check(_lib.load().adfl_slq_qerror_batched_int4(flat.data_ptr(), packed.data_ptr(),
                                                    layout.device_chunks(dev).data_ptr(), layout.nchunks,
@@ -386,7 +446,7 @@ def dequantize_add_batched(q: torch.Tensor, scales: torch.Tensor, layout: Bucket
             ptrs.append(x.data_ptr())
     table = torch.tensor(ptrs, dtype=torch.int64).to(dev, non_blocking=True)
     check(_lib.load().adfl_slq_dequantize_add_batched(q.data_ptr(), layout.device_chunks(dev).data_ptr(),
-                                                      layout.nchunks, _dev(scales, "scales").data_ptr(),
+                                                      layout.nchunks, _f32_on(scales, layout.ntensors, dev, "scales").data_ptr(),
                                                       table.data_ptr(), layout.ntensors, len(targets),
                                                       _stream(dev)))
     # `table` may be freed on return: the caching allocator only reuses it for later work on this stream
@@ -404,26 +464,20 @@ def dequantize_mean_batched(q_rows: torch.Tensor, scales: torch.Tensor, layout: 
     PackedSLQChannel exchange. Returns the flat fp32 bucket; positions outside every tensor are zero when
     `out` is None (left untouched otherwise)."""
     dt = torch.uint8 if packed else torch.int8
-    if q_rows.dim() != 2 or q_rows.dtype != dt or not q_rows.is_contiguous():
-        raise ValueError(f"dequantize_mean_batched: q_rows must be a contiguous [K, row_bytes] {dt} tensor")
+    if q_rows.dim() != 2 or q_rows.dtype != dt or not q_rows.is_contiguous() or not q_rows.is_cuda:
+        raise ValueError(f"dequantize_mean_batched: q_rows must be a contiguous [K, row_bytes] {dt} device tensor")
     k, row = q_rows.shape
     if packed:
         _require_even_offsets(layout)
     if row < ((layout.total + 1) // 2 if packed else layout.total):
         raise ValueError("dequantize_mean_batched: rows shorter than the bucket layout")
-    sc = scales.reshape(k, -1)
-    if sc.shape[1] < layout.ntensors or sc.dtype != torch.float32:
-        raise ValueError("dequantize_mean_batched: scales must be fp32 [K, >= ntensors]")
     dev = q_rows.device
+    sc = _scale_rows(scales, k, layout.ntensors, dev, "scales")
     xp = None
     if self_row >= 0:
-        self_x = _dev(self_x, "self_x")
-        if self_x.dtype != torch.float32 or self_x.numel() < layout.total:
-            raise ValueError("dequantize_mean_batched: self_x must be an fp32 bucket of the layout")
+        self_x = _f32_on(self_x, layout.total, dev, "self_x")
         xp = self_x.data_ptr()
-    out = torch.zeros(layout.total, dtype=torch.float32, device=dev) if out is None else out
-    if out.dtype != torch.float32 or out.numel() < layout.total or not out.is_contiguous():
-        raise ValueError("dequantize_mean_batched: out must be a contiguous fp32 bucket of the layout")
+    out = _dst(out, layout.total, torch.float32, dev, "out", zero=True)
     fn = _lib.load().adfl_slq_dequantize_mean_batched_int4 if packed else _lib.load().adfl_slq_dequantize_mean_batched
     check(fn(q_rows.data_ptr(), row, k, layout.device_chunks(dev).data_ptr(), layout.nchunks, sc.data_ptr(),
              sc.stride(0), self_row, xp, out.data_ptr(), _stream(dev)))
@@ -447,12 +501,9 @@ def encode_batched_int4(flat: torch.Tensor, layout: BucketLayout, bits: int = 4,
     if flat.numel() < layout.total:
         raise ValueError("encode_batched_int4: flat buffer smaller than the layout")
     dev = flat.device
-    packed = torch.empty((layout.total + 1) // 2, dtype=torch.uint8, device=dev) if packed is None else packed
-    scales = torch.empty(layout.ntensors, dtype=torch.float32, device=dev) if scales is None else scales
-    partials = torch.empty(layout.nchunks, dtype=torch.int32, device=dev) if partials is None else partials
-    if packed.numel() < (layout.total + 1) // 2 or scales.numel() < layout.ntensors or \
-            partials.numel() < layout.nchunks:
-        raise ValueError("encode_batched_int4: packed / scales / partials smaller than the layout needs")
+    packed = _dst(packed, (layout.total + 1) // 2, torch.uint8, dev, "packed")
+    scales = _dst(scales, layout.ntensors, torch.float32, dev, "scales", align=4)
+    partials = _dst(partials, layout.nchunks, torch.int32, dev, "partials", align=4)
     check(_lib.load().adfl_slq_encode_batched_int4_work(flat.data_ptr(), layout.device_chunks(dev).data_ptr(),
                                                         layout.nchunks, layout.device_work(dev).data_ptr(),
                                                         layout.nwork, bits, packed.data_ptr(), scales.data_ptr(),
@@ -466,9 +517,10 @@ def decode_batched_int4(packed: torch.Tensor, scales: torch.Tensor, layout: Buck
     _require_even_offsets(layout)
     packed = _dev(packed, "packed")
     dev = packed.device
-    out = torch.empty(layout.total, dtype=torch.float32, device=dev) if out is None else out
-    if packed.numel() < (layout.total + 1) // 2 or out.numel() < layout.total or scales.numel() < layout.ntensors:
+    if packed.numel() * packed.element_size() < (layout.total + 1) // 2:
         raise ValueError("decode_batched_int4: packed / scales / out smaller than the layout needs")
+    out = _dst(out, layout.total, torch.float32, dev, "out")
+    scales = _f32_on(scales, layout.ntensors, dev, "scales")
     check(_lib.load().adfl_slq_dequantize_batched_int4(packed.data_ptr(), layout.device_chunks(dev).data_ptr(),
                                                        layout.nchunks, scales.data_ptr(), out.data_ptr(),
                                                        _stream(dev)))

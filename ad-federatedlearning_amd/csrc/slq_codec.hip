@@ -35,6 +35,7 @@
 #include <cstring>
 
 #include "adfl_slq.h"
+#include "torch_sum_order.h"
 
 namespace {
 
@@ -431,10 +432,29 @@ __global__ __launch_bounds__(kBlock) void k_unpack_int4(const uint8_t* __restric
   }
 }
 
-// Peer-exchange epilogue: mean of K dequantized int8 rows, rows summed in order (fp32), then / K.
-// Per row: one coalesced 16-byte load per lane + LDS transpose; output: coalesced NT float4 stores.
-// self_row >= 0: that row is skipped and the rank's own fp32 update self_x is added LAST instead, exactly
+// Peer-exchange epilogue / synchronous aggregate: mean of K dequantized rows in torch's summation order
+// (torch_sum_order.h: the CPU sum(stack(rows), dim=0) that stack(...).mean(0) at ray_ad.py:188 and
+// simple_aggregate at model.py:229-231 compute), then a correctly rounded division by K. The row sequence is
+// rows r != self_row in r order, then (self_row >= 0) the rank's own fp32 update self_x, exactly, LAST
 // (async_peer.py:170-174 / ray_ad.py:183-188 append the local parameters after the received updates).
+// Vector tiles are SEQ-order columns of the one tensor (a tile ends below n & ~31); the < 1024 tail elements
+// take each element's own order. Per row: one coalesced 16-byte load per lane + LDS transpose; output:
+// coalesced NT float4 stores. DEEP: K >= 256 (the cascade's levels 2-3).
+__device__ __forceinline__ int seq_row(int s, int self_row) { return (self_row >= 0 && s >= self_row) ? s + 1 : s; }
+
+// Element e of the rows, summed in torch's order for tensor-relative index j of an n-element tensor.
+template <class Dequant>
+__device__ __forceinline__ float mean_elem_torch(const Dequant& dq, int k, int self_row,
+                                                 const float* __restrict__ self_x, int64_t e, int64_t j, int64_t n,
+                                                 double dk) {
+  auto get = [&](int s) -> float {
+    if (self_row >= 0 && s == k - 1) return self_x[e];
+    return dq(seq_row(s, self_row), e);
+  };
+  return (float)((double)adfl_sum::sum_elem(get, k, adfl_sum::mode_of(j, n, k)) / dk);
+}
+
+template <bool DEEP>
 __global__ __launch_bounds__(kBlock) void k_dequantize_mean(const int8_t* __restrict__ q, int64_t row_stride, int k,
                                                             int64_t n, const float* __restrict__ scales,
                                                             int64_t scale_stride, int self_row,
@@ -446,8 +466,8 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_mean(const int8_t* __rest
   const int64_t wstride = (int64_t)gridDim.x * kWaves;
   const double dk = (double)k;
   for (int64_t t = (int64_t)blockIdx.x * kWaves + wave; t < ntiles; t += wstride) {
-    float4 acc[4];
-    bool first = true;
+    adfl_sum::SeqTile<4, DEEP> acc;
+    acc.init();
     for (int r = 0; r < k; ++r) {
       if (r == self_row) continue;
       const uint4* q16 = reinterpret_cast<const uint4*>(q + r * row_stride) + t * (kTile / 16);
@@ -455,41 +475,29 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_mean(const int8_t* __rest
       reinterpret_cast<uint4*>(lds[wave])[lane] = q16[lane];
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float4 v = dequant4(lds[wave][j * 64 + lane], s);
-        acc[j] = first ? v : add4(acc[j], v);
-      }
+      for (int j = 0; j < 4; ++j) acc.add(j, dequant4(lds[wave][j * 64 + lane], s));
       __builtin_amdgcn_wave_barrier();
-      first = false;
+      acc.step();
     }
     if (self_row >= 0) {
       const float4* xs = reinterpret_cast<const float4*>(self_x) + t * (kTile / 4);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float4 v = xs[j * 64 + lane];
-        acc[j] = first ? v : add4(acc[j], v);
-      }
+      for (int j = 0; j < 4; ++j) acc.add(j, xs[j * 64 + lane]);
+      acc.step();
     }
     float4* o4 = reinterpret_cast<float4*>(out) + t * (kTile / 4);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) store4_nt(o4 + j * 64 + lane, div4(acc[j], dk));
+    for (int j = 0; j < 4; ++j) store4_nt(o4 + j * 64 + lane, div4(acc.result(j), dk));
   }
-  if (blockIdx.x == gridDim.x - 1)
-    for (int64_t i = ntiles * kTile + threadIdx.x; i < n; i += kBlock) {
-      float acc = 0.0f;
-      bool first = true;
-      for (int r = 0; r < k; ++r) {
-        if (r == self_row) continue;
-        const float d = scales[r * scale_stride] * (float)q[r * row_stride + i];
-        acc = first ? d : acc + d;
-        first = false;
-      }
-      if (self_row >= 0) acc = first ? self_x[i] : acc + self_x[i];
-      out[i] = (float)((double)acc / dk);
-    }
+  if (blockIdx.x == gridDim.x - 1) {
+    auto dq = [&](int r, int64_t e) -> float { return scales[r * scale_stride] * (float)q[r * row_stride + e]; };
+    for (int64_t i = ntiles * kTile + threadIdx.x; i < n; i += kBlock)
+      out[i] = mean_elem_torch(dq, k, self_row, self_x, i, i, n, dk);
+  }
 }
 
 // Same over K int4-packed rows (2048-element wave tiles, 1 KiB of packed bytes per row per tile).
+template <bool DEEP>
 __global__ __launch_bounds__(kBlock) void k_dequantize_mean_int4(const uint8_t* __restrict__ p, int64_t row_stride,
                                                                  int k, int64_t n, const float* __restrict__ scales,
                                                                  int64_t scale_stride, int self_row,
@@ -501,8 +509,8 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_mean_int4(const uint8_t* 
   const int64_t wstride = (int64_t)gridDim.x * kWaves;
   const double dk = (double)k;
   for (int64_t t = (int64_t)blockIdx.x * kWaves + wave; t < ntiles; t += wstride) {
-    float4 acc[8];
-    bool first = true;
+    adfl_sum::SeqTile<8, DEEP> acc;
+    acc.init();
     for (int r = 0; r < k; ++r) {
       if (r == self_row) continue;
       const uint4* p16 = reinterpret_cast<const uint4*>(p + r * row_stride) + t * 64;
@@ -510,40 +518,29 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_mean_int4(const uint8_t* 
       reinterpret_cast<uint4*>(lds[wave])[lane] = p16[lane];
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float4 v = dequant2_int4(lds[wave][j * 64 + lane], s);
-        acc[j] = first ? v : add4(acc[j], v);
-      }
+      for (int j = 0; j < 8; ++j) acc.add(j, dequant2_int4(lds[wave][j * 64 + lane], s));
       __builtin_amdgcn_wave_barrier();
-      first = false;
+      acc.step();
     }
     if (self_row >= 0) {
       const float4* xs = reinterpret_cast<const float4*>(self_x) + t * (kTile4 / 4);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float4 v = xs[j * 64 + lane];
-        acc[j] = first ? v : add4(acc[j], v);
-      }
+      for (int j = 0; j < 8; ++j) acc.add(j, xs[j * 64 + lane]);
+      acc.step();
     }
     float4* o4 = reinterpret_cast<float4*>(out) + t * (kTile4 / 4);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) store4_nt(o4 + j * 64 + lane, div4(acc[j], dk));
+    for (int j = 0; j < 8; ++j) store4_nt(o4 + j * 64 + lane, div4(acc.result(j), dk));
   }
-  if (blockIdx.x == gridDim.x - 1)
-    for (int64_t i = ntiles * kTile4 + threadIdx.x; i < n; i += kBlock) {
-      float acc = 0.0f;
-      bool first = true;
-      for (int r = 0; r < k; ++r) {
-        if (r == self_row) continue;
-        float e0, e1;
-        dequant_byte_int4(p[r * row_stride + (i >> 1)], scales[r * scale_stride], e0, e1);
-        const float d = (i & 1) ? e1 : e0;
-        acc = first ? d : acc + d;
-        first = false;
-      }
-      if (self_row >= 0) acc = first ? self_x[i] : acc + self_x[i];
-      out[i] = (float)((double)acc / dk);
-    }
+  if (blockIdx.x == gridDim.x - 1) {
+    auto dq = [&](int r, int64_t e) -> float {
+      float e0, e1;
+      dequant_byte_int4(p[r * row_stride + (e >> 1)], scales[r * scale_stride], e0, e1);
+      return (e & 1) ? e1 : e0;
+    };
+    for (int64_t i = ntiles * kTile4 + threadIdx.x; i < n; i += kBlock)
+      out[i] = mean_elem_torch(dq, k, self_row, self_x, i, i, n, dk);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -836,26 +833,31 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_batched(const int8_t* __r
 
 // Peer mean of K bucketed payloads with per-tensor scales — the decentralized exchange of a whole state dict
 // under SLQChannel's per-tensor codec (ray_ad.py:164-190 averaging every tensor; quant.py:74-94 giving each
-// tensor its own scale): for tensor t and element i of the bucket,
-//   out[i] = fp32(sum over rows r != self_row, in r order, of fp32(scale_r[t] * q_r[i]), then + self_x[i]) / K
-// with the division correctly rounded, exactly k_dequantize_mean's arithmetic per tensor. Row r's payload is
-// q + r * row_stride (one bucket payload each, the same layout), its scales scales + r * scale_stride.
-// One block per chunk: the < 16 head elements and the tail element-wise, wave tiles in between.
-__device__ __forceinline__ float mean_elem(const int8_t* __restrict__ q, int64_t row_stride, int k,
-                                           const float* __restrict__ scales, int64_t scale_stride, int tensor,
-                                           int self_row, const float* __restrict__ self_x, int64_t e, double dk) {
-  float acc = 0.0f;
-  bool first = true;
-  for (int r = 0; r < k; ++r) {
-    if (r == self_row) continue;
-    const float d = scales[r * scale_stride + tensor] * (float)q[r * row_stride + e];
-    acc = first ? d : acc + d;
-    first = false;
-  }
-  if (self_row >= 0) acc = first ? self_x[e] : acc + self_x[e];
-  return (float)((double)acc / dk);
+// tensor its own scale), and SLQChannel.receive_mean (simple_aggregate over K decoded dicts, model.py:221-234):
+// for tensor t and element i of the bucket, the torch-order sum (torch_sum_order.h, per tensor: the column
+// index is i's offset in its tensor) of fp32(scale_r[t] * q_r[i]) over the row sequence (rows != self_row in
+// r order, then self_x[i]), then / K correctly rounded — k_dequantize_mean's arithmetic per tensor. Row r's
+// payload is q + r * row_stride (one bucket payload each, the same layout), its scales
+// scales + r * scale_stride. One block per chunk: wave tiles over the chunk's SEQ columns (16-element aligned
+// in the bucket), the < 16 head elements and everything past the tiles element-wise in each one's order.
+struct TensorSpan {
+  int64_t start, n;  // the chunk's tensor: bucket offset and element count
+};
+__device__ __forceinline__ TensorSpan tensor_span(const adfl_slq_chunk* __restrict__ chunks, const adfl_slq_chunk& c) {
+  TensorSpan t;
+  t.start = chunks[c.first_chunk].start;
+  t.n = (int64_t)(c.nchunks - 1) * ADFL_SLQ_CHUNK_ELEMS + chunks[c.first_chunk + c.nchunks - 1].len;
+  return t;
 }
 
+// wave tiles of `tile` elements the chunk can take: from `head` up to the tensor's last SEQ column
+__device__ __forceinline__ int seq_tiles(const adfl_slq_chunk& c, const TensorSpan& ts, int head, int tile) {
+  int64_t lim = ts.start + adfl_sum::seq_end(ts.n) - c.start;  // chunk-relative end of the SEQ columns
+  lim = lim < c.len ? lim : c.len;
+  return lim > head ? (int)((lim - head) / tile) : 0;
+}
+
+template <bool DEEP>
 __global__ __launch_bounds__(kBlock) void k_dequantize_mean_batched(const int8_t* __restrict__ q, int64_t row_stride,
                                                                     int k, const adfl_slq_chunk* __restrict__ chunks,
                                                                     const float* __restrict__ scales,
@@ -864,17 +866,22 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_mean_batched(const int8_t
                                                                     float* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kWaves][kTile / 4];
   const adfl_slq_chunk c = chunks[blockIdx.x];
+  const TensorSpan ts = tensor_span(chunks, c);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const double dk = (double)k;
   const int head = chunk_head(c.start, c.len, 16);
-  if ((int)threadIdx.x < head)
-    out[c.start + threadIdx.x] =
-        mean_elem(q, row_stride, k, scales, scale_stride, c.tensor, self_row, self_x, c.start + threadIdx.x, dk);
-  const int ntiles = (c.len - head) / kTile;
+  const int ntiles = seq_tiles(c, ts, head, kTile);
+  auto dq = [&](int r, int64_t e) -> float {
+    return scales[r * scale_stride + c.tensor] * (float)q[r * row_stride + e];
+  };
+  if ((int)threadIdx.x < head) {
+    const int64_t e = c.start + threadIdx.x;
+    out[e] = mean_elem_torch(dq, k, self_row, self_x, e, e - ts.start, ts.n, dk);
+  }
   for (int t = wave; t < ntiles; t += kWaves) {
     const int64_t base = c.start + head + (int64_t)t * kTile;  // 16-element aligned
-    float4 acc[4];
-    bool first = true;
+    adfl_sum::SeqTile<4, DEEP> acc;
+    acc.init();
     for (int r = 0; r < k; ++r) {
       if (r == self_row) continue;
       const uint4* q16 = reinterpret_cast<const uint4*>(q + r * row_stride + base);
@@ -882,67 +889,54 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_mean_batched(const int8_t
       reinterpret_cast<uint4*>(lds[wave])[lane] = q16[lane];
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float4 v = dequant4(lds[wave][j * 64 + lane], s);
-        acc[j] = first ? v : add4(acc[j], v);
-      }
+      for (int j = 0; j < 4; ++j) acc.add(j, dequant4(lds[wave][j * 64 + lane], s));
       __builtin_amdgcn_wave_barrier();
-      first = false;
+      acc.step();
     }
     if (self_row >= 0) {
       const float4* xs = reinterpret_cast<const float4*>(self_x + base);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float4 v = xs[j * 64 + lane];
-        acc[j] = first ? v : add4(acc[j], v);
-      }
+      for (int j = 0; j < 4; ++j) acc.add(j, xs[j * 64 + lane]);
+      acc.step();
     }
     float4* o4 = reinterpret_cast<float4*>(out + base);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) store4_nt(o4 + j * 64 + lane, div4(acc[j], dk));
+    for (int j = 0; j < 4; ++j) store4_nt(o4 + j * 64 + lane, div4(acc.result(j), dk));
   }
-  for (int i = head + ntiles * kTile + threadIdx.x; i < c.len; i += kBlock)
-    out[c.start + i] = mean_elem(q, row_stride, k, scales, scale_stride, c.tensor, self_row, self_x, c.start + i, dk);
+  for (int i = head + ntiles * kTile + threadIdx.x; i < c.len; i += kBlock) {
+    const int64_t e = c.start + i;
+    out[e] = mean_elem_torch(dq, k, self_row, self_x, e, e - ts.start, ts.n, dk);
+  }
 }
 
 // The same mean over K int4-packed bucket payloads (PackedSLQChannel per tensor; encode_batched_int4's
 // layout: even tensor offsets, flat element e in byte e/2, high nibble for even e). Heads run to a 32-element
 // (16-byte) boundary, wave tiles are kTile4 = 2048 elements = 1 KiB of packed bytes per row.
-__device__ __forceinline__ float mean_elem_int4(const uint8_t* __restrict__ p, int64_t row_stride, int k,
-                                                const float* __restrict__ scales, int64_t scale_stride, int tensor,
-                                                int self_row, const float* __restrict__ self_x, int64_t e,
-                                                double dk) {
-  float acc = 0.0f;
-  bool first = true;
-  for (int r = 0; r < k; ++r) {
-    if (r == self_row) continue;
-    float e0, e1;
-    dequant_byte_int4(p[r * row_stride + (e >> 1)], scales[r * scale_stride + tensor], e0, e1);
-    const float d = (e & 1) ? e1 : e0;
-    acc = first ? d : acc + d;
-    first = false;
-  }
-  if (self_row >= 0) acc = first ? self_x[e] : acc + self_x[e];
-  return (float)((double)acc / dk);
-}
-
+template <bool DEEP>
 __global__ __launch_bounds__(kBlock) void k_dequantize_mean_batched_int4(
     const uint8_t* __restrict__ p, int64_t row_stride, int k, const adfl_slq_chunk* __restrict__ chunks,
     const float* __restrict__ scales, int64_t scale_stride, int self_row, const float* __restrict__ self_x,
     float* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint16_t lds[kWaves][kTile4 / 4];
   const adfl_slq_chunk c = chunks[blockIdx.x];
+  const TensorSpan ts = tensor_span(chunks, c);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const double dk = (double)k;
   const int head = chunk_head(c.start, c.len, 32);
-  if ((int)threadIdx.x < head)
-    out[c.start + threadIdx.x] = mean_elem_int4(p, row_stride, k, scales, scale_stride, c.tensor, self_row, self_x,
-                                                c.start + threadIdx.x, dk);
-  const int ntiles = (c.len - head) / kTile4;
+  const int ntiles = seq_tiles(c, ts, head, kTile4);
+  auto dq = [&](int r, int64_t e) -> float {
+    float e0, e1;
+    dequant_byte_int4(p[r * row_stride + (e >> 1)], scales[r * scale_stride + c.tensor], e0, e1);
+    return (e & 1) ? e1 : e0;
+  };
+  if ((int)threadIdx.x < head) {
+    const int64_t e = c.start + threadIdx.x;
+    out[e] = mean_elem_torch(dq, k, self_row, self_x, e, e - ts.start, ts.n, dk);
+  }
   for (int t = wave; t < ntiles; t += kWaves) {
     const int64_t base = c.start + head + (int64_t)t * kTile4;  // 32-element aligned
-    float4 acc[8];
-    bool first = true;
+    adfl_sum::SeqTile<8, DEEP> acc;
+    acc.init();
     for (int r = 0; r < k; ++r) {
       if (r == self_row) continue;
       const uint4* p16 = reinterpret_cast<const uint4*>(p + r * row_stride + (base >> 1));
@@ -950,28 +944,24 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_mean_batched_int4(
       reinterpret_cast<uint4*>(lds[wave])[lane] = p16[lane];
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float4 v = dequant2_int4(lds[wave][j * 64 + lane], s);
-        acc[j] = first ? v : add4(acc[j], v);
-      }
+      for (int j = 0; j < 8; ++j) acc.add(j, dequant2_int4(lds[wave][j * 64 + lane], s));
       __builtin_amdgcn_wave_barrier();
-      first = false;
+      acc.step();
     }
     if (self_row >= 0) {
       const float4* xs = reinterpret_cast<const float4*>(self_x + base);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float4 v = xs[j * 64 + lane];
-        acc[j] = first ? v : add4(acc[j], v);
-      }
+      for (int j = 0; j < 8; ++j) acc.add(j, xs[j * 64 + lane]);
+      acc.step();
     }
     float4* o4 = reinterpret_cast<float4*>(out + base);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) store4_nt(o4 + j * 64 + lane, div4(acc[j], dk));
+    for (int j = 0; j < 8; ++j) store4_nt(o4 + j * 64 + lane, div4(acc.result(j), dk));
   }
-  for (int i = head + ntiles * kTile4 + threadIdx.x; i < c.len; i += kBlock)
-    out[c.start + i] = mean_elem_int4(p, row_stride, k, scales, scale_stride, c.tensor, self_row, self_x,
-                                      c.start + i, dk);
+  for (int i = head + ntiles * kTile4 + threadIdx.x; i < c.len; i += kBlock) {
+    const int64_t e = c.start + i;
+    out[e] = mean_elem_torch(dq, k, self_row, self_x, e, e - ts.start, ts.n, dk);
+  }
 }
 
 // Decode + accumulate into K models (pool.py:62-75, qafel.py:176-179 via model.py:337-347): the chunk's
@@ -1146,6 +1136,10 @@ inline int tile_grid(int64_t tiles) { return clamp_grid((tiles + kWaves - 1) / k
 inline int absmax_grid(int64_t n) { return clamp_grid((n >> 2) / (8 * kBlock), kAbsmaxBlocks); }
 
 inline int check_bits(int bits) { return (bits >= 1 && bits <= 16) ? ADFL_OK : ADFL_E_BITS; }
+
+// mean kernels: K rows from which the cascade needs its levels 2-3 (torch_sum_order.h), and the most rows
+constexpr int kDeepRows = 256;
+inline bool bad_rows(int k) { return k < 1 || k > adfl_sum::kMaxRows; }
 
 // q_max as the fp32 value torch divides by (quant.py:99-100).
 inline float qmax_f(int bits) { return (float)((1LL << (bits - 1)) - 1); }
@@ -1401,12 +1395,13 @@ int adfl_slq_dequantize_mean(const int8_t* d_q, int64_t row_stride_bytes, int32_
 int adfl_slq_dequantize_mean_self(const int8_t* d_q, int64_t row_stride_bytes, int32_t k, int64_t n,
                                   const float* d_scales, int64_t scale_stride, int32_t self_row,
                                   const float* d_self_x, float* d_out, void* stream) {
-  if (!d_q || !d_scales || !d_out || n < 1 || k < 1 || row_stride_bytes < n || scale_stride < 1) return ADFL_E_ARG;
+  if (!d_q || !d_scales || !d_out || n < 1 || bad_rows(k) || row_stride_bytes < n || scale_stride < 1) return ADFL_E_ARG;
   if (self_row >= k || self_row < -1 || (self_row >= 0 && !d_self_x)) return ADFL_E_ARG;
   if (!aligned16(d_q) || !aligned16(d_out) || (row_stride_bytes & 15) != 0) return ADFL_E_ALIGN;
   if (self_row >= 0 && !aligned16(d_self_x)) return ADFL_E_ALIGN;
-  hipLaunchKernelGGL(k_dequantize_mean, dim3(tile_grid(n / kTile)), dim3(kBlock), 0, (hipStream_t)stream, d_q,
-                     row_stride_bytes, (int)k, n, d_scales, scale_stride, (int)self_row, d_self_x, d_out);
+  auto kern = k >= kDeepRows ? k_dequantize_mean<true> : k_dequantize_mean<false>;
+  hipLaunchKernelGGL(kern, dim3(tile_grid(n / kTile)), dim3(kBlock), 0, (hipStream_t)stream, d_q, row_stride_bytes,
+                     (int)k, n, d_scales, scale_stride, (int)self_row, d_self_x, d_out);
   return launch_status();
 }
 
@@ -1414,14 +1409,15 @@ int adfl_slq_dequantize_mean_batched(const int8_t* d_q, int64_t row_stride_bytes
                                      const adfl_slq_chunk* d_chunks, int64_t nchunks, const float* d_scales,
                                      int64_t scale_stride, int32_t self_row, const float* d_self_x, float* d_out,
                                      void* stream) {
-  if (!d_q || !d_chunks || !d_scales || !d_out || k < 1 || nchunks < 1 || nchunks > INT32_MAX || scale_stride < 1 ||
+  if (!d_q || !d_chunks || !d_scales || !d_out || bad_rows(k) || nchunks < 1 || nchunks > INT32_MAX || scale_stride < 1 ||
       row_stride_bytes < 1)
     return ADFL_E_ARG;
   if (self_row >= k || self_row < -1 || (self_row >= 0 && !d_self_x)) return ADFL_E_ARG;
   if (!aligned16(d_q) || !aligned16(d_out) || (row_stride_bytes & 15) != 0) return ADFL_E_ALIGN;
   if (self_row >= 0 && !aligned16(d_self_x)) return ADFL_E_ALIGN;
-  hipLaunchKernelGGL(k_dequantize_mean_batched, dim3((unsigned)nchunks), dim3(kBlock), 0, (hipStream_t)stream, d_q,
-                     row_stride_bytes, (int)k, d_chunks, d_scales, scale_stride, (int)self_row, d_self_x, d_out);
+  auto kern = k >= kDeepRows ? k_dequantize_mean_batched<true> : k_dequantize_mean_batched<false>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)nchunks), dim3(kBlock), 0, (hipStream_t)stream, d_q, row_stride_bytes,
+                     (int)k, d_chunks, d_scales, scale_stride, (int)self_row, d_self_x, d_out);
   return launch_status();
 }
 
@@ -1429,15 +1425,15 @@ int adfl_slq_dequantize_mean_batched_int4(const uint8_t* d_packed, int64_t row_s
                                           const adfl_slq_chunk* d_chunks, int64_t nchunks, const float* d_scales,
                                           int64_t scale_stride, int32_t self_row, const float* d_self_x,
                                           float* d_out, void* stream) {
-  if (!d_packed || !d_chunks || !d_scales || !d_out || k < 1 || nchunks < 1 || nchunks > INT32_MAX ||
+  if (!d_packed || !d_chunks || !d_scales || !d_out || bad_rows(k) || nchunks < 1 || nchunks > INT32_MAX ||
       scale_stride < 1 || row_stride_bytes < 1)
     return ADFL_E_ARG;
   if (self_row >= k || self_row < -1 || (self_row >= 0 && !d_self_x)) return ADFL_E_ARG;
   if (!aligned16(d_packed) || !aligned16(d_out) || (row_stride_bytes & 15) != 0) return ADFL_E_ALIGN;
   if (self_row >= 0 && !aligned16(d_self_x)) return ADFL_E_ALIGN;
-  hipLaunchKernelGGL(k_dequantize_mean_batched_int4, dim3((unsigned)nchunks), dim3(kBlock), 0, (hipStream_t)stream,
-                     d_packed, row_stride_bytes, (int)k, d_chunks, d_scales, scale_stride, (int)self_row, d_self_x,
-                     d_out);
+  auto kern = k >= kDeepRows ? k_dequantize_mean_batched_int4<true> : k_dequantize_mean_batched_int4<false>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)nchunks), dim3(kBlock), 0, (hipStream_t)stream, d_packed, row_stride_bytes,
+                     (int)k, d_chunks, d_scales, scale_stride, (int)self_row, d_self_x, d_out);
   return launch_status();
 }
 
@@ -1462,13 +1458,14 @@ int adfl_slq_dequantize_mean_int4(const uint8_t* d_packed, int64_t row_stride_by
 int adfl_slq_dequantize_mean_self_int4(const uint8_t* d_packed, int64_t row_stride_bytes, int32_t k, int64_t n,
                                        const float* d_scales, int64_t scale_stride, int32_t self_row,
                                        const float* d_self_x, float* d_out, void* stream) {
-  if (!d_packed || !d_scales || !d_out || n < 1 || k < 1 || row_stride_bytes < (n + 1) / 2 || scale_stride < 1)
+  if (!d_packed || !d_scales || !d_out || n < 1 || bad_rows(k) || row_stride_bytes < (n + 1) / 2 || scale_stride < 1)
     return ADFL_E_ARG;
   if (self_row >= k || self_row < -1 || (self_row >= 0 && !d_self_x)) return ADFL_E_ARG;
   if (!aligned16(d_packed) || !aligned16(d_out) || (row_stride_bytes & 15) != 0) return ADFL_E_ALIGN;
   if (self_row >= 0 && !aligned16(d_self_x)) return ADFL_E_ALIGN;
-  hipLaunchKernelGGL(k_dequantize_mean_int4, dim3(tile_grid(n / kTile4)), dim3(kBlock), 0, (hipStream_t)stream,
-                     d_packed, row_stride_bytes, (int)k, n, d_scales, scale_stride, (int)self_row, d_self_x, d_out);
+  auto kern = k >= kDeepRows ? k_dequantize_mean_int4<true> : k_dequantize_mean_int4<false>;
+  hipLaunchKernelGGL(kern, dim3(tile_grid(n / kTile4)), dim3(kBlock), 0, (hipStream_t)stream, d_packed,
+                     row_stride_bytes, (int)k, n, d_scales, scale_stride, (int)self_row, d_self_x, d_out);
   return launch_status();
 }
 

@@ -33,6 +33,7 @@
 #include "adfl_stoch.h"
 #include "cnat_log2_table.h"
 #include "philox.h"
+#include "torch_sum_order.h"
 
 namespace {
 
@@ -1131,19 +1132,21 @@ __global__ __launch_bounds__(kBlock) void k_stoch_dequantize(const uint8_t* __re
 
 // Server-side mean of K clients' payloads: simple_aggregate (Src/ADFL/model.py:221-234) over the K decodes
 // (quant.py:243-252 / :385-398 / :537-545), the synchronous server's aggregate of K updates:
-//   out[i] = fp32(((0 + d_0[i]) + d_1[i]) + ... + d_{K-1}[i]) / K   (the division correctly rounded)
-// with d_r the decode of row r's level / exponent and sign bytes under row r's norm (+0 where that norm is 0,
-// as the decoder returns zeros). Row r's planes are levels / signs + r * row_stride (one bucket payload each,
-// one chunk table), its norms norms + r * norm_stride (RQSGD's minima likewise). The sum starts from +0 as
-// torch's does, so a column of -0 decodes (level 0, sign -1) sums to +0. One block per chunk; each thread's
-// dword groups (after the < 4-element head), all of a row's loads issued before its decodes; the exact
-// decode forms throughout (K decodes per output element; the loads dominate).
+//   out[i] = fp32(torch-order sum over r of d_r[i]) / K   (the division correctly rounded)
+// in torch's CPU summation order for sum(stack(...), dim=0) (torch_sum_order.h: per tensor, the order depends
+// on the element's index in its tensor; SEQ columns from +0, cascaded every 16 rows), with d_r the decode of
+// row r's level / exponent and sign bytes under row r's norm (+0 where that norm is 0, as the decoder returns
+// zeros). Row r's planes are levels / signs + r * row_stride (one bucket payload each, one chunk table), its
+// norms norms + r * norm_stride (RQSGD's minima likewise). The sum starts from +0 as torch's does, so a column
+// of -0 decodes (level 0, sign -1) sums to +0. One block per chunk; each thread's dword groups of SEQ columns
+// (after the < 4-element head), all of a row's loads issued before its decodes; the < 4-element head and the
+// elements past the tensor's last SEQ column element-wise in their own order. DEEP: K >= 256.
 template <int KIND>
 __device__ __forceinline__ float mean_term(uint32_t l, uint32_t g, float norm, float mn, float s) {
   return norm == 0.0f ? 0.0f : decode_exact<KIND>(l, g, norm, mn, s);
 }
 
-template <int KIND>
+template <int KIND, bool DEEP>
 __global__ __launch_bounds__(kBlock) void k_stoch_dequantize_mean(const uint8_t* __restrict__ levels,
                                                                   const uint8_t* __restrict__ signs,
                                                                   int64_t row_stride, int k,
@@ -1152,13 +1155,15 @@ __global__ __launch_bounds__(kBlock) void k_stoch_dequantize_mean(const uint8_t*
                                                                   const float* __restrict__ mins, int64_t norm_stride,
                                                                   float s, float* __restrict__ out) {
   const adfl_slq_chunk c = chunks[blockIdx.x];
+  const int64_t t_start = chunks[c.first_chunk].start;
+  const int64_t t_n = (int64_t)(c.nchunks - 1) * ADFL_SLQ_CHUNK_ELEMS + chunks[c.first_chunk + c.nchunks - 1].len;
   const int head = chunk_head4(c.start, c.len);
-  const int n4 = (c.len - head) >> 2;
-  const int ie = edge_elem(head, head + (n4 << 2), c.len);
-  float4 acc[kPer];
-#pragma unroll
-  for (int j = 0; j < kPer; ++j) acc[j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  float acc_e = 0.0f;
+  int64_t lim = t_start + adfl_sum::seq_end(t_n) - c.start;  // chunk-relative end of the SEQ columns
+  lim = lim < c.len ? lim : c.len;
+  const int n4 = lim > head ? (int)((lim - head) >> 2) : 0;  // dword groups wholly in SEQ columns
+  const double dk = (double)k;
+  adfl_sum::SeqTile<kPer, DEEP> acc;
+  acc.init();
   for (int r = 0; r < k; ++r) {
     const float norm = norms[r * norm_stride + c.tensor];
     const float mn = KIND == 1 ? mins[r * norm_stride + c.tensor] : 0.0f;
@@ -1175,26 +1180,37 @@ __global__ __launch_bounds__(kBlock) void k_stoch_dequantize_mean(const uint8_t*
     }
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
-      if ((int)threadIdx.x + j * kBlock < n4) {
-        acc[j].x += mean_term<KIND>(L[j] & 0xffu, G[j] & 0xffu, norm, mn, s);
-        acc[j].y += mean_term<KIND>((L[j] >> 8) & 0xffu, (G[j] >> 8) & 0xffu, norm, mn, s);
-        acc[j].z += mean_term<KIND>((L[j] >> 16) & 0xffu, (G[j] >> 16) & 0xffu, norm, mn, s);
-        acc[j].w += mean_term<KIND>(L[j] >> 24, G[j] >> 24, norm, mn, s);
-      }
+      if ((int)threadIdx.x + j * kBlock < n4)
+        acc.add(j, make_float4(mean_term<KIND>(L[j] & 0xffu, G[j] & 0xffu, norm, mn, s),
+                               mean_term<KIND>((L[j] >> 8) & 0xffu, (G[j] >> 8) & 0xffu, norm, mn, s),
+                               mean_term<KIND>((L[j] >> 16) & 0xffu, (G[j] >> 16) & 0xffu, norm, mn, s),
+                               mean_term<KIND>(L[j] >> 24, G[j] >> 24, norm, mn, s)));
     }
-    if (ie >= 0) acc_e += mean_term<KIND>(lv[ie], sg[ie], norm, mn, s);
+    acc.step();
   }
-  const double dk = (double)k;
   float* oc = out + c.start;
   float4* o4 = reinterpret_cast<float4*>(oc + head);
 #pragma unroll
   for (int j = 0; j < kPer; ++j) {
     const int q = threadIdx.x + j * kBlock;
-    if (q < n4)
-      store4_nt(o4 + q, make_float4((float)((double)acc[j].x / dk), (float)((double)acc[j].y / dk),
-                                    (float)((double)acc[j].z / dk), (float)((double)acc[j].w / dk)));
+    if (q < n4) {
+      const float4 a = acc.result(j);
+      store4_nt(o4 + q, make_float4((float)((double)a.x / dk), (float)((double)a.y / dk), (float)((double)a.z / dk),
+                                    (float)((double)a.w / dk)));
+    }
   }
-  if (ie >= 0) oc[ie] = (float)((double)acc_e / dk);
+  // head elements and those past the SEQ groups: each in its own order
+  const int rest = c.len - (head + (n4 << 2));
+  for (int t = threadIdx.x; t < head + rest; t += kBlock) {
+    const int i = t < head ? t : head + (n4 << 2) + (t - head);
+    auto get = [&](int r) -> float {
+      const float norm = norms[r * norm_stride + c.tensor];
+      const float mn = KIND == 1 ? mins[r * norm_stride + c.tensor] : 0.0f;
+      return mean_term<KIND>(levels[r * row_stride + c.start + i], signs[r * row_stride + c.start + i], norm, mn, s);
+    };
+    const int64_t j = c.start + i - t_start;
+    oc[i] = (float)((double)adfl_sum::sum_elem(get, k, adfl_sum::mode_of(j, t_n, k)) / dk);
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void k_philox_uniforms(float* __restrict__ out, int64_t n, int64_t start,
@@ -1425,7 +1441,7 @@ int adfl_stoch_dequantize_mean_batched(int32_t codec, const uint8_t* d_levels, c
                                        int64_t norm_stride, float* d_out, void* stream) {
   if (codec != ADFL_CODEC_QSGD && codec != ADFL_CODEC_RQSGD && codec != ADFL_CODEC_CNAT) return ADFL_E_ARG;
   if (!d_levels || !d_signs || !d_norms || !d_out || (codec == ADFL_CODEC_RQSGD && !d_mins) ||
-      bad_table(d_chunks, nchunks) || k < 1 || row_stride_bytes < 0 || norm_stride < 0 ||
+      bad_table(d_chunks, nchunks) || k < 1 || k > adfl_sum::kMaxRows || row_stride_bytes < 0 || norm_stride < 0 ||
       (k > 1 && (row_stride_bytes == 0 || norm_stride == 0)))
     return ADFL_E_ARG;
   if (codec != ADFL_CODEC_CNAT)
@@ -1435,15 +1451,13 @@ int adfl_stoch_dequantize_mean_batched(int32_t codec, const uint8_t* d_levels, c
   const auto* sg = reinterpret_cast<const uint8_t*>(d_signs);
   const dim3 grid((unsigned)nchunks), block(kBlock);
   hipStream_t st = (hipStream_t)stream;
-  if (codec == ADFL_CODEC_QSGD)
-    hipLaunchKernelGGL(k_stoch_dequantize_mean<0>, grid, block, 0, st, d_levels, sg, row_stride_bytes, k, d_chunks,
-                       d_norms, d_mins, norm_stride, s, d_out);
-  else if (codec == ADFL_CODEC_RQSGD)
-    hipLaunchKernelGGL(k_stoch_dequantize_mean<1>, grid, block, 0, st, d_levels, sg, row_stride_bytes, k, d_chunks,
-                       d_norms, d_mins, norm_stride, s, d_out);
-  else
-    hipLaunchKernelGGL(k_stoch_dequantize_mean<2>, grid, block, 0, st, d_levels, sg, row_stride_bytes, k, d_chunks,
-                       d_norms, d_mins, norm_stride, s, d_out);
+  const bool deep = k >= 256;
+  auto kern = codec == ADFL_CODEC_QSGD
+                  ? (deep ? k_stoch_dequantize_mean<0, true> : k_stoch_dequantize_mean<0, false>)
+                  : codec == ADFL_CODEC_RQSGD ? (deep ? k_stoch_dequantize_mean<1, true> : k_stoch_dequantize_mean<1, false>)
+                                              : (deep ? k_stoch_dequantize_mean<2, true> : k_stoch_dequantize_mean<2, false>);
+  hipLaunchKernelGGL(kern, grid, block, 0, st, d_levels, sg, row_stride_bytes, k, d_chunks, d_norms, d_mins, norm_stride,
+                     s, d_out);
   return launch_status();
 }
 

@@ -15,6 +15,7 @@
  */
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 /* torch.max(torch.abs(t)) — Src/ADFL/Channel/quant.py:100. NaN propagates (torch.max semantics). */
@@ -105,55 +106,117 @@ void oracle_slq_dequantize_int4(const uint8_t* packed, int64_t n, float scale, f
     }
 }
 
-/* Peer mean of K decoded payloads (Examples/ray_ad.py:188 torch.stack(...).mean(0)): fp32 sum in
- * payload order, then divide by K. */
-void oracle_slq_dequantize_mean(const int8_t* const* qs, const float* scales, int32_t k, int64_t n, float* out) {
-    for (int64_t i = 0; i < n; ++i) {
-        float s = scales[0] * (float)qs[0][i];
-        for (int32_t r = 1; r < k; ++r) s += scales[r] * (float)qs[r][i];
-        out[i] = s / (float)k;
+/* torch 2.10's CPU summation order of torch.sum(torch.stack(rows), dim=0) — simple_aggregate
+ * (Src/ADFL/model.py:229-231) and stack(...).mean(0) (Examples/ray_ad.py:188; CPU mean = that sum / K) —
+ * restated from aten/src/ATen/native/cpu/SumKernel.cpp (cascade_sum, the AVX2 kernel: 8-float vectors) and
+ * pinned against torch itself and the reference's simple_aggregate executed in place
+ * (tests/golden/aggregate.npz, tests/test_sum_order_golden.py). d[s * stride] is row s's value of one
+ * element; j is the element's index in its n-element tensor.
+ *   SEQ   j < (n >= 8 ? n & ~31 : n & ~3): rows in order into a 4-level cascade (fold every 16 rows);
+ *   ILP4  other columns, and n == 1 with K < 8: 4 interleaved partials (rows 4g+p), leftover rows into
+ *         partial 0, then p0 + p1 + p2 + p3;
+ *   INNER n == 1 with K >= 8: vectorized_inner_sum (8 lanes, each an ILP4 sum over its vectors). */
+static float cascade_f(const float* d, int64_t count, int64_t stride) {
+    float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+    for (int64_t i = 0; i < count;) {
+        a0 = a0 + d[i * stride];
+        ++i;
+        if ((i & 15) == 0) {
+            a1 = a1 + a0; a0 = 0.0f;
+            if ((i & 0xF0) == 0) {
+                a2 = a2 + a1; a1 = 0.0f;
+                if ((i & 0xF00) == 0) { a3 = a3 + a2; a2 = 0.0f; }
+            }
+        }
     }
+    a0 = a0 + a1;
+    a0 = a0 + a2;
+    return a0 + a3;
 }
 
-/* Same mean over K int4-packed payloads (unpack_4bit then dequantize, compression.py:51-66). */
-void oracle_slq_dequantize_mean_int4(const uint8_t* const* ps, const float* scales, int32_t k, int64_t n, float* out) {
-    for (int64_t i = 0; i < n; ++i) {
-        float s = 0.0f;
-        for (int32_t r = 0; r < k; ++r) {
-            uint8_t b = ps[r][i / 2];
-            int v = (i & 1) ? ((b & 0xF) - 8) : (((b >> 4) & 0xF) - 8);
-            float d = scales[r] * (float)v;
-            s = (r == 0) ? d : s + d;
-        }
-        out[i] = s / (float)k;
+static float ilp4_f(const float* d, int64_t count, int64_t stride) {
+    const int64_t g = count / 4;
+    float p0 = cascade_f(d, g, 4 * stride);
+    const float p1 = cascade_f(d + stride, g, 4 * stride);
+    const float p2 = cascade_f(d + 2 * stride, g, 4 * stride);
+    const float p3 = cascade_f(d + 3 * stride, g, 4 * stride);
+    for (int64_t i = 4 * g; i < count; ++i) p0 = p0 + d[i * stride];
+    p0 = p0 + p1;
+    p0 = p0 + p2;
+    return p0 + p3;
+}
+
+float oracle_torch_sum_col(const float* d, int32_t k, int64_t j, int64_t n) {
+    if (n == 1) {
+        if (k < 8) return ilp4_f(d, k, 1);
+        const int64_t v = k / 8;
+        float acc = 0.0f;
+        for (int64_t i = 8 * v; i < k; ++i) acc = acc + d[i];
+        for (int l = 0; l < 8; ++l) acc = acc + ilp4_f(d + l, v, 8);
+        return acc;
     }
+    const int64_t seq_end = n >= 8 ? (n & ~(int64_t)31) : (n & ~(int64_t)3);
+    return j < seq_end ? cascade_f(d, k, 1) : ilp4_f(d, k, 1);
+}
+
+/* torch.stack(rows).sum(0) / K for a row-major [k, n] fp32 matrix (one tensor per row). */
+void oracle_torch_mean_rows(const float* rows, int32_t k, int64_t n, float* out) {
+    float* col = (float*)malloc(sizeof(float) * (size_t)k);
+    for (int64_t i = 0; i < n; ++i) {
+        for (int32_t r = 0; r < k; ++r) col[r] = rows[(int64_t)r * n + i];
+        out[i] = oracle_torch_sum_col(col, k, i, n) / (float)k;
+    }
+    free(col);
+}
+
+void oracle_torch_sum_rows(const float* rows, int32_t k, int64_t n, float* out) {
+    float* col = (float*)malloc(sizeof(float) * (size_t)k);
+    for (int64_t i = 0; i < n; ++i) {
+        for (int32_t r = 0; r < k; ++r) col[r] = rows[(int64_t)r * n + i];
+        out[i] = oracle_torch_sum_col(col, k, i, n);
+    }
+    free(col);
+}
+
+static float row_value(const void* row, int32_t packed, float scale, int64_t i) {
+    int v;
+    if (packed) {
+        uint8_t b = ((const uint8_t*)row)[i / 2];
+        v = (i & 1) ? ((b & 0xF) - 8) : (((b >> 4) & 0xF) - 8);
+    } else {
+        v = ((const int8_t*)row)[i];
+    }
+    return scale * (float)v;
 }
 
 /* The receiving peer's mean with its own update exact (Src/ADFL/Client/async_peer.py:170-174,
  * Examples/ray_ad.py:183-188: own fp32 parameters appended after the received updates, then
- * stack(...).mean(0)): rows other than self_row in r order, then self_x, fp32, then / K. int4 rows when
- * packed != 0 (compression.py:51-66). */
+ * stack(...).mean(0)): the row sequence is the rows other than self_row in r order, then self_x; summed in
+ * torch's order for an n-element tensor, then / K. self_row < 0: all K rows (simple_aggregate of K decodes).
+ * int4 rows when packed != 0 (compression.py:51-66). */
 void oracle_slq_dequantize_mean_self(const void* const* rows, const float* scales, int32_t k, int64_t n,
                                      int32_t self_row, const float* self_x, int32_t packed, float* out) {
+    float* col = (float*)malloc(sizeof(float) * (size_t)k);
     for (int64_t i = 0; i < n; ++i) {
-        float s = 0.0f;
-        int first = 1;
+        int32_t s = 0;
         for (int32_t r = 0; r < k; ++r) {
             if (r == self_row) continue;
-            int v;
-            if (packed) {
-                uint8_t b = ((const uint8_t*)rows[r])[i / 2];
-                v = (i & 1) ? ((b & 0xF) - 8) : (((b >> 4) & 0xF) - 8);
-            } else {
-                v = ((const int8_t*)rows[r])[i];
-            }
-            float d = scales[r] * (float)v;
-            s = first ? d : s + d;
-            first = 0;
+            col[s++] = row_value(rows[r], packed, scales[r], i);
         }
-        if (self_row >= 0) s = first ? self_x[i] : s + self_x[i];
-        out[i] = s / (float)k;
+        if (self_row >= 0) col[s++] = self_x[i];
+        out[i] = oracle_torch_sum_col(col, k, i, n) / (float)k;
     }
+    free(col);
+}
+
+/* Peer mean / aggregate of K decoded int8 payloads of one n-element tensor. */
+void oracle_slq_dequantize_mean(const int8_t* const* qs, const float* scales, int32_t k, int64_t n, float* out) {
+    oracle_slq_dequantize_mean_self((const void* const*)qs, scales, k, n, -1, NULL, 0, out);
+}
+
+/* Same mean over K int4-packed payloads (unpack_4bit then dequantize, compression.py:51-66). */
+void oracle_slq_dequantize_mean_int4(const uint8_t* const* ps, const float* scales, int32_t k, int64_t n, float* out) {
+    oracle_slq_dequantize_mean_self((const void* const*)ps, scales, k, n, -1, NULL, 1, out);
 }
 
 /* Thread-free helper the tests use for SHA inputs of recipe cases. */

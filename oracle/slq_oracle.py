@@ -59,6 +59,9 @@ def lib():
         L.oracle_slq_dequantize_mean_int4.restype = None
         L.oracle_slq_dequantize_mean_self.argtypes = [P, P, I32, I64, I32, P, I32, P]
         L.oracle_slq_dequantize_mean_self.restype = None
+        L.oracle_torch_sum_col.argtypes, L.oracle_torch_sum_col.restype = [P, I32, I64, I64], F
+        L.oracle_torch_mean_rows.argtypes, L.oracle_torch_mean_rows.restype = [P, I32, I64, P], None
+        L.oracle_torch_sum_rows.argtypes, L.oracle_torch_sum_rows.restype = [P, I32, I64, P], None
         _lib = L
     return _lib
 
@@ -112,6 +115,25 @@ def decode_int4(packed: np.ndarray, n: int, scale) -> np.ndarray:
     packed = np.ascontiguousarray(packed).view(np.uint8).reshape(-1)
     out = np.empty(n, np.float32)
     lib().oracle_slq_dequantize_int4(_ptr(packed), n, float(np.float32(scale)), _ptr(out))
+    return out
+
+
+def torch_sum_rows(rows) -> np.ndarray:
+    """torch.sum(torch.stack(rows), dim=0) for K fp32 rows of one n-element tensor, in torch 2.10's CPU
+    summation order (slq_oracle.c oracle_torch_sum_col; the sum simple_aggregate takes,
+    Src/ADFL/model.py:229-231)."""
+    m = np.ascontiguousarray(np.stack([np.asarray(r, np.float32).reshape(-1) for r in rows]), dtype=np.float32)
+    out = np.empty(m.shape[1], np.float32)
+    lib().oracle_torch_sum_rows(_ptr(m), m.shape[0], m.shape[1], _ptr(out))
+    return out
+
+
+def torch_mean_rows(rows) -> np.ndarray:
+    """simple_aggregate of one tensor (Src/ADFL/model.py:229-231) = stack(rows).mean(0) (Examples/ray_ad.py:188):
+    the torch-order sum, then a correctly rounded fp32 division by K."""
+    m = np.ascontiguousarray(np.stack([np.asarray(r, np.float32).reshape(-1) for r in rows]), dtype=np.float32)
+    out = np.empty(m.shape[1], np.float32)
+    lib().oracle_torch_mean_rows(_ptr(m), m.shape[0], m.shape[1], _ptr(out))
     return out
 
 

@@ -125,13 +125,13 @@ def test_passthrough_only_dict_needs_no_device():
     assert dec["b"].data_ptr() == b.data_ptr()  # `q_param.data.data`: a new view of the same storage
 
 
-@pytest.mark.parametrize("k", [1, 2, 3, 4, 5, 8])
+@pytest.mark.parametrize("k", [1, 2, 3, 4, 5, 8, 16, 17, 20, 64])
 def test_receive_mean_passthrough_entries_are_simple_aggregate(k):
     """receive_mean over updates with nothing quantized: simple_aggregate's own values on the host
     (Src/ADFL/model.py:221-234: stack, sum over dim 0, / K; an int64 counter becomes fp32), key order of
-    the first update, no device. The entries are summed batched (concatenated per dtype, K elementwise
-    adds from zero) where that equals the per-entry torch.sum — int64 always, fp32 for K <= 4 — and per
-    entry otherwise; every value, sign of zero included, must equal the per-entry call's."""
+    the first update, no device. The entries are summed batched (concatenated per dtype: int64 with K
+    elementwise adds, fp32 in torch's own summation order per entry, adfl_amd.sum_order) and one-element
+    fp32 entries at K >= 8 per entry; every value, sign of zero included, must equal the per-entry call's."""
     ch = SLQChannel(8)
     g = torch.Generator().manual_seed(k)
     ups = []
@@ -139,7 +139,8 @@ def test_receive_mean_passthrough_entries_are_simple_aggregate(k):
         d = {f"b{i}": torch.randn(1 + (i * 37) % 300, generator=g) * 10.0 ** (i % 7 - 3) for i in range(40)}
         d["zeros"] = torch.tensor([-0.0, 0.0, -0.0 if r % 2 else 0.0])
         d["n"] = torch.tensor(3 + r)
-        d["big"] = torch.randn(40000, generator=g)    # above torch's grain size: always per entry
+        d["big"] = torch.randn(40000, generator=g)    # above torch's grain size (multi-threaded sum)
+        d["one"] = torch.randn(1, generator=g)        # torch's inner-sum kernel from K = 8
         d["i64v"] = torch.arange(5, dtype=torch.int64) * (r + 1)
         ups.append(ch.on_client_send(d)[0])
     got, t = ch.receive_mean(ups)
