@@ -62,6 +62,8 @@ def parse():
                    help="C4 peer-exchange leg (encode + RCCL all-gather + decode-mean); auto = only when N > 1")
     p.add_argument("--pmc", choices=("auto", "off"), default="auto",
                    help="roofline.traffic from live rocprofv3 PMC passes (auto: N=1 only, after the timed region)")
+    p.add_argument("--extras", choices=("auto", "on", "off"), default="auto",
+                   help="C3 / C5 int4 / host-inclusive (pcie) objects after the timed headline; auto = N=1 only")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--cpu-child", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--cpu-input", help=argparse.SUPPRESS)
@@ -436,6 +438,241 @@ def copy_ceiling_GBs(x: torch.Tensor, out: torch.Tensor, stream, reps: int = 10)
     return 2 * x.numel() * x.element_size() / (ms * 1e-3) / 1e9
 
 
+RESNET18_PARAMS = 11_689_512          # C3: ResNet-18's parameter count in 256 tensors
+C5_ELEMS = 1 << 30                    # C5: 4 GiB of fp32 per client
+
+
+def _median(xs):
+    xs = sorted(xs)
+    return xs[len(xs) // 2]
+
+
+def _ref_encode(t: torch.Tensor, bits: int):
+    """The reference's own op sequence on a host tensor (Src/ADFL/Channel/quant.py:99-104): scale =
+    max|t| / q_max in fp32 tensor math, then quantize_per_tensor with float(scale)."""
+    scale = torch.max(torch.abs(t)) / (2 ** (bits - 1) - 1)
+    return torch.quantize_per_tensor(t, float(scale), 0, torch.qint8), float(scale)
+
+
+def extra_c3(dev, lib, steps: int) -> dict:
+    """BASELINE configs[2] (C3) beside the headline: ResNet-18's 11,689,512 fp32 parameters in 256 equal tensors,
+    one bucket with per-tensor scales (quant.py:74-94), device-resident, the Infinity Cache flushed by a 512 MiB
+    READ before every step. Encode = ONE launch (k_encode_resident: a block per tensor, x read once), decode
+    one launch. Fractions: on the bytes the two kernels move (encode 5 B + decode 5 B per element; the PMC
+    passes count 1.004-1.008x that) and at the survey's 14 B/element round-trip count. parity: the
+    payload, the 256 scales and the decoded floats against the reference's ATen ops per tensor."""
+    from adfl_amd import _lib, ops
+    base, rem = divmod(RESNET18_PARAMS, 256)
+    sizes = [base + (1 if i < rem else 0) for i in range(256)]
+    lay = ops.BucketLayout(sizes)
+    g = torch.Generator(device=dev).manual_seed(3)
+    x = torch.randn(lay.total, device=dev, generator=g) * 1e-3
+    q = torch.empty(lay.total, dtype=torch.int8, device=dev)
+    scales = torch.empty(lay.ntensors, device=dev)
+    partials = torch.empty(lay.nchunks, dtype=torch.int32, device=dev)
+    out = torch.zeros(lay.total, device=dev)
+    chunks, work = lay.device_chunks(dev), lay.device_work(dev)
+    junk = torch.ones(128 << 20, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+
+    def enc():
+        _lib.check(lib.adfl_slq_encode_batched_work(x.data_ptr(), chunks.data_ptr(), lay.nchunks, work.data_ptr(),
+                                                    lay.nwork, 8, q.data_ptr(), scales.data_ptr(),
+                                                    partials.data_ptr(), sh))
+
+    def dec():
+        _lib.check(lib.adfl_slq_dequantize_batched(q.data_ptr(), chunks.data_ptr(), lay.nchunks, scales.data_ptr(),
+                                                   out.data_ptr(), sh))
+    for _ in range(3):
+        junk.amax()
+        enc()
+        dec()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    rt = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(steps)]
+    for e in evs:           # encode and decode apart
+        junk.amax()
+        e[0].record(stream)
+        enc()
+        e[1].record(stream)
+        dec()
+        e[2].record(stream)
+    for e in rt:            # the round trip as one span (no event between the launches)
+        junk.amax()
+        e[0].record(stream)
+        enc()
+        dec()
+        e[1].record(stream)
+    torch.cuda.synchronize()
+    e_ms = _median([e[0].elapsed_time(e[1]) for e in evs])
+    d_ms = _median([e[1].elapsed_time(e[2]) for e in evs])
+    r_ms = _median([e[0].elapsed_time(e[1]) for e in rt])
+    n = RESNET18_PARAMS
+    frac = lambda b, ms: round(b * n / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)  # noqa: E731
+    # parity against the reference's ATen ops, tensor by tensor (quant.py:97-112)
+    xc, qc, sc, oc = x.cpu(), q.cpu(), scales.cpu(), out.cpu()
+    ok = True
+    for t, (o, m) in enumerate(zip(lay.offsets.tolist(), sizes)):
+        qr, s = _ref_encode(xc[o:o + m].view(1, m), 8)
+        ok = ok and float(sc[t]) == s and torch.equal(qr.int_repr().view(-1), qc[o:o + m]) \
+            and torch.equal(qr.dequantize().view(-1), oc[o:o + m])
+    return {"workload": "C3: 11,689,512 fp32 in 256 tensors (ResNet-18 size, equal layout), per-tensor scales, "
+                        "bits=8, device-resident, Infinity Cache flushed by a 512 MiB read before each step",
+            "steps": steps, "encode_launches": 1 if lay.nwork else 2, "encode_ms": round(e_ms, 4),
+            "decode_ms": round(d_ms, 4), "round_trip_ms": round(r_ms, 4),
+            "GiB_per_s": round(n * 4 / GIB / (r_ms * 1e-3), 1),
+            "frac_moved": frac(10, r_ms), "encode_frac_moved": frac(5, e_ms), "decode_frac_moved": frac(5, d_ms),
+            "frac_14B": frac(14, r_ms), "parity": bool(ok)}
+
+
+def extra_c5(dev, lib, steps: int) -> dict:
+    """BASELINE configs[4]'s codec (C5) beside the headline: 2^30 fp32 (4 GiB) per client, SLQ bits=4 packed
+    two codes per byte (pack_4bit's layout, compression.py:35-48): absmax, fused quantize+pack, fused
+    unpack+dequantize, HIP events per kernel. Bytes per element: absmax 4, quantize+pack 4.5, unpack+dequantize
+    4.5 (13 per round trip). parity: the scale against max|x| / 7 (quant.py:99-100), every code against the
+    reference's quantize_per_tensor on the host copy (the nibbles unpacked with torch ops), and the decoded
+    floats against fp32(scale * code) (quant.py:110)."""
+    from adfl_amd import _lib, ops
+    n = C5_ELEMS
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = torch.randn(n, device=dev, generator=g) * 1e-3
+    packed = torch.empty(n // 2, dtype=torch.uint8, device=dev)
+    scale = torch.empty(1, device=dev)
+    ws = ops.new_workspace(dev)
+    out = torch.empty(n, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+
+    def step(e=None):
+        if e is not None:
+            e[0].record(stream)
+        _lib.check(lib.adfl_slq_absmax(x.data_ptr(), n, ws.data_ptr(), ws.numel(), sh))
+        if e is not None:
+            e[1].record(stream)
+        _lib.check(lib.adfl_slq_quantize_int4(x.data_ptr(), n, 4, ws.data_ptr(), packed.data_ptr(), scale.data_ptr(),
+                                              sh))
+        if e is not None:
+            e[2].record(stream)
+        _lib.check(lib.adfl_slq_dequantize_int4(packed.data_ptr(), n, scale.data_ptr(), out.data_ptr(), sh))
+        if e is not None:
+            e[3].record(stream)
+    for _ in range(2):
+        step()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(steps)]
+    for e in evs:
+        step(e)
+    torch.cuda.synchronize()
+    names = ("absmax", "quantize_pack", "unpack_dequantize")
+    ms = {k: _median([e[i].elapsed_time(e[i + 1]) for e in evs]) for i, k in enumerate(names)}
+    per = dict(zip(names, (4.0, 4.5, 4.5)))
+    rt = sum(ms.values())
+    xc = x.cpu()
+    qr, s = _ref_encode(xc, 4)
+    del xc
+    ok = float(scale.item()) == s
+    qd = qr.int_repr().to(dev)
+    del qr
+    hi = (packed >> 4).to(torch.int16) - 8
+    lo = (packed & 15).to(torch.int16) - 8
+    ok = ok and torch.equal(hi, qd[0::2].to(torch.int16)) and torch.equal(lo, qd[1::2].to(torch.int16))
+    ok = ok and torch.equal(out.view(torch.int32), (qd.to(torch.float32) * scale).view(torch.int32))
+    return {"workload": "C5: 2^30 fp32 (4 GiB) per client, SLQ bits=4, pack_4bit layout, device-resident",
+            "steps": steps, "kernels_ms": {k: round(v, 4) for k, v in ms.items()},
+            "kernels_frac": {k: round(per[k] * n / (ms[k] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) for k in names},
+            "round_trip_ms": round(rt, 4), "GiB_per_s": round(n * 4 / GIB / (rt * 1e-3), 1),
+            "frac_13B": round(13 * n / (rt * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "parity": bool(ok)}
+
+
+def extra_pcie(dev, lib, steps: int) -> dict:
+    """The rate that includes the host hops (north_star: the path starts and ends in host memory, ADFL's Ray
+    loopback): (1) the 1 GiB C2 round trip from and to pinned host memory — H2D of x (4N), encode, the payload
+    D2H and back H2D (2N), decode, D2H of the output (4N); (2) ADFL's own call pattern: a CPU ResNet-18-sized
+    state dict (256 weights + 256 biases) through SLQChannel.on_client_send then on_server_receive, host to
+    host, as Src/ADFL/Client/worker.py:176 and Src/ADFL/Server/async_sc.py:209 call it. parity: both against
+    the reference's ATen ops on the same host tensors (quant.py:97-112)."""
+    from adfl_amd import _lib, ops
+    from adfl_amd.Channel import SLQChannel
+    n = N_ELEMS
+    x_h = (torch.randn(n, generator=torch.Generator().manual_seed(7)) * 1e-3).pin_memory()
+    q_h = torch.empty(n, dtype=torch.int8).pin_memory()
+    out_h = torch.empty(n).pin_memory()
+    x = torch.empty(n, device=dev)
+    q = torch.empty(n, dtype=torch.int8, device=dev)
+    q2 = torch.empty(n, dtype=torch.int8, device=dev)
+    s = torch.empty(1, device=dev)
+    out = torch.empty(n, device=dev)
+    ws = ops.new_workspace(dev)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+
+    def step(e=None):
+        rec = (lambda i: e[i].record(stream)) if e is not None else (lambda i: None)
+        rec(0)
+        x.copy_(x_h, non_blocking=True)
+        rec(1)
+        _lib.check(lib.adfl_slq_encode(x.data_ptr(), n, 8, q.data_ptr(), s.data_ptr(), ws.data_ptr(), ws.numel(), sh))
+        rec(2)
+        q_h.copy_(q, non_blocking=True)
+        q2.copy_(q_h, non_blocking=True)   # the payload crosses the host "wire" and comes back
+        rec(3)
+        _lib.check(lib.adfl_slq_dequantize(q2.data_ptr(), n, s.data_ptr(), out.data_ptr(), sh))
+        rec(4)
+        out_h.copy_(out, non_blocking=True)
+        rec(5)
+    step()
+    torch.cuda.synchronize()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(steps)]
+    t0 = time.perf_counter()
+    for e in evs:
+        step(e)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / steps
+    segs = {k: round(_median([e[i].elapsed_time(e[i + 1]) for e in evs]), 4)
+            for i, k in enumerate(("h2d_x", "encode", "payload_d2h_h2d", "decode", "d2h_out"))}
+    pcie_ms = segs["h2d_x"] + segs["payload_d2h_h2d"] + segs["d2h_out"]
+    qr, sr = _ref_encode(x_h, 8)
+    pinned_ok = float(s.item()) == sr and torch.equal(qr.int_repr(), q_h) and torch.equal(qr.dequantize(), out_h)
+    del qr, x, q, q2, out, x_h, q_h, out_h
+
+    base, rem = divmod(RESNET18_PARAMS, 256)
+    g = torch.Generator().manual_seed(11)
+    params = {}
+    for i in range(256):
+        params[f"layer{i}.weight"] = torch.randn(1, base + (1 if i < rem else 0), generator=g) * 1e-3
+        params[f"layer{i}.bias"] = torch.randn(64, generator=g) * 1e-3
+    ch = SLQChannel(8)
+    enc_t, dec_t = [], []
+    for k in range(3 + max(steps, 10)):
+        t1 = time.perf_counter()
+        qp, _ = ch.on_client_send(params)
+        t2 = time.perf_counter()
+        dp, _ = ch.on_server_receive(qp)
+        t3 = time.perf_counter()
+        if k >= 3:
+            enc_t.append(t2 - t1)
+            dec_t.append(t3 - t2)
+    dict_ok = True
+    for name, t in params.items():
+        if t.ndim > 1:
+            qr, _ = _ref_encode(t, 8)
+            dict_ok = dict_ok and torch.equal(qp.params[name].data.int_repr(), qr.int_repr()) \
+                and qp.params[name].data.q_scale() == qr.q_scale() and torch.equal(dp[name], qr.dequantize())
+        else:
+            dict_ok = dict_ok and torch.equal(dp[name], t)
+    e_ms, d_ms = _median(enc_t) * 1e3, _median(dec_t) * 1e3
+    gib_dict = sum(t.numel() for t in params.values()) * 4 / GIB
+    return {"pinned_1GiB": {"workload": "C2's 1 GiB fp32 from and to pinned host memory (10N bytes over PCIe)",
+                            "steps": steps, "ms_per_round_trip": round(wall * 1e3, 3),
+                            "GiB_per_s": round(n * 4 / GIB / wall, 2), "segments_ms": segs,
+                            "pcie_GBs": round(10 * n / (pcie_ms * 1e-3) / 1e9, 1), "parity": bool(pinned_ok)},
+            "channel_c3_dict": {"workload": "SLQChannel(8).on_client_send + on_server_receive on a CPU state dict "
+                                            "of 256 weights (11,689,512 fp32) + 256 biases, host to host",
+                                "rounds": len(enc_t), "encode_ms": round(e_ms, 3), "decode_ms": round(d_ms, 3),
+                                "round_trip_ms": round(e_ms + d_ms, 3),
+                                "GiB_per_s": round(gib_dict / ((e_ms + d_ms) * 1e-3), 2),
+                                "statistic": "median", "parity": bool(dict_ok)}}
+
+
 _FP_MUL = -7046029254386353131        # 0x9E3779B97F4A7C15 as int64 (golden-ratio multiplier)
 
 
@@ -722,6 +959,15 @@ def main():
     if exchange is not None:
         line["exchange"] = exchange
         line["exchange_c3"] = exchange_c3
+    if args.extras == "on" or (args.extras == "auto" and world == 1):
+        # BASELINE's other single-GPU configs and the host-inclusive rate, after the timed headline (never in
+        # `value`); each carries its own parity against the reference's ATen ops
+        for key, fn, st in (("c3", extra_c3, 20), ("c5_int4", extra_c5, 10), ("pcie", extra_pcie, 5)):
+            try:
+                line[key] = fn(dev, lib, st)
+            except Exception as e:  # noqa: BLE001
+                line[key] = {"error": f"{type(e).__name__}: {e}"[:400]}
+            torch.cuda.empty_cache()
     if world == 1 and not args.no_cpu_baseline:
         cpu, parity = cpu_baseline(x, args.bits, args.cpu_seconds, q, scale)
         line["cpu_baseline"] = cpu

@@ -1,6 +1,7 @@
 """bench.py's output contract on the GPU (the line the driver parses): exactly one JSON line on stdout with the
 headline keys, n_gpus = 1, a roofline object for the dominant kernel, and value consistent with ms_per_step.
-A short run: 3 timed steps, no CPU baseline, no PMC passes, no exchange leg (each is covered elsewhere)."""
+A short run: 3 timed steps, no CPU baseline, no PMC passes, no exchange leg, no extras (each is covered
+elsewhere)."""
 
 import json
 import os
@@ -16,7 +17,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def test_bench_emits_one_contract_line():
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "3", "--warmup", "1",
-                        "--no-cpu-baseline", "--pmc", "off", "--exchange", "off"],
+                        "--no-cpu-baseline", "--pmc", "off", "--exchange", "off", "--extras", "off"],
                        cwd=REPO, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
@@ -45,7 +46,7 @@ def test_bench_exchange_leg_checks_itself():
     """The C4 exchange leg at world 1 over RCCL (--exchange on): after its timed steps it verifies the
     gathered rows against the sent rows and the exact_self=False mean across ranks, and says so."""
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2", "--warmup", "1",
-                        "--no-cpu-baseline", "--pmc", "off", "--exchange", "on"],
+                        "--no-cpu-baseline", "--pmc", "off", "--exchange", "on", "--extras", "off"],
                        cwd=REPO, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-2000:]
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])
@@ -79,3 +80,53 @@ def test_bench_two_ranks_share_one_gpu():
     c3 = d["exchange_c3"]
     assert "error" not in c3, c3
     assert c3["parity"] is True and c3["check"]["rows_checked"] == 2 and c3["check"]["mean_identical_on_all_ranks"]
+
+
+@pytest.mark.timeout(240)
+def test_bench_eight_ranks_share_one_gpu():
+    """The driver's 8-GPU command shape, rehearsed on one GPU: bench.py --gpus 8 starts
+    eight rank processes itself, each a simulated client on cuda:0 (hidden --share-gpu: gloo, host-staged
+    rows), runs its timed round trips, then both exchange legs at K = 8 — the C4 1 GiB update and the
+    ResNet-18-sized bucket (Examples/ray_ad.py:175,183-188) — and exchange_verify over 8 row sets: every
+    received row's fingerprint equals its sender's, and the exact_self=False mean is identical on all ranks."""
+    import time
+    t0 = time.perf_counter()
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "8", "--steps", "2", "--warmup", "1",
+                        "--no-cpu-baseline", "--pmc", "off", "--share-gpu"],
+                       cwd=REPO, capture_output=True, text=True, timeout=230)
+    wall = time.perf_counter() - t0
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["config"]["parallelism"] == "independent clients x8"
+    assert abs(d["value"] - 8.0 / (d["ms_per_step"] * 1e-3)) / d["value"] < 0.01
+    for leg in ("exchange", "exchange_c3"):
+        ex = d[leg]
+        assert "error" not in ex, (leg, ex)
+        assert ex["parity"] is True, (leg, ex)
+        assert ex["check"]["rows_checked"] == 8 and ex["check"]["mean_identical_on_all_ranks"], (leg, ex)
+    assert d["exchange"]["backend"] == "gloo"
+    print(f"8-rank share-gpu bench: {wall:.1f} s wall; exchange {d['exchange']['ms_per_step']} ms/step, "
+          f"C3 bucket exchange {d['exchange_c3']['ms_per_step']} ms/step")
+    assert wall < 150, wall
+
+
+def test_bench_extras_c3_c5_pcie():
+    """The objects bench.py adds after the timed headline at N = 1: C3 (ResNet-18-sized
+    bucket, flushed), C5 (4 GiB int4 round trip) and the host-inclusive rates (pinned 1 GiB round trip, the C3
+    CPU dict through SLQChannel), each with its parity against the reference's ATen ops true."""
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "3", "--warmup", "1",
+                        "--no-cpu-baseline", "--pmc", "off", "--exchange", "off", "--extras", "on"],
+                       cwd=REPO, capture_output=True, text=True, timeout=170)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])
+    c3, c5, pc = d["c3"], d["c5_int4"], d["pcie"]
+    for o in (c3, c5, pc):
+        assert "error" not in o, o
+    assert c3["parity"] is True and c3["encode_launches"] == 1 and 0 < c3["frac_14B"] < 1, c3
+    assert abs(c3["frac_14B"] / c3["frac_moved"] - 1.4) < 1e-2
+    assert c5["parity"] is True and set(c5["kernels_ms"]) == {"absmax", "quantize_pack", "unpack_dequantize"}, c5
+    assert 0 < c5["frac_13B"] < 1
+    assert pc["pinned_1GiB"]["parity"] is True and pc["channel_c3_dict"]["parity"] is True, pc
+    assert pc["pinned_1GiB"]["pcie_GBs"] > 1 and pc["channel_c3_dict"]["round_trip_ms"] > 0
