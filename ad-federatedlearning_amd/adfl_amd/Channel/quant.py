@@ -23,6 +23,7 @@ There is no CPU fallback: without a GPU and the built HIP library these methods 
 """
 
 import math
+import os
 import threading
 import time
 from collections import OrderedDict
@@ -79,6 +80,7 @@ _STAGING_LOCK = threading.Lock()
 
 
 def _staging() -> _DeviceStaging:
+    hostcopy.keep_host_heap()   # once per process (ADFL_KEEP_HOST_HEAP=0: off)
     idx = torch.cuda.current_device()
     with _STAGING_LOCK:
         st = _STAGING.get(idx)
@@ -113,29 +115,58 @@ def _gather(tensors: List[torch.Tensor], lay: ops.BucketLayout, out: torch.Tenso
     torch.cat(pieces, out=out)
 
 
-_PIECE_BYTES = 8 << 20  # staging pieces of at least this size: one gather + one H2D each
+_PIECE_BYTES = 4 << 20  # staging pieces of at least this size: one gather + one H2D each
+_PIECES = 8             # ... and at most this many per bucket
 
 
 def _ranges(lay: ops.BucketLayout, elem_bytes: int) -> List[Tuple[int, int]]:
-    """The bucket split into element ranges [lo, hi) of about max(_PIECE_BYTES, total / 4) bytes. Ranges
-    may cut through a tensor (one 1 GiB tensor still stages in pipelined pieces)."""
-    step = max(_PIECE_BYTES // elem_bytes, -(-lay.total // 4))
+    """The bucket split into element ranges [lo, hi) of about max(_PIECE_BYTES, total / _PIECES) bytes.
+    Ranges may cut through a tensor (one 1 GiB tensor still stages in pipelined pieces). Eight pieces: the
+    copy engine starts after the first eighth is gathered, and the last eighth's copy is the exposed tail."""
+    step = max(_PIECE_BYTES // elem_bytes, -(-lay.total // _PIECES))
     return [(lo, min(lo + step, lay.total)) for lo in range(0, lay.total, step)]
 
 
-def _range_copies(ptrs: np.ndarray, lay: ops.BucketLayout, base: int, es: int, lo: int, hi: int, to_bucket: bool):
+class _RangePlan:
+    """For one layout and staging range [lo, hi): which tensor each copy piece belongs to, where it starts in
+    that tensor and in the bucket, and its length — everything but the call's pointers, computed once per
+    (layout, range) and cached on the layout (the per-call numpy work was ~20 us per range)."""
+
+    __slots__ = ("k", "t_off", "b_off", "n", "ku")
+
+    def __init__(self, lay: ops.BucketLayout, lo: int, hi: int):
+        a = np.maximum(lay.offsets, lo)
+        b = np.minimum(lay.offsets + lay.sizes, hi)
+        k = np.nonzero(a < b)[0]
+        self.k = k
+        self.ku = k.astype(np.uint64)
+        self.t_off = (a[k] - lay.offsets[k]).astype(np.uint64)
+        self.b_off = a[k].astype(np.uint64)
+        self.n = (b[k] - a[k]).astype(np.int64)
+
+    def copies(self, ptrs: np.ndarray, base: int, es: int, to_bucket: bool):
+        t_ptr = ptrs[self.k] + self.t_off * np.uint64(es)
+        b_ptr = np.uint64(base) + self.b_off * np.uint64(es)
+        nbytes = self.n * es
+        return (b_ptr, t_ptr, nbytes) if to_bucket else (t_ptr, b_ptr, nbytes)
+
+
+def _plan(lay: ops.BucketLayout, lo: int, hi: int) -> _RangePlan:
+    cache = lay.__dict__.setdefault("_range_plans", {})
+    p = cache.get((lo, hi))
+    if p is None:
+        p = cache[(lo, hi)] = _RangePlan(lay, lo, hi)
+    return p
+
+
+def _range_copies(ptrs: np.ndarray, lay: ops.BucketLayout, base: int, es: int, lo: int, hi: int, to_bucket: bool,
+                  with_tensors: bool = False):
     """Byte-copy lists moving bucket elements [lo, hi) between the host bucket at `base` and the tensors
-    whose data pointers are `ptrs` (tensor k at lay.offsets[k]; pads are never copied)."""
-    starts = lay.offsets
-    ends = lay.offsets + lay.sizes
-    a = np.maximum(starts, lo)
-    b = np.minimum(ends, hi)
-    k = np.nonzero(a < b)[0]
-    a, b = a[k], b[k]
-    t_ptr = (ptrs[k] + ((a - starts[k]) * es).astype(np.uint64)).astype(np.uint64)
-    b_ptr = (np.uint64(base) + (a * es).astype(np.uint64)).astype(np.uint64)
-    nbytes = ((b - a) * es).astype(np.int64)
-    return (b_ptr, t_ptr, nbytes) if to_bucket else (t_ptr, b_ptr, nbytes)
+    whose data pointers are `ptrs` (tensor k at lay.offsets[k]; pads are never copied). with_tensors: the
+    tensor index of every piece is returned too."""
+    p = _plan(lay, lo, hi)
+    out = p.copies(ptrs, base, es, to_bucket)
+    return out + (p.k,) if with_tensors else out
 
 
 def _ptrs(tensors: List[torch.Tensor]) -> np.ndarray:
@@ -175,6 +206,9 @@ def _stage_in(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _DeviceSta
     return dev_buf
 
 
+_PIPELINE = os.environ.get("ADFL_HOST_PIPELINE", "1") != "0"
+
+
 class _PendingD2H:
     """D2H of a device bucket into the reused pinned staging, enqueued range by range with an event each;
     finish() scatters every range into the per-tensor CPU storages as soon as its copy lands (the native
@@ -192,6 +226,47 @@ class _PendingD2H:
             ev = torch.cuda.Event()
             ev.record(stream)
             self.events.append(ev)
+
+    def finish_building(self, make, count: int) -> List[torch.Tensor]:
+        """Create the `count` outputs (make(k): a fresh contiguous CPU tensor for tensor k of the layout) in
+        offset order while the D2H runs, and hand each staging range's scatter to the native pool as soon as
+        its copy has landed and every output it touches exists; the pool copies while this thread goes on
+        creating the next outputs (their creation was otherwise serial with the scatter). Returns the outputs
+        once every byte has landed in them. ADFL_HOST_PIPELINE=0: create all, then finish() (the A/B)."""
+        lay = self.lay
+        offs = lay.offsets
+        if not _PIPELINE or count != lay.ntensors or (count > 1 and (np.diff(offs) < 0).any()):
+            outs = [make(k) for k in range(count)]
+            hostcopy.advise_huge(outs)
+            self.finish(outs)
+            return outs
+        es = self.host.element_size()
+        base = self.host.data_ptr()
+        ptrs = np.zeros(count, dtype=np.uint64)
+        outs: List[torch.Tensor] = []
+        pending = []
+        k = 0
+        try:
+            for (lo, hi), ev in zip(self.ranges, self.events):
+                while k < count and offs[k] < hi:   # every tensor the range [lo, hi) touches starts below hi
+                    t = make(k)
+                    if t.is_cuda or not t.is_contiguous() or t.element_size() != es:
+                        raise ValueError("staging: outputs must be contiguous CPU tensors of the bucket's element size")
+                    if t.numel() * es >= (4 << 20):
+                        hostcopy.advise_huge([t])
+                    ptrs[k] = t.data_ptr()
+                    outs.append(t)
+                    k += 1
+                ev.synchronize()   # usually landed already: the outputs took longer than the copy
+                pending.append(hostcopy.submit_pieces(*_range_copies(ptrs, lay, base, es, lo, hi, to_bucket=False),
+                                                      stream=True, keep=self.host))
+            while k < count:   # tensors past the last range (none for a bucket layout; kept for safety)
+                outs.append(make(k))
+                k += 1
+        finally:
+            for pd in pending:
+                pd.wait()
+        return outs
 
     def finish(self, outs: List[torch.Tensor]) -> None:
         """outs: contiguous CPU tensors owned by the caller, tensor k receiving bucket elements at offsets[k]."""
@@ -222,10 +297,8 @@ def _hand_out(out_dev: torch.Tensor, lay: ops.BucketLayout, shapes: List[torch.S
     outs: List[Optional[torch.Tensor]] = [None] * len(shapes)
     if all(on_cpu):
         pending = _PendingD2H(out_dev, lay, st, key)
-        host_outs = [torch.empty(s, dtype=out_dev.dtype) for s in shapes]
-        hostcopy.advise_huge(host_outs)
-        pending.finish(host_outs)
-        return host_outs
+        dt = out_dev.dtype
+        return pending.finish_building(lambda k: torch.empty(shapes[k], dtype=dt), len(shapes))
     if not any(on_cpu) and out_dev.device == st.device:
         # device dict: fresh owned tensors filled from the bucket by one launch (not one clone per tensor)
         dev_outs = [torch.empty(s, dtype=out_dev.dtype, device=st.device) for s in shapes]
@@ -242,16 +315,102 @@ def _hand_out(out_dev: torch.Tensor, lay: ops.BucketLayout, shapes: List[torch.S
     return outs
 
 
+def _host_scales(amax_bits: np.ndarray, bits: int) -> np.ndarray:
+    """fp32(max|x| / q_max) from the magnitude bits the staging gather reduced (quant.py:99-100: fp32 tensor
+    math, correctly rounded; a NaN magnitude gives a NaN scale) — what the device encode computes."""
+    return (amax_bits.view(np.float32) / np.float32((1 << (bits - 1)) - 1)).astype(np.float32)
+
+
+def _encode_host_dict(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _DeviceStaging, bits: int,
+                      stats: Optional[list], emit, idle):
+    """The all-CPU fp32 dict's encode with its outputs built in the shadow of the copies.
+
+    The gather into the pinned bucket is queued on the native pool range by range and reduces max|x| per
+    tensor as it copies (adfl_host_copy_submit_absmax), so a tensor's scale is known on the host as soon as
+    its last byte is staged. While the copy engine moves range r, this thread creates the qint8 outputs of the
+    tensors completed so far (emit(k, q, scale) per tensor) and runs `idle()` (the caller's other payload
+    objects). Then one encode launch, the payload D2H range by range with the native scatter behind it. The
+    device's scales are checked against the host's (a mismatch rebuilds that output with the device's, which
+    the payload was quantized with). Returns [(q, scale)] per tensor."""
+    dev = st.device
+    stream = torch.cuda.current_stream(dev)
+    x_dev = st.buf("x", lay.total, torch.float32)
+    host = st.buf("x_host", lay.total, torch.float32, pinned=True)
+    amax = np.zeros(lay.ntensors, dtype=np.uint32)
+    a_base = amax.ctypes.data
+    ptrs = _ptrs(tensors)
+    ranges = _ranges(lay, 4)
+    jobs = []
+    for lo, hi in ranges:
+        plan = _plan(lay, lo, hi)
+        b_ptr, t_ptr, nb = plan.copies(ptrs, host.data_ptr(), 4, True)
+        jobs.append(hostcopy.submit_pieces(b_ptr, t_ptr, nb, absmax_ptrs=np.uint64(a_base) + plan.ku * np.uint64(4),
+                                           keep=(host, amax)))
+    ends = lay.offsets + lay.sizes
+    eaq, qint8 = torch._empty_affine_quantized, torch.qint8
+    outs: List[torch.Tensor] = []
+    scales = np.zeros(lay.ntensors, dtype=np.float32)
+    made = 0
+    try:
+        for (lo, hi), job in zip(ranges, jobs):
+            job.wait()
+            x_dev[lo:hi].copy_(host[lo:hi], non_blocking=True)
+            done = int(np.searchsorted(ends, hi, side="right"))   # tensors whose every byte is staged
+            if done > made:
+                scales[made:done] = _host_scales(amax[made:done], bits)
+                for k in range(made, done):
+                    sc = float(scales[k])
+                    q = eaq(tensors[k].shape, scale=sc, zero_point=0, dtype=qint8)
+                    outs.append(q)
+                    emit(k, q, sc)
+                made = done
+            idle()
+    finally:
+        for j in jobs:
+            j.wait()
+    q_dev, s_dev = ops.encode_batched(x_dev, lay, bits, q=st.buf("q", lay.total, torch.int8),
+                                      scales=st.buf("scales", lay.ntensors, torch.float32),
+                                      partials=st.buf("partials", lay.nchunks, torch.int32))
+    if stats is not None:
+        stats.extend(ops.qerror_batched(x_dev, q_dev, s_dev, lay))
+    scales_host = st.buf("scales_host", lay.ntensors, torch.float32, pinned=True)
+    scales_host.copy_(s_dev, non_blocking=True)
+    scales_ready = torch.cuda.Event()
+    scales_ready.record(stream)
+    pending = _PendingD2H(q_dev, lay, st, "q")
+    while idle():   # the caller's remaining objects while the kernel and the D2H run
+        pass
+    pending.finish(outs)
+    scales_ready.synchronize()
+    dev_scales = scales_host.numpy()
+    bad = np.nonzero(dev_scales.view(np.uint32) != scales.view(np.uint32))[0]
+    res = [(q, float(sc)) for q, sc in zip(outs, scales)]
+    for k in bad.tolist():   # never seen: both reduce the same bits and divide correctly rounded
+        sc = float(dev_scales[k])
+        q = torch._make_per_tensor_quantized_tensor(_int8_view(outs[k]), sc, 0)
+        res[k] = (q, sc)
+        emit(k, q, sc)
+    return res
+
+
 @_serialized
-def _encode_dict(params: Parameters, names: List[str], bits: int, stats: Optional[list] = None):
+def _encode_dict(params: Parameters, names: List[str], bits: int, stats: Optional[list] = None,
+                 emit=None, idle=None):
     """Encode the ndim>1 tensors `names` of `params` in one bucketed pass.
 
     Returns {name: (qint8 tensor on the input's device, python float scale)}. With `stats` (a list), the
-    four q-error sums of the bucket against its payload are appended to it (ops.qerror_batched)."""
+    four q-error sums of the bucket against its payload are appended to it (ops.qerror_batched). For a dict
+    of contiguous CPU fp32 tensors the outputs are built while the copies run (_encode_host_dict): emit(k, q,
+    scale) is called for each as it is created and idle() (returning True while it has work left) between
+    the copy ranges."""
     st = _staging()
     dev = st.device
     tensors = [params[n] for n in names]
     lay = st.layout(tuple(int(t.numel()) for t in tensors))
+    if _PIPELINE and all(not t.is_cuda and t.is_contiguous() and t.dtype == torch.float32 for t in tensors):
+        res = _encode_host_dict(tensors, lay, st, bits, stats, emit or (lambda k, q, sc: None),
+                                idle or (lambda: False))
+        return {name: r for name, r in zip(names, res)}
     x_dev = _stage_in(tensors, lay, st, "x", torch.float32)
     q_dev, s_dev = ops.encode_batched(x_dev, lay, bits, q=st.buf("q", lay.total, torch.int8),
                                       scales=st.buf("scales", lay.ntensors, torch.float32),
@@ -270,10 +429,9 @@ def _encode_dict(params: Parameters, names: List[str], bits: int, stats: Optiona
         pending = _PendingD2H(q_dev, lay, st, "q")
         scales_ready.synchronize()
         scales = scales_host.tolist()
-        qs = [torch._empty_affine_quantized(t.shape, scale=sc, zero_point=0, dtype=torch.qint8)
-              for t, sc in zip(tensors, scales)]
-        hostcopy.advise_huge(qs)
-        pending.finish(qs)
+        eaq, qint8 = torch._empty_affine_quantized, torch.qint8
+        qs = pending.finish_building(
+            lambda k: eaq(tensors[k].shape, scale=scales[k], zero_point=0, dtype=qint8), len(tensors))
         return {name: (qt, sc) for name, qt, sc in zip(names, qs, scales)}
     torch.cuda.current_stream(dev).synchronize()
     scales = scales_host.tolist()
@@ -306,10 +464,11 @@ def _decode_dict(items: List[Tuple[str, torch.Tensor]]) -> Dict[str, torch.Tenso
     """Decode qint8 tensors (per-tensor affine, zero point 0) in one bucketed pass."""
     st = _staging()
     dev = st.device
+    qint8, pta = torch.qint8, torch.per_tensor_affine
     for name, q in items:
-        if q.qscheme() != torch.per_tensor_affine or q.dtype != torch.qint8 or q.q_zero_point() != 0:
+        if q.dtype != qint8 or q.qscheme() != pta or q.q_zero_point() != 0:
             raise ValueError(f"SLQChannel: '{name}' is not a per-tensor qint8 payload with zero point 0")
-    lay = st.layout(tuple(int(q.numel()) for _, q in items))
+    lay = st.layout(tuple([q.numel() for _, q in items]))
     # CPU qint8 payloads are gathered byte-wise straight from their storage; device ones through int8 views
     all_host = all(not q.is_cuda and q.is_contiguous() for _, q in items)
     all_dev = all(q.is_cuda and q.device == dev and q.is_contiguous() for _, q in items)
@@ -659,19 +818,36 @@ class SLQChannel(Channel):
         names = [name for name, p in params.items() if p.ndim > 1]
         for name in names:
             ops.require_quantizable(params[name])
-        encoded = _encode_dict(params, names, bits, stats) if names else {}
-        q_params = QuantParameters({}, 0)
         signs = torch.zeros(1, dtype=torch.uint8)  # the unused field (quant.py:91), one object per call
-        for name, param in params.items():
-            if name in encoded:
-                q_param, scale = encoded[name]
-            else:
-                q_param, scale = param, 1
-            q_params.params[name] = QuantParameter(
-                data=q_param, bits=bits, scale=scale, signs=signs,
-                shape=param.shape, dtype=param.dtype, q_dtype=q_param.dtype)
-            q_params.size += q_param.nbytes
-        return q_params
+        qp = QuantParameter
+        made: Dict[str, QuantParameter] = {}
+        size = [0]
+        # positional: QuantParameter(data, bits, scale, signs, shape, dtype, q_dtype) (model.py:21-31)
+
+        def emit(k, q, scale):   # a quantized entry, built as soon as its output exists
+            n = names[k]
+            p = params[n]
+            if n not in made:
+                size[0] += q.numel()          # a qint8 payload: one byte per element
+            made[n] = qp(q, bits, scale, signs, p.shape, p.dtype, q.dtype)
+        rest = iter([(n, p) for n, p in params.items() if p.ndim <= 1])
+
+        def idle(batch=32):      # passthrough entries (quant.py:80-81), a batch per copy range
+            for _ in range(batch):
+                e = next(rest, None)
+                if e is None:
+                    return False
+                t = e[1]
+                made[e[0]] = qp(t, bits, 1, signs, t.shape, t.dtype, t.dtype)
+                size[0] += t.nbytes
+            return True
+        encoded = _encode_dict(params, names, bits, stats, emit=emit, idle=idle) if names else {}
+        for k, n in enumerate(names):
+            if n not in made:    # device dicts and the other staging paths: built here
+                emit(k, *encoded[n])
+        while idle():
+            pass
+        return QuantParameters({name: made[name] for name in params}, size[0])
 
 
 class USLQChannel(SLQChannel):

@@ -92,6 +92,10 @@ SIGNATURES = {
     "adfl_host_copy": (INT, [P, P, P, I64, I32]),
     "adfl_host_copy_ex": (INT, [P, P, P, I64, I32, I32]),
     "adfl_host_threads": (I32, []),
+    "adfl_host_copy_submit": (I64, [P, P, P, I64, I32, I32, P, P]),
+    "adfl_host_copy_wait": (INT, [I64]),
+    "adfl_host_copy_submit_absmax": (I64, [P, P, P, I64, I32, I32, P, P, P]),
+    "adfl_event_synchronize": (INT, [P]),
 }
 
 NORM_L2, NORM_LINF, NORM_L2_TORCH = 0, 1, 2  # ADFL_NORM_*

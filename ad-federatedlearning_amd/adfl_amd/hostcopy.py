@@ -25,7 +25,8 @@ def _host_lib():
         path = os.environ.get("ADFL_HOST_LIB")
         if path:
             lib = ctypes.CDLL(path)
-            for name in ("adfl_host_copy", "adfl_host_copy_ex", "adfl_host_threads"):
+            for name in ("adfl_host_copy", "adfl_host_copy_ex", "adfl_host_threads", "adfl_host_copy_submit",
+                         "adfl_host_copy_wait", "adfl_host_copy_submit_absmax"):
                 fn = getattr(lib, name)
                 fn.restype, fn.argtypes = _lib.SIGNATURES[name]
             _host = lib
@@ -48,6 +49,71 @@ def copy_pieces(dst_ptrs: Sequence[int], src_ptrs: Sequence[int], nbytes: Sequen
         raise ValueError("copy_pieces: pointer and size lists differ in length")
     check(_host_lib().adfl_host_copy_ex(d.ctypes.data, s.ctypes.data, b.ctypes.data, len(b), threads,
                                         STREAM if stream else 0))
+
+
+class Pending:
+    """An asynchronous copy job (adfl_host_copy_submit): the pool's workers run it — after `event` has
+    completed, when one is given — while the caller's thread goes on; wait() blocks (GIL released) until every
+    byte is copied. The arrays and tensors named by the job are kept alive here until then."""
+
+    __slots__ = ("ticket", "_keep")
+
+    def __init__(self, ticket: int, keep):
+        self.ticket = ticket
+        self._keep = keep
+
+    def wait(self) -> None:
+        if self.ticket:
+            t, self.ticket = self.ticket, 0
+            self._keep = None
+            check(_host_lib().adfl_host_copy_wait(t))
+
+    def __del__(self):   # a job is always waited for: its buffers must outlive the copy
+        try:
+            self.wait()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+_event_wait = None
+
+
+def _event_wait_fn() -> int:
+    """Address of adfl_event_synchronize (the HIP library's own export) for the pool's wait callback."""
+    global _event_wait
+    if _event_wait is None:
+        _event_wait = ctypes.cast(_lib.load().adfl_event_synchronize, ctypes.c_void_p).value
+    return _event_wait
+
+
+def submit_pieces(dst_ptrs: Sequence[int], src_ptrs: Sequence[int], nbytes: Sequence[int], *, stream: bool = False,
+                  event: "torch.cuda.Event | None" = None, keep=None, threads: int = 0,
+                  absmax_ptrs: "np.ndarray | None" = None) -> Pending:
+    """copy_pieces on the pool's workers, asynchronously; with `event` (a recorded torch.cuda.Event) every
+    part first waits for it (hipEventSynchronize), so the copy starts the moment the D2H that fills its
+    source lands. `keep`: objects the copy reads or writes, held until wait(). `absmax_ptrs` (uint64 per
+    piece, 0 = none): fp32 pieces whose max |bits| is max'ed into the uint32 at that address
+    (adfl_host_copy_submit_absmax)."""
+    d = np.ascontiguousarray(dst_ptrs, dtype=np.uint64)
+    s = np.ascontiguousarray(src_ptrs, dtype=np.uint64)
+    b = np.ascontiguousarray(nbytes, dtype=np.int64)
+    if not (len(d) == len(s) == len(b)):
+        raise ValueError("submit_pieces: pointer and size lists differ in length")
+    fn, arg = (None, None) if event is None else (_event_wait_fn(), event.cuda_event)
+    if absmax_ptrs is not None:
+        a = np.ascontiguousarray(absmax_ptrs, dtype=np.uint64)
+        if len(a) != len(b):
+            raise ValueError("submit_pieces: one absmax slot per piece")
+        t = _host_lib().adfl_host_copy_submit_absmax(d.ctypes.data, s.ctypes.data, b.ctypes.data, len(b), threads,
+                                                     STREAM if stream else 0, fn, arg, a.ctypes.data)
+        if t <= 0:
+            check(int(t))
+        return Pending(int(t), (keep, event, a))
+    t = _host_lib().adfl_host_copy_submit(d.ctypes.data, s.ctypes.data, b.ctypes.data, len(b), threads,
+                                          STREAM if stream else 0, fn, arg)
+    if t <= 0:
+        check(int(t))
+    return Pending(int(t), (keep, event))
 
 
 def gather(srcs: Sequence[torch.Tensor], dst: torch.Tensor, offsets: Sequence[int]) -> None:
@@ -102,6 +168,34 @@ def advise_huge(tensors: Sequence[torch.Tensor], min_bytes: int = 4 << 20) -> No
         e = (p + nb) // _HUGE * _HUGE
         if e > a:
             _libc.madvise(a, e - a, _MADV_HUGEPAGE)  # failure is harmless: the advice is simply not taken
+
+
+_M_TRIM_THRESHOLD, _M_MMAP_THRESHOLD = -1, -3   # glibc mallopt parameters (malloc.h)
+_heap_kept = None
+
+
+def keep_host_heap() -> bool:
+    """Keep freed host memory in the process heap instead of returning it to the kernel after every call:
+    glibc's mallopt(M_MMAP_THRESHOLD, 32 MiB) puts the channel's per-tensor outputs (ResNet-18's are about
+    180 KiB each, above glibc's 128 KiB default, so each was a fresh mmap: 256 page-fault storms and munmaps
+    per call) on the heap, and mallopt(M_TRIM_THRESHOLD, 1 GiB) keeps up to 1 GiB of freed heap resident. A
+    round's outputs then reuse the pages of the previous round's: no first-touch faults in the scatter, no
+    munmap on free, no mmap_lock contention between the allocating thread and the copying pool. Called once,
+    on the first host-resident channel call; ADFL_KEEP_HOST_HEAP=0 leaves the allocator as it is.
+    Returns whether the setting is in force."""
+    global _heap_kept
+    if _heap_kept is None:
+        _heap_kept = False
+        if os.environ.get("ADFL_KEEP_HOST_HEAP", "1") != "0":
+            try:
+                libc = ctypes.CDLL("libc.so.6")
+                libc.mallopt.argtypes = [ctypes.c_int, ctypes.c_int]
+                libc.mallopt.restype = ctypes.c_int
+                _heap_kept = bool(libc.mallopt(_M_MMAP_THRESHOLD, 32 << 20)) and \
+                    bool(libc.mallopt(_M_TRIM_THRESHOLD, 1 << 30))
+            except (OSError, AttributeError):
+                _heap_kept = False
+    return _heap_kept
 
 
 def threads() -> int:

@@ -14,6 +14,7 @@
 
 #include <cstdint>
 
+#include "adfl_host.h"
 #include "adfl_slq.h"
 
 namespace {
@@ -81,6 +82,12 @@ int launch(bool to_bucket, void* d_bucket, const adfl_slq_chunk* d_chunks, int64
 }  // namespace
 
 extern "C" {
+
+// include/adfl_host.h: the completion wait the host copy pool runs before scattering a staging range.
+int adfl_event_synchronize(void* event) {
+  const hipError_t e = hipEventSynchronize(static_cast<hipEvent_t>(event));
+  return e == hipSuccess ? 0 : (int)e;
+}
 
 int adfl_bucket_gather(void* d_bucket, const adfl_slq_chunk* d_chunks, int64_t nchunks, const void* const* d_srcs,
                        int32_t elem_bytes, void* stream) {

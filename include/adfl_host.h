@@ -30,7 +30,33 @@ enum { ADFL_HOST_COPY_STREAM = 1 };
 int adfl_host_copy_ex(void* const* dsts, const void* const* srcs, const int64_t* nbytes, int64_t n, int32_t nthreads,
                       int32_t flags);
 
-/* Threads the pool would use for nthreads <= 0 (for logging and tests). */
+/* Asynchronous adfl_host_copy_ex: the copy list is copied, queued behind earlier jobs and run by the pool's
+ * worker threads only; the call returns at once with a ticket (> 0) or ADFL_E_ARG. If wait_fn is not null,
+ * every part first calls wait_fn(wait_arg) and copies only when it returns 0 (the host-resident channel passes
+ * adfl_event_synchronize and a HIP event recorded after the D2H that fills the source, so the scatter of a
+ * staging range starts the moment its copy lands while the caller's thread builds the output tensors).
+ * The buffers must stay valid until adfl_host_copy_wait(ticket) returns; every ticket is waited exactly once.
+ * adfl_host_copy_wait returns 0, or the first nonzero status a wait_fn returned. */
+int64_t adfl_host_copy_submit(void* const* dsts, const void* const* srcs, const int64_t* nbytes, int64_t n,
+                              int32_t nthreads, int32_t flags, int (*wait_fn)(void*), void* wait_arg);
+int adfl_host_copy_wait(int64_t ticket);
+
+/* adfl_host_copy_submit that also reduces what it copies: piece k is fp32 (nbytes[k] and srcs[k] multiples of
+ * 4) and, when absmax_bits[k] is not null, max over its elements of (bits & 0x7fffffff) is max'ed atomically
+ * into *absmax_bits[k] — torch.max(torch.abs(t)) as an unsigned compare of the magnitude bits, NaN winning
+ * (Src/ADFL/Channel/quant.py:100), exactly as the device encode reduces it. The host-resident SLQ encode
+ * gathers a CPU state dict this way, so every tensor's scale is known on the host when its bytes reach the
+ * pinned bucket and its qint8 output can be built while the H2D and the kernels run. ADFL_E_ARG for a piece
+ * that is not whole fp32 words. */
+int64_t adfl_host_copy_submit_absmax(void* const* dsts, const void* const* srcs, const int64_t* nbytes, int64_t n,
+                                     int32_t nthreads, int32_t flags, int (*wait_fn)(void*), void* wait_arg,
+                                     uint32_t* const* absmax_bits);
+
+/* hipEventSynchronize(event) as an int-returning callback for adfl_host_copy_submit (0 = complete). */
+int adfl_event_synchronize(void* event);
+
+/* Threads the pool would use for nthreads <= 0 (for logging and tests): the CPUs in this process's affinity
+ * mask, at most 16, or ADFL_HOST_THREADS when set. */
 int32_t adfl_host_threads(void);
 
 #ifdef __cplusplus

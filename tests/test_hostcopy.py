@@ -104,3 +104,50 @@ def test_advise_huge_is_advice_only():
     ts[2].fill_(3)
     assert torch.equal(ts[0], torch.arange(10, dtype=torch.float32)) and int(ts[1].abs().sum()) == 0
     assert int(ts[2].sum()) == 3 * ((5 << 20) - 1)
+
+
+def test_async_submit_and_wait():
+    """hostcopy.submit_pieces (adfl_host_copy_submit): jobs queued behind each other run on the pool's workers
+    while the caller goes on; wait() returns when every byte is in place (the channel's pipelined scatter)."""
+    rng = np.random.default_rng(5)
+    srcs = [torch.from_numpy(rng.standard_normal(n).astype(np.float32)) for n in (1, 70_001, 3_000_000, 0, 513)]
+    dsts = [torch.full_like(s, -7.0) for s in srcs]
+    jobs = [hostcopy.submit_pieces([d.data_ptr()], [s.data_ptr()], [s.numel() * 4], stream=bool(i % 2), keep=(s, d))
+            for i, (s, d) in enumerate(zip(srcs, dsts))]
+    for j in reversed(jobs):
+        j.wait()
+        j.wait()   # idempotent
+    for s, d in zip(srcs, dsts):
+        assert torch.equal(s, d)
+    lib = _lib.load()
+    assert lib.adfl_host_copy_wait(0) == -1
+    with pytest.raises(ValueError):
+        hostcopy.submit_pieces([1, 2], [3], [4])
+
+
+def test_async_gather_reduces_absmax_bits():
+    """adfl_host_copy_submit_absmax: the staging gather of the host-resident SLQ encode reduces max|x| per
+    tensor as it copies — the magnitude bits' unsigned max (NaN wins, -0 is 0, denormals kept), the value
+    torch.max(torch.abs(t)) gives (quant.py:100) — whatever the piece split across threads."""
+    rng = np.random.default_rng(9)
+    sizes = [1, 3, 1_000_003, 70_000, 4, 2_000_000, 17]
+    xs = [rng.standard_normal(n).astype(np.float32) * np.float32(10.0 ** (i - 3)) for i, n in enumerate(sizes)]
+    xs[1][:] = [-0.0, 1e-40, -3e-45]                  # denormals only
+    xs[2][123_457] = np.float32(np.inf) * -1          # -inf
+    xs[4][2] = np.nan                                  # NaN wins
+    xs[6][:] = 0.0
+    srcs = [torch.from_numpy(x) for x in xs]
+    bucket = torch.empty(sum(sizes))
+    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
+    amax = np.zeros(len(sizes), np.uint32)
+    job = hostcopy.submit_pieces([bucket.data_ptr() + 4 * int(o) for o in offs], [s.data_ptr() for s in srcs],
+                                 [4 * n for n in sizes], absmax_ptrs=np.uint64(amax.ctypes.data) +
+                                 np.arange(len(sizes), dtype=np.uint64) * np.uint64(4), keep=(srcs, bucket, amax))
+    job.wait()
+    assert np.array_equal(bucket.numpy().view(np.uint32), np.concatenate(xs).view(np.uint32))
+    for k, x in enumerate(xs):
+        want = torch.max(torch.abs(torch.from_numpy(x))).numpy()
+        got = amax[k:k + 1].view(np.float32)[0]
+        assert (np.isnan(got) and np.isnan(want)) or got.view(np.uint32) == want.view(np.uint32), k
+    with pytest.raises(Exception):   # pieces that are not whole fp32 words
+        hostcopy.submit_pieces([bucket.data_ptr()], [srcs[2].data_ptr()], [6], absmax_ptrs=[amax.ctypes.data])
