@@ -44,6 +44,7 @@ class _DeviceStaging:
 
     def __init__(self, device: torch.device):
         self.device = device
+        self.cpus = hostcopy.bind_to_device(device)   # the copy pool on the GPU's NUMA node
         self.lock = threading.RLock()
         self._bufs: Dict[str, torch.Tensor] = {}
         self.layouts: "OrderedDict[Tuple[int, ...], ops.BucketLayout]" = OrderedDict()
@@ -53,7 +54,8 @@ class _DeviceStaging:
         if t is None or t.numel() < numel:
             numel = max(numel, 1)
             if pinned:
-                t = torch.empty(numel, dtype=dtype, pin_memory=True)
+                with hostcopy.on_cpus(self.cpus):   # pages on the GPU's NUMA node
+                    t = torch.empty(numel, dtype=dtype, pin_memory=True)
             else:
                 t = torch.empty(numel, dtype=dtype, device=self.device)
             self._bufs[key] = t

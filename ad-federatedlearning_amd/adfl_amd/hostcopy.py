@@ -26,7 +26,7 @@ def _host_lib():
         if path:
             lib = ctypes.CDLL(path)
             for name in ("adfl_host_copy", "adfl_host_copy_ex", "adfl_host_threads", "adfl_host_copy_submit",
-                         "adfl_host_copy_wait", "adfl_host_copy_submit_absmax"):
+                         "adfl_host_copy_wait", "adfl_host_copy_submit_absmax", "adfl_host_bind"):
                 fn = getattr(lib, name)
                 fn.restype, fn.argtypes = _lib.SIGNATURES[name]
             _host = lib
@@ -196,6 +196,66 @@ def keep_host_heap() -> bool:
             except (OSError, AttributeError):
                 _heap_kept = False
     return _heap_kept
+
+
+def _cpulist(text: str):
+    cpus = []
+    for part in text.strip().split(","):
+        if part:
+            a, _, b = part.partition("-")
+            cpus.extend(range(int(a), int(b or a) + 1))
+    return cpus
+
+
+def device_cpus(device: "torch.device") -> "list[int]":
+    """The CPUs of the NUMA node the GPU hangs off (sysfs local_cpulist of its PCI function), within this
+    process's affinity mask; [] when unknown."""
+    try:
+        p = torch.cuda.get_device_properties(device)
+        path = f"/sys/bus/pci/devices/{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+        with open(os.path.join(path, "local_cpulist")) as f:
+            cpus = _cpulist(f.read())
+    except (OSError, ValueError, AttributeError, RuntimeError):
+        return []
+    allowed = os.sched_getaffinity(0)
+    return [c for c in cpus if c in allowed] if len(cpus) < os.cpu_count() else []
+
+
+_bound = {}
+
+
+def bind_to_device(device: "torch.device") -> "list[int]":
+    """Pin the copy pool's workers to the GPU's NUMA node (once per process; ADFL_HOST_BIND=0: never). The
+    pinned staging buckets are allocated from a thread on that node too (on_cpus). Returns the CPUs used."""
+    key = (device.type, device.index)
+    if key not in _bound:
+        cpus = device_cpus(device) if os.environ.get("ADFL_HOST_BIND", "1") != "0" else []
+        if cpus:
+            arr = np.asarray(cpus, dtype=np.int32)
+            if _host_lib().adfl_host_bind(arr.ctypes.data, len(arr)) != 0:
+                cpus = []
+        _bound[key] = cpus
+    return _bound[key]
+
+
+class on_cpus:
+    """Run a block with this thread's affinity set to `cpus` (restored after): a pinned host buffer allocated
+    inside gets its pages on their NUMA node. No-op for an empty list."""
+
+    def __init__(self, cpus):
+        self.cpus = cpus
+        self.old = None
+
+    def __enter__(self):
+        if self.cpus:
+            self.old = os.sched_getaffinity(0)
+            os.sched_setaffinity(0, self.cpus)
+        return self
+
+    def __exit__(self, *exc):
+        if self.old is not None:
+            os.sched_setaffinity(0, self.old)
+        return False
 
 
 def threads() -> int:

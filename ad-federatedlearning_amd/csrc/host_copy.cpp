@@ -4,6 +4,7 @@
 
 #include <emmintrin.h>
 
+#include <pthread.h>
 #include <sched.h>
 
 #include <algorithm>
@@ -21,7 +22,7 @@
 
 namespace {
 
-constexpr int kMaxThreads = 16;
+constexpr int kMaxThreads = 8;  // host channel A/B on the GPU box: 8 and 4 beat 16 (profiles/r04/host_channel)
 constexpr int64_t kMinBytesPerThread = 256 << 10;  // below this, extra threads cost more than they copy
 
 // One list of copies. Synchronous jobs (adfl_host_copy_ex) borrow the caller's arrays and the caller's
@@ -154,6 +155,25 @@ class Pool {
   int size() const { return (int)workers_.size() + 1; }
   int workers() const { return (int)workers_.size(); }
 
+  // pin every worker to `cpus` (the GPU's NUMA node: the staging copies then run next to the pinned buckets
+  // and the GPU's PCIe root)
+  int bind(const int32_t* cpus, int32_t n) {
+#ifdef __linux__
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    for (int32_t i = 0; i < n; ++i)
+      if (cpus[i] >= 0 && cpus[i] < CPU_SETSIZE) CPU_SET(cpus[i], &set);
+    if (CPU_COUNT(&set) == 0) return -1;
+    for (auto& h : handles_)
+      if (pthread_setaffinity_np(h, sizeof(set), &set) != 0) return -1;
+    return 0;
+#else
+    (void)cpus;
+    (void)n;
+    return -1;
+#endif
+  }
+
   void run(Job& job) {
     push(&job);
     int p;
@@ -177,7 +197,7 @@ class Pool {
 
  private:
   // threads = the CPUs this process may run on (its affinity mask, not the machine's count: a container or a
-  // job share sees 16 of 256), at most kMaxThreads, or ADFL_HOST_THREADS when set (1 = the caller only)
+  // job share may see fewer), at most kMaxThreads, or ADFL_HOST_THREADS when set (1 = the caller only)
   static int pool_threads() {
     int hw = (int)std::thread::hardware_concurrency();
 #ifdef __linux__
@@ -195,7 +215,10 @@ class Pool {
   Pool() {
     const int n = pool_threads() - 1;
     for (int i = 0; i < n; ++i) workers_.emplace_back([this] { loop(); });
-    for (auto& t : workers_) t.detach();
+    for (auto& t : workers_) {
+      handles_.push_back(t.native_handle());
+      t.detach();
+    }
   }
 
   // the caller's claim on its own (synchronous) job
@@ -237,6 +260,7 @@ class Pool {
   }
 
   std::vector<std::thread> workers_;
+  std::vector<std::thread::native_handle_type> handles_;
   std::mutex mu_;
   std::condition_variable cv_, done_cv_;
   std::deque<Job*> queue_;
@@ -331,6 +355,11 @@ int64_t adfl_host_copy_submit_absmax(void* const* dsts, const void* const* srcs,
     pool.push(job);
   }
   return reinterpret_cast<int64_t>(job);
+}
+
+int adfl_host_bind(const int32_t* cpus, int32_t n) {
+  if (!cpus || n < 1) return ADFL_E_ARG;
+  return Pool::get().bind(cpus, n) == 0 ? ADFL_OK : ADFL_E_ARG;
 }
 
 int adfl_host_copy_wait(int64_t ticket) {
