@@ -149,6 +149,12 @@ def _encode_stoch(params: Parameters, names: List[str], codec: str, bits: int, u
     return _payloads(names, datas, signs, nm, lay.ntensors, codec)
 
 
+# Philox block-counter base of each dtype bucket: one seed serves an fp32 bucket and every fp16 / bf16 / fp64
+# bucket of the same call, and each draws from its own disjoint part of the stream (2^40 blocks = 2^42
+# uniforms each), so no two buckets' rounding decisions share a uniform.
+COUNTER_BASE = {torch.float32: 0, torch.float16: 1 << 40, torch.bfloat16: 2 << 40, torch.float64: 3 << 40}
+
+
 @_serialized
 def _encode_stoch_dt(params: Parameters, names: List[str], codec: str, bits: int, uniforms=None, seed=None):
     """Encode the ndim > 1 tensors `names` (all of one dtype: fp16 / bf16 / fp64) in one bucketed pass, in
@@ -165,7 +171,8 @@ def _encode_stoch_dt(params: Parameters, names: List[str], codec: str, bits: int
         seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
     ws = st.buf("stoch_ws", lay.nchunks * 16, torch.uint8)
     u = uniforms if uniforms is not None and uniforms.dtype == dtype else None
-    lv, sg, norms, mins = sops.encode_batched_dt(codec, x_dev, lay, bits, uniforms=u, seed=seed, counter=0,
+    lv, sg, norms, mins = sops.encode_batched_dt(codec, x_dev, lay, bits, uniforms=u, seed=seed,
+                                                 counter=COUNTER_BASE[dtype],
                                                  levels=st.buf("s_levels", lay.total, torch.uint8).view(
                                                      torch.int8 if codec == "cnat" else torch.uint8),
                                                  signs=st.buf("s_signs", lay.total, torch.int8), ws=ws)
@@ -409,6 +416,9 @@ class _StochChannel(Channel):
         names = [name for name, p in params.items() if p.ndim > 1 and p.numel() > 0]
         for name in names:
             _require_codable(name, params[name], self.__class__.__name__)
+        if uniforms is not None and {params[n].dtype for n in names} - {uniforms.dtype}:
+            raise ValueError(f"{self.__class__.__name__}: injected uniforms ({uniforms.dtype}) cover one dtype bucket; "
+                             f"this dict also holds {sorted(str(d) for d in {params[n].dtype for n in names})}")
         f32 = [n for n in names if params[n].dtype == torch.float32]
         encoded = (_encode_stoch(params, f32, self.CODEC, bits, uniforms if uniforms is None or
                                  uniforms.dtype == torch.float32 else None, seed,

@@ -22,13 +22,22 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp
 def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(LIB_DIR, exist_ok=True)
     deps = DEPENDS + [os.path.join(INCLUDE, h) for h in ("adfl_slq.h", "adfl_stoch.h", "adfl_host.h")]
-    if (not force and os.path.exists(LIB_PATH)
+    stamp = LIB_PATH + ".rounds"
+    want = os.environ.get("ADFL_PHILOX_ROUNDS", "7")
+    built = open(stamp).read().strip() if os.path.exists(stamp) else "7"
+    if (not force and os.path.exists(LIB_PATH) and built == want
             and os.path.getmtime(LIB_PATH) >= max(os.path.getmtime(d) for d in deps)):
         return LIB_PATH
-    cmd = [HIPCC, *FLAGS, f"-I{INCLUDE}", "-o", LIB_PATH, *SOURCES]
+    rounds = int(os.environ.get("ADFL_PHILOX_ROUNDS", "7"))
+    if rounds not in (7, 10):
+        raise ValueError("ADFL_PHILOX_ROUNDS must be 7 (the product) or 10 (Random123's margin)")
+    defs = [] if rounds == 7 else [f"-DADFL_PHILOX_ROUNDS={rounds}"]
+    cmd = [HIPCC, *FLAGS, *defs, f"-I{INCLUDE}", "-o", LIB_PATH, *SOURCES]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
+    with open(stamp, "w") as f:
+        f.write(f"{rounds}\n")
     return LIB_PATH
 
 

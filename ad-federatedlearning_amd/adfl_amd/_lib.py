@@ -95,6 +95,7 @@ SIGNATURES = {
     "adfl_host_copy_submit": (I64, [P, P, P, I64, I32, I32, P, P]),
     "adfl_host_copy_wait": (INT, [I64]),
     "adfl_host_bind": (INT, [P, I32]),
+    "adfl_philox_rounds": (INT, []),
     "adfl_host_copy_submit_absmax": (I64, [P, P, P, I64, I32, I32, P, P, P]),
     "adfl_event_synchronize": (INT, [P]),
 }

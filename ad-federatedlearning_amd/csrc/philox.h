@@ -2,6 +2,20 @@
 // stoch_codec.hip (fp32 tensors) and stoch_dtype.hip (fp16 / bf16 / fp64 tensors). Round function,
 // multipliers and key schedule are Philox4x32's (pinned by the 10-round known-answer vectors in
 // tests/test_stoch_golden.py); the codecs run R = 7 rounds (stoch_codec.hip header).
+//
+// Why 7: Salmon et al. (SC'11, Table 2) report Philox4x32-7 as the fewest rounds that pass all of TestU01's
+// BigCrush ("Crush-resistant"); 10 rounds is Random123's and curand's default safety margin. These codecs
+// compare each uniform with a threshold at 24-bit resolution (fp16 / bf16: 11 / 8 bits), and the
+// reference's own draws are torch.rand_like's mt19937, so no run is bit-comparable with the reference's
+// stream under any R. What is tested here: the 7-round words continued by 3 more rounds give the 10-round
+// known answers (round function, multipliers, key schedule pinned), and the 7-round stream's statistics on
+// 2^20 draws — a 256-bucket chi-square, lag-1 and lag-4 correlation, each of the 24 used bits at 1/2
+// (tests/test_stoch_golden.py: test_philox_7_rounds_is_a_prefix_of_the_known_answer_computation,
+// test_philox_7_round_stream_statistics), plus the unbiased-decode and CNAT frequency checks on the GPU.
+// BigCrush / PractRand themselves are not in this image. For the standard margin, build with
+// ADFL_PHILOX_ROUNDS=10 in the environment (adfl_amd/_build.py passes -DADFL_PHILOX_ROUNDS; the oracle,
+// oracle/stoch_oracle.py, reads the same variable; adfl_philox_rounds() reports what was compiled). Streams
+// for a fixed (seed, counter) differ between the two builds.
 #pragma once
 
 #include <hip/hip_runtime.h>

@@ -1461,6 +1461,8 @@ int adfl_stoch_dequantize_mean_batched(int32_t codec, const uint8_t* d_levels, c
   return launch_status();
 }
 
+int adfl_philox_rounds(void) { return adfl::kPhiloxRounds; }
+
 int adfl_philox_uniforms(float* d_out, int64_t n, int64_t start, uint64_t seed, uint64_t counter, void* stream) {
   if (!d_out || n < 1 || start < 0) return ADFL_E_ARG;
   const Uniforms U{nullptr, seed, counter};

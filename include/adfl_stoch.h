@@ -131,6 +131,10 @@ int adfl_cnat_encode_batched_work(const float* d_x, const adfl_slq_chunk* d_chun
  * (Exposed for tests and for callers that want the uniforms a call used.) */
 int adfl_philox_uniforms(float* d_out, int64_t n, int64_t start, uint64_t seed, uint64_t counter, void* stream);
 
+/* The Philox4x32 round count this library was built with: 7 (the product) or 10 (an ADFL_PHILOX_ROUNDS=10
+ * build; csrc/philox.h records why 7). */
+int adfl_philox_rounds(void);
+
 /* ---- fp16 / bf16 / fp64 tensors -------------------------------------------------------------------
  * The reference computes QSGD / RQSGD / CNAT in the tensor's own dtype (quant.py:223-240, :364-382,
  * :509-534): each op on fp16 / bf16 computes in fp32 and rounds to the dtype; fp64 ops are fp64. These

@@ -41,6 +41,8 @@ from a counter-based Philox4x32-7 stream instead (``philox_uniforms`` below rest
 takes injected uniforms; with the same uniforms every output is bit-identical to the reference.
 """
 
+import os
+
 import numpy as np
 
 F32 = np.float32
@@ -207,7 +209,9 @@ def cnat_dequantize(e: np.ndarray, signs: np.ndarray, norm) -> np.ndarray:
 # ------------------------------------------------------------------------------------------------
 PHILOX_M0, PHILOX_M1 = 0xD2511F53, 0xCD9E8D57
 PHILOX_W0, PHILOX_W1 = 0x9E3779B9, 0xBB67AE85
-PHILOX_ROUNDS = 7      # the codec's stream; 10 is Random123's / curand's default (known-answer vectors)
+# the codec's stream; 10 is Random123's / curand's default (known-answer vectors). ADFL_PHILOX_ROUNDS=10
+# follows an opt-in 10-round build of the library (csrc/philox.h)
+PHILOX_ROUNDS = int(os.environ.get("ADFL_PHILOX_ROUNDS", "7"))
 MASK32 = 0xFFFFFFFF
 
 

@@ -168,3 +168,10 @@ def test_build_chunks_host_planning():
     zero = sizes.copy()
     zero[0] = 0
     assert lib.adfl_slq_build_chunks(offsets.ctypes.data, zero.ctypes.data, len(sizes), None, 0) == -1
+
+
+def test_philox_rounds_match_the_oracle():
+    """The stochastic codecs' stream is Philox4x32-7 unless the library was built with ADFL_PHILOX_ROUNDS=10
+    (csrc/philox.h); the oracle follows the same variable."""
+    import stoch_oracle as so
+    assert _lib.load().adfl_philox_rounds() == so.PHILOX_ROUNDS

@@ -27,6 +27,7 @@ pytestmark = pytest.mark.gpu
 adfl_amd = pytest.importorskip("adfl_amd")
 from adfl_amd import ops, stoch  # noqa: E402
 from adfl_amd.Channel import CNATChannel, QSGDChannel, RQSGDChannel  # noqa: E402
+from adfl_amd.Channel import stoch as stoch_channel  # noqa: E402
 
 DEV = torch.device("cuda", 0)
 MANIFEST = json.load(open(os.path.join(GOLDEN, "stoch_dt_manifest.json")))
@@ -159,10 +160,11 @@ def test_channel_mixed_dtype_dict(codec):
             continue
         dt = {torch.float16: do.DT_F16, torch.bfloat16: do.DT_BF16, torch.float64: do.DT_F64}[x.dtype]
         raw = x.numpy() if dt == do.DT_F64 else x.view(torch.int16).numpy().view(np.uint16)
-        # the dtype bucket holds this dtype's tensors back to back (z16 after w16 for fp16), stream counter 0
+        # the dtype bucket holds this dtype's tensors back to back (z16 after w16 for fp16), drawing from its own
+        # part of the stream (Channel.stoch.COUNTER_BASE: disjoint from the fp32 bucket's and the others')
         group = [n for n in params if params[n].ndim > 1 and params[n].dtype == x.dtype]
         off = sum(params[n].numel() for n in group[:group.index(name)])
-        u = do.philox_uniforms_dt(dt, x.numel(), seed, 0, start=off)
+        u = do.philox_uniforms_dt(dt, x.numel(), seed, stoch_channel.COUNTER_BASE[x.dtype], start=off)
         norm = p.scale
         qo, so_ = do.quantize(codec, raw.reshape(-1), dt, 8, norm, u)
         np.testing.assert_array_equal(p.data.numpy().reshape(-1).view(np.uint8), qo.view(np.uint8), err_msg=name)
@@ -196,3 +198,19 @@ def test_large_tensor_multichunk_norm_and_bytes(dtname, n):
         qo, so_ = do.quantize(codec, raw, dt, 8, norm, do.philox_uniforms_dt(dt, n, 77, 0))
         assert np.array_equal(q.cpu().numpy().view(np.uint8), qo.view(np.uint8)), codec
         assert np.array_equal(s.cpu().numpy(), so_), codec
+
+
+@pytest.mark.parametrize("codec", ["qsgd", "cnat"])
+def test_dtype_buckets_draw_disjoint_uniforms_and_injection_covers_one_dtype(codec):
+    """One seed for a mixed dict: the fp32 bucket draws from counter 0 and each other dtype from its own base
+    (identical (seed, counter) made rounding decisions correlated across dtypes); injected uniforms
+    for a dict with more than their own dtype are refused instead of silently replaced."""
+    params = {"w32": torch.randn(64, 64) * 1e-2, "w16": (torch.randn(64, 64) * 1e-2).half()}
+    ch = CHANNELS[codec](8)
+    bases = set(stoch_channel.COUNTER_BASE.values())
+    assert len(bases) == 4 and stoch_channel.COUNTER_BASE[torch.float32] == 0
+    u32 = stoch.philox_uniforms(4096, 77, 0, device=DEV)
+    u16 = stoch.philox_uniforms_dt(torch.float16, 4096, 77, stoch_channel.COUNTER_BASE[torch.float16], device=DEV)
+    assert not torch.equal(u32.double(), u16.double())
+    with pytest.raises(ValueError, match="cover one dtype"):
+        ch._quantize_params(params, 8, uniforms=torch.rand(4096, device=DEV))

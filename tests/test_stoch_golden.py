@@ -161,7 +161,7 @@ def test_philox_known_answer():
 def test_philox_7_rounds_is_a_prefix_of_the_known_answer_computation():
     """The codec's stream (PHILOX_ROUNDS = 7) is the first 7 rounds of the KAT-pinned Philox4x32-10: three
     more rounds, key schedule continued, give the 10-round known answers."""
-    assert so.PHILOX_ROUNDS == 7
+    assert so.PHILOX_ROUNDS == int(os.environ.get("ADFL_PHILOX_ROUNDS", "7"))
     for c, k in KAT10:
         key = k[0] | (k[1] << 32)
         lo, hi = np.array([c[0]], np.uint64), np.array([c[1]], np.uint64)
