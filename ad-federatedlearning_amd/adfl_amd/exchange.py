@@ -273,7 +273,9 @@ class PeerExchange:
         measured 0.096 ms eager and 0.041 ms replayed (tools/exchange_graph_probe.py). Collective over the
         group: every rank must capture (and later replay) in the same order. RCCL (device-direct) groups
         only; x and out stay bound to the graph. With a bucket layout, out's gaps between tensors are zeroed
-        here and never written again."""
+        here and never written again. Validated on hardware at world 1 only (tests/test_gpu_exchange.py:
+        replays equal eager and the oracle): a one-GPU box cannot form a two-rank RCCL group, and the
+        driver's 8-GPU runs use the eager exchange, so a capture across ranks has not yet been executed."""
         if self.device.type != "cuda" or self.host_staged:
             raise ValueError("PeerExchange.graph: needs device tensors over an RCCL group (host staging cannot "
                              "be captured)")
