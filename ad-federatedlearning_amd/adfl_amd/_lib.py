@@ -70,6 +70,9 @@ SIGNATURES = {
     # adfl_stoch.h
     "adfl_stoch_workspace_bytes": (I64, [I64]),
     "adfl_stoch_norms_batched": (INT, [P, P, I64, INT, P, I64, P, P, P]),
+    "adfl_stoch_torch_norm_scratch_bytes": (I64, [I64]),
+    "adfl_stoch_norms_torch": (INT, [P, P, I64, I32, P, I64, P, P]),
+    "adfl_stoch_torch_norm_walk_max": (I64, []),
     "adfl_qsgd_quantize_batched": (INT, [P, P, I64, INT, P, P, U64, U64, P, P, P]),
     "adfl_qsgd_encode_batched": (INT, [P, P, I64, INT, P, U64, U64, P, I64, P, P, P, P]),
     "adfl_rqsgd_encode_batched": (INT, [P, P, I64, INT, P, U64, U64, P, I64, P, P, P, P, P]),
@@ -112,10 +115,11 @@ def load() -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        raise ImportError(f"adfl_amd: HIP codec library not found at {LIB_PATH}; "
+    path = os.environ.get("ADFL_LIB_VARIANT") or LIB_PATH  # A/B builds of the same sources (tools/)
+    if not os.path.exists(path):
+        raise ImportError(f"adfl_amd: HIP codec library not found at {path}; "
                           "build it with `python -c 'import __graft_entry__ as g; g.build()'`")
-    lib = ctypes.CDLL(LIB_PATH)
+    lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype, fn.argtypes = res, args

@@ -28,7 +28,7 @@ from .ops import BucketLayout, _dev, _stream
 
 __all__ = ["RngStream", "norms_batched", "qsgd_quantize_batched", "qsgd_encode_batched", "rqsgd_encode_batched",
            "qsgd_decode_batched", "rqsgd_decode_batched", "cnat_encode_batched", "cnat_decode_batched",
-           "philox_uniforms", "workspace", "NORM_L2", "NORM_LINF", "NORM_L2_TORCH", "DT_DTYPES", "encode_batched_dt",
+           "philox_uniforms", "workspace", "torch_norms", "NORM_L2", "NORM_LINF", "NORM_L2_TORCH", "DT_DTYPES", "encode_batched_dt",
            "quantize_batched_dt", "norms_batched_dt", "philox_uniforms_dt", "dequantize_mean_batched"]
 
 
@@ -105,6 +105,40 @@ def norms_batched(flat: torch.Tensor, layout: BucketLayout, mode: int = NORM_L2,
     return norms, mins
 
 
+_TORCH_NORM_SCRATCH = {}  # (device index, stream handle) -> zeroed-once scratch of adfl_stoch_norms_torch
+
+
+def _torch_norm_scratch(layout: BucketLayout, dev) -> torch.Tensor:
+    """The look-back scratch for this device and stream: zeroed when allocated, then reused as is (each launch
+    leaves it ready for the next); grown, zeroed again, when a larger layout needs more."""
+    need = _lib.load().adfl_stoch_torch_norm_scratch_bytes(max(layout.nchunks, 1))
+    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
+    buf = _TORCH_NORM_SCRATCH.get(key)
+    if buf is None or buf.numel() < need:
+        buf = torch.zeros(need, dtype=torch.uint8, device=dev)
+        _TORCH_NORM_SCRATCH[key] = buf
+    return buf
+
+
+def torch_norms(flat: torch.Tensor, layout: BucketLayout, *, norms: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Per-tensor ||x||_2 bit-identical to torch's CPU vector_norm (the reference's QSGD / CNAT norm,
+    quant.py:226,512) at streaming rate: adfl_stoch_norms_torch, one pass with a look-back across each
+    tensor's tiles (csrc/torch_norm_lb.h). Same bits as norms_batched(..., NORM_L2_TORCH), the sequential
+    one-wave-per-tensor kernel."""
+    flat = _check_flat(flat, layout)
+    dev = flat.device
+    norms = torch.empty(layout.ntensors, dtype=torch.float32, device=dev) if norms is None else norms
+    if layout.nchunks == 0:
+        return norms
+    scratch = _torch_norm_scratch(layout, dev)
+    L = _lib.load()
+    walk_max = L.adfl_stoch_torch_norm_walk_max()
+    kinds = (1 if min(layout.sizes) <= walk_max else 0) | (2 if max(layout.sizes) > walk_max else 0)
+    check(L.adfl_stoch_norms_torch(flat.data_ptr(), layout.device_chunks(dev).data_ptr(), layout.nchunks, kinds,
+                                   scratch.data_ptr(), scratch.numel(), _dev(norms, "norms").data_ptr(), _stream(dev)))
+    return norms
+
+
 def _planes(layout, dev, levels, signs, ldtype):
     levels = torch.empty(layout.total, dtype=ldtype, device=dev) if levels is None else levels
     signs = torch.empty(layout.total, dtype=torch.int8, device=dev) if signs is None else signs
@@ -141,7 +175,7 @@ def qsgd_encode_batched(flat: torch.Tensor, layout: BucketLayout, bits: int, *,
     norms = torch.empty(layout.ntensors, dtype=torch.float32, device=dev) if norms is None else norms
     ws = _ws(ws, layout, dev)
     if torch_norm:
-        norms_batched(flat, layout, NORM_L2_TORCH, norms=norms, ws=ws)
+        torch_norms(flat, layout, norms=norms)
         qsgd_quantize_batched(flat, layout, bits, norms, uniforms=uniforms, seed=seed, counter=counter,
                               levels=levels, signs=signs)
         return levels, signs, norms
@@ -215,7 +249,7 @@ def cnat_encode_batched(flat: torch.Tensor, layout: BucketLayout, bits: int, *,
                                                     ws.numel(), exps.data_ptr(), signs.data_ptr(), norms.data_ptr(),
                                                     _stream(dev)))
     if torch_norm:
-        norms_batched(flat, layout, NORM_L2_TORCH, norms=norms, ws=ws)
+        torch_norms(flat, layout, norms=norms)
     return exps, signs, norms
 
 

@@ -33,6 +33,7 @@
 #include "adfl_stoch.h"
 #include "cnat_log2_table.h"
 #include "philox.h"
+#include "torch_norm_lb.h"
 #include "torch_sum_order.h"
 
 namespace {
@@ -527,66 +528,9 @@ __global__ __launch_bounds__(kBigBlock) void k_norm_finalize(const adfl_slq_chun
 // QSGD / CNAT norm, quant.py:226,512; restated and pinned to every golden norm in oracle/slq_oracle.c
 // oracle_torch_l2_norm): 8 fp32 lane accumulators acc[j] = fma(x[8i+j], x[8i+j], acc[j]) over i in order,
 // a left-to-right sum of the 8 lanes, then the n % 8 tail with fma; below 8 elements plain b + x*x.
-// The chains are inherently sequential (n / 8 dependent FMAs per lane), so one wave serves one tensor:
-// all 64 lanes load 64 consecutive elements (8 rows, coalesced), lanes 0..7 take their column's 8 values
-// in row order through cross-lane shuffles. Opt-in (ADFL_NORM_L2_TORCH): it is latency-bound, about one
-// element per cycle per tensor, against the fp64 default's full HBM rate.
-constexpr int kTorchNormGroups = 4;  // 64-element groups loaded ahead of the FMA chain
-
-__global__ __launch_bounds__(64) void k_norm_torch_order(const float* __restrict__ x,
-                                                         const adfl_slq_chunk* __restrict__ chunks,
-                                                         float* __restrict__ norms) {
-  const adfl_slq_chunk c = chunks[blockIdx.x];
-  if ((int64_t)blockIdx.x != c.first_chunk) return;  // one wave per tensor
-  const int lane = threadIdx.x;
-  const int64_t n = (int64_t)(c.nchunks - 1) * ADFL_SLQ_CHUNK_ELEMS + chunks[blockIdx.x + c.nchunks - 1].len;
-  const float* xt = x + c.start;
-  float b = 0.0f;
-  if (n < 8) {
-    if (lane == 0)
-      for (int i = 0; i < (int)n; ++i) {
-        const float sq = xt[i] * xt[i];
-        b = b + sq;
-      }
-  } else {
-    const int64_t nv = n - n % 8;
-    const int64_t ngroups = nv / 64;
-    const int col = lane & 7;
-    float acc = 0.0f;
-    for (int64_t g = 0; g < ngroups; g += kTorchNormGroups) {
-      float v[kTorchNormGroups];
-#pragma unroll
-      for (int u = 0; u < kTorchNormGroups; ++u) v[u] = (g + u < ngroups) ? xt[(g + u) * 64 + lane] : 0.0f;
-#pragma unroll
-      for (int u = 0; u < kTorchNormGroups; ++u) {
-        if (g + u >= ngroups) break;  // wave-uniform
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          const float e = __shfl(v[u], col + 8 * r, 64);
-          acc = __builtin_fmaf(e, e, acc);
-        }
-      }
-    }
-    const int rem_rows = (int)((nv % 64) / 8);
-    if (rem_rows > 0) {
-      const float v = lane < rem_rows * 8 ? xt[ngroups * 64 + lane] : 0.0f;
-      for (int r = 0; r < rem_rows; ++r) {
-        const float e = __shfl(v, col + 8 * r, 64);
-        acc = __builtin_fmaf(e, e, acc);
-      }
-    }
-    float lanes[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) lanes[j] = __shfl(acc, j, 64);
-    b = lanes[0];
-#pragma unroll
-    for (int j = 1; j < 8; ++j) b = b + lanes[j];
-    if (lane == 0)
-      for (int64_t i = nv; i < n; ++i) b = __builtin_fmaf(xt[i], xt[i], b);
-  }
-  if (lane == 0) norms[c.tensor] = (float)__builtin_sqrt((double)b);  // correctly rounded fp32 sqrt
-}
-
+// The chains are sequential (n / 8 dependent FMAs per lane): here one wave serves one tensor
+// (adfl_tn::walk_tensor: a 32-row register ring keeps the loads ahead of the FMA chain). The tile-parallel
+// look-back kernel (adfl_stoch_norms_torch, torch_norm_lb.h) gives the same bits at streaming rate.
 __device__ __forceinline__ void fill_zero_norm(uint8_t* __restrict__ lv, int8_t* __restrict__ sg, int len,
                                                int t = threadIdx.x) {
   for (int i = t; i < len; i += kBlock) {
@@ -1296,7 +1240,7 @@ int adfl_stoch_norms_batched(const float* d_x, const adfl_slq_chunk* d_chunks, i
   if (!aligned16(d_x)) return ADFL_E_ALIGN;
   hipStream_t st = (hipStream_t)stream;
   if (mode == ADFL_NORM_L2_TORCH) {  // no workspace: one wave per tensor
-    hipLaunchKernelGGL(k_norm_torch_order, dim3((unsigned)nchunks), dim3(64), 0, st, d_x, d_chunks, d_norms);
+    hipLaunchKernelGGL(adfl_tn::k_norm_walk, dim3((unsigned)nchunks), dim3(64), 0, st, d_x, d_chunks, INT64_MAX, d_norms);
     return launch_status();
   }
   if (int s = check_ws(d_workspace, workspace_bytes, nchunks)) return s;
@@ -1311,6 +1255,36 @@ int adfl_stoch_norms_batched(const float* d_x, const adfl_slq_chunk* d_chunks, i
   if (int s = launch_status()) return s;
   return launch_finalize<ADFL_NORM_LINF>(d_chunks, nchunks, d_workspace, d_norms, d_mins, st);
 }
+
+int64_t adfl_stoch_torch_norm_scratch_bytes(int64_t nchunks) {
+  return nchunks < 1 ? (int64_t)ADFL_E_ARG : adfl_tn::scratch_bytes(nchunks);
+}
+
+int adfl_stoch_norms_torch(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, int32_t kinds,
+                           void* d_scratch, int64_t scratch_bytes, float* d_norms, void* stream) {
+  if (!d_x || !d_norms || !d_scratch || bad_table(d_chunks, nchunks)) return ADFL_E_ARG;
+  const int64_t ntiles = nchunks * adfl_tn::kTilesPerChunk;
+  if (ntiles > 0x7fffffff) return ADFL_E_ARG;
+  if (scratch_bytes < adfl_tn::scratch_bytes(nchunks)) return ADFL_E_WORKSPACE;
+  if (reinterpret_cast<uintptr_t>(d_scratch) % 64) return ADFL_E_ALIGN;
+  if (kinds == 0) kinds = ADFL_TORCH_NORM_SHORT | ADFL_TORCH_NORM_LONG;
+  hipStream_t st = (hipStream_t)stream;
+  if (kinds & ADFL_TORCH_NORM_SHORT) {
+    hipLaunchKernelGGL(adfl_tn::k_norm_walk, dim3((unsigned)nchunks), dim3(64), 0, st, d_x, d_chunks,
+                       adfl_tn::kWalkMax, d_norms);
+    if (int s = launch_status()) return s;
+  }
+  if (kinds & ADFL_TORCH_NORM_LONG) {
+    auto* hdr = static_cast<adfl_tn::Header*>(d_scratch);
+    auto* recs = reinterpret_cast<adfl_tn::Rec*>(static_cast<char*>(d_scratch) + sizeof(adfl_tn::Header));
+    hipLaunchKernelGGL(adfl_tn::k_norm_torch, dim3((unsigned)ntiles), dim3(adfl_tn::kThreads), 0, st, d_x, d_chunks,
+                       ntiles, hdr, recs, d_norms);
+    return launch_status();
+  }
+  return ADFL_OK;
+}
+
+int64_t adfl_stoch_torch_norm_walk_max(void) { return adfl_tn::kWalkMax; }
 
 int adfl_qsgd_quantize_batched(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, int bits,
                                const float* d_norms, const float* d_uniforms, uint64_t seed, uint64_t counter,

@@ -55,6 +55,21 @@ int adfl_stoch_norms_batched(const float* d_x, const adfl_slq_chunk* d_chunks, i
                              void* d_workspace, int64_t workspace_bytes, float* d_norms, float* d_mins,
                              void* stream);
 
+/* ADFL_NORM_L2_TORCH's norms (the same bits: torch 2.10's CPU vector_norm, quant.py:226,512) at streaming
+ * rate: one pass over x in 4096-element tiles with a decoupled look-back across each tensor's tiles (the
+ * reduction is exact integer arithmetic while an accumulator stays in one binade; csrc/torch_norm_lb.h).
+ * d_scratch: adfl_stoch_torch_norm_scratch_bytes(nchunks) bytes of device memory, 64-byte aligned, ZEROED
+ * ONCE when allocated and then reused as is (each launch leaves it ready for the next); launches that may
+ * run concurrently need scratches of their own (one per stream). One launch. */
+int64_t adfl_stoch_torch_norm_scratch_bytes(int64_t nchunks);
+/* kinds: which tensors the bucket holds, so a launch with nothing to do is skipped — ADFL_TORCH_NORM_SHORT
+ * (some of at most adfl_stoch_torch_norm_walk_max() elements: one wave walks each, the reference loop with
+ * its loads kept ahead of the FMA chain) | ADFL_TORCH_NORM_LONG (some longer: the tile look-back); 0 = both. */
+enum { ADFL_TORCH_NORM_SHORT = 1, ADFL_TORCH_NORM_LONG = 2 };
+int64_t adfl_stoch_torch_norm_walk_max(void);
+int adfl_stoch_norms_torch(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, int32_t kinds,
+                           void* d_scratch, int64_t scratch_bytes, float* d_norms, void* stream);
+
 /* QSGD / RQSGD level quantization given per-tensor norms (quant.py:230-238 and :371-379), levels =
  * 2^bits - 1: scaled = fl(fl(levels*|x|) / norm); l = floor(scaled); q = u8(l + (u < scaled - l));
  * norm == 0 gives levels 0 and signs 1 (quant.py:227-228). One launch. */
