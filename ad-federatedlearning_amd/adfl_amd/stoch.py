@@ -120,18 +120,6 @@ def _torch_norm_scratch(layout: BucketLayout, dev) -> torch.Tensor:
     return buf
 
 
-_ARRIVAL_COUNTERS = {}  # (device index, stream handle) -> zeroed-once int32 counters of adfl_cnat_encode_arrival
-
-
-def _arrival_counters(layout: BucketLayout, dev) -> torch.Tensor:
-    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
-    buf = _ARRIVAL_COUNTERS.get(key)
-    if buf is None or buf.numel() < layout.ntensors:
-        buf = torch.zeros(max(layout.ntensors, 256), dtype=torch.int32, device=dev)
-        _ARRIVAL_COUNTERS[key] = buf
-    return buf
-
-
 def torch_norms(flat: torch.Tensor, layout: BucketLayout, *, norms: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Per-tensor ||x||_2 bit-identical to torch's CPU vector_norm (the reference's QSGD / CNAT norm,
     quant.py:226,512) at streaming rate: adfl_stoch_norms_torch, one pass with a look-back across each
@@ -246,7 +234,7 @@ def cnat_encode_batched(flat: torch.Tensor, layout: BucketLayout, bits: int, *,
                         uniforms: Optional[torch.Tensor] = None, seed: int = 0, counter: int = 0,
                         exps: Optional[torch.Tensor] = None, signs: Optional[torch.Tensor] = None,
                         norms: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None,
-                        torch_norm: bool = False, resident: Optional[bool] = None, arrival: Optional[bool] = None):
+                        torch_norm: bool = False, resident: Optional[bool] = None):
     """CNAT encode (x read once; resident as for QSGD): (exponents i8, signs i8, L2 norms f32). A tensor
     whose norm is 0 gets the reference's zero-branch bytes (0 / 1). torch_norm=True then replaces the norms
     with torch's own (the exponents do not depend on the norm; both norms are 0 for exactly the same tensors)."""
@@ -255,17 +243,6 @@ def cnat_encode_batched(flat: torch.Tensor, layout: BucketLayout, bits: int, *,
     exps, signs = _planes(layout, dev, exps, signs, torch.int8)
     norms = torch.empty(layout.ntensors, dtype=torch.float32, device=dev) if norms is None else norms
     ws = _ws(ws, layout, dev)
-    if arrival is None:
-        arrival = os.environ.get("ADFL_CNAT_ARRIVAL", "0") == "1"
-    L = _lib.load()
-    if arrival and layout.max_tensor_chunks <= L.adfl_cnat_arrival_max_chunks():
-        check(L.adfl_cnat_encode_arrival(flat.data_ptr(), layout.device_chunks(dev).data_ptr(), layout.nchunks, bits,
-                                         _uniforms(uniforms, layout), seed, counter, ws.data_ptr(), ws.numel(),
-                                         _arrival_counters(layout, dev).data_ptr(), exps.data_ptr(), signs.data_ptr(),
-                                         norms.data_ptr(), _stream(dev)))
-        if torch_norm:
-            torch_norms(flat, layout, norms=norms)
-        return exps, signs, norms
     check(_lib.load().adfl_cnat_encode_batched_work(flat.data_ptr(), layout.device_chunks(dev).data_ptr(),
                                                     layout.nchunks, *_work(layout, dev, resident), bits,
                                                     _uniforms(uniforms, layout), seed, counter, ws.data_ptr(),

@@ -671,82 +671,6 @@ __global__ __launch_bounds__(kBlock) void k_cnat_quantize(const float* __restric
   acc.flush(partials, blockIdx.x);
 }
 
-// CNAT in ONE launch with one block per chunk: k_cnat_quantize's work and partial, the
-// partial handed to the tensor's last block by an arrival counter — the last block (told by the value its
-// agent-scope add returned) sums the partials in chunk order exactly as finalize_small does, writes the norm
-// and, for an all-zero tensor, rewrites every chunk's bytes. Hand-off (cdna_hip_programming.md Guideline 16,
-// table row 1): the partial is an sc1 store drained before the add; a block whose own partial is 0 — the
-// only case its bytes can be rewritten by another block — also writes back its L2 (agent release) first,
-// so the rewrite lands after them. Counters: one int per tensor, zeroed once; the last block resets its
-// tensor's. Only for buckets whose tensors have at most kSmallChunks chunks (the sum is one thread's).
-typedef __attribute__((address_space(1))) unsigned long long gu64_t;
-typedef __attribute__((address_space(1))) int gi32_t;
-
-template <int PB>
-__global__ __launch_bounds__(kBlock) void k_cnat_encode_arrival(const float* __restrict__ x,
-                                                                const adfl_slq_chunk* __restrict__ chunks, int min_e,
-                                                                int max_e, Uniforms U, int8_t* __restrict__ exps,
-                                                                int8_t* __restrict__ signs, double* partials,
-                                                                int* counters, float* __restrict__ norms) {
-  __shared__ int s_last;
-  __shared__ float s_norm;
-  const adfl_slq_chunk c = chunks[blockIdx.x];
-  const float* xc = x + c.start;
-  int8_t* ex = exps + c.start;
-  int8_t* sg = signs + c.start;
-  const int head = chunk_head4(c.start, c.len);
-  const int n4 = (c.len - head) >> 2;
-  const auto fast = [=](float xv, float uv, bool& bad) { return cnat_exp_fast(xv, uv, min_e, max_e, bad); };
-  const auto exact = [=](float xv, float uv) { return cnat_exp_exact(xv, uv, min_e, max_e); };
-  NormAcc<ADFL_NORM_L2> acc;
-  quantize_chunk_vec<PB>(reinterpret_cast<const float4*>(xc + head), n4, c.start + head, U,
-                         reinterpret_cast<uint32_t*>(ex + head), reinterpret_cast<uint32_t*>(sg + head), fast, exact,
-                         false, &acc);
-  const int i = edge_elem(head, head + (n4 << 2), c.len);
-  if (i >= 0) {
-    const float v = xc[i];
-    ex[i] = (int8_t)exact(v, U.one(c.start + i));
-    sg[i] = (int8_t)sign_byte(v);
-    acc.add(v);
-  }
-  const double part = block_sum(acc.s);  // k_cnat_quantize's partial, bit for bit (block-uniform)
-  if (part == 0.0) {  // this chunk's bytes may be rewritten: every storing wave drains, then one release
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  }
-  if (threadIdx.x == 0) {
-    __hip_atomic_store((gu64_t*)(partials + blockIdx.x), (unsigned long long)__double_as_longlong(part),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int old = __hip_atomic_fetch_add((gi32_t*)(counters + c.tensor), 1, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-    int last = old == c.nchunks - 1;
-    if (last) {
-      __hip_atomic_store((gi32_t*)(counters + c.tensor), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      double p[kSmallChunks];
-      const int lastk = c.nchunks - 1;
-#pragma unroll
-      for (int k = 0; k < kSmallChunks; ++k)
-        p[k] = __longlong_as_double((long long)__hip_atomic_load(
-            (gu64_t*)(partials + c.first_chunk + min(k, lastk)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      double t = 0.0;
-#pragma unroll
-      for (int k = 0; k < kSmallChunks; ++k) t += k <= lastk ? p[k] : 0.0;  // finalize_small's order
-      const float norm = (float)__builtin_sqrt((double)(float)t);
-      norms[c.tensor] = norm;
-      s_norm = norm;
-    }
-    s_last = last;
-  }
-  __syncthreads();
-  if (s_last && s_norm == 0.0f)  // quant.py:513-514: u8 zeros, int8 ones over the whole tensor
-    for (int k = 0; k < c.nchunks; ++k) {
-      const adfl_slq_chunk ck = chunks[c.first_chunk + k];
-      fill_zero_norm(reinterpret_cast<uint8_t*>(exps) + ck.start, signs + ck.start, ck.len);
-    }
-}
-
 // CNAT norm == 0 (an all-zero tensor): the reference returns u8 zeros and int8 ones (quant.py:513-514).
 // One THREAD per chunk checks its tensor's norm; a wave then fills its zero-norm chunks one at a time, all
 // 64 lanes on each. Nearly every launch only reads a norm per chunk and exits: one block per chunk made it
@@ -1441,24 +1365,6 @@ int adfl_cnat_encode_batched(const float* d_x, const adfl_slq_chunk* d_chunks, i
                      d_chunks, nchunks, (const float*)d_norms, d_exps, d_signs);
   return launch_status();
 }
-
-int adfl_cnat_encode_arrival(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, int bits,
-                             const float* d_uniforms, uint64_t seed, uint64_t counter, void* d_workspace,
-                             int64_t workspace_bytes, int32_t* d_counters, int8_t* d_exps, int8_t* d_signs,
-                             float* d_norms, void* stream) {
-  if (!d_x || !d_exps || !d_signs || !d_norms || !d_counters || bad_table(d_chunks, nchunks)) return ADFL_E_ARG;
-  if (int s = check_bits(bits)) return s;
-  if (int s = check_ws(d_workspace, workspace_bytes, nchunks)) return s;
-  if (!aligned16(d_x) || !aligned16(d_exps) || !aligned16(d_signs) || (d_uniforms && !aligned16(d_uniforms)))
-    return ADFL_E_ALIGN;
-  const Uniforms U{d_uniforms, seed, counter};
-  const int min_e = -(1 << (bits - 1)), max_e = (1 << (bits - 1)) - 1;  // quant.py:519-520
-  hipLaunchKernelGGL(k_cnat_encode_arrival<kPbQuantize>, dim3((unsigned)nchunks), dim3(kBlock), 0, (hipStream_t)stream,
-                     d_x, d_chunks, min_e, max_e, U, d_exps, d_signs, (double*)d_workspace, d_counters, d_norms);
-  return launch_status();
-}
-
-int64_t adfl_cnat_arrival_max_chunks(void) { return kSmallChunks; }
 
 int adfl_cnat_dequantize_batched(const int8_t* d_exps, const int8_t* d_signs, const adfl_slq_chunk* d_chunks,
                                  int64_t nchunks, const float* d_norms, float* d_out, void* stream) {

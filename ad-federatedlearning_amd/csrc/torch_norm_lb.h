@@ -17,11 +17,14 @@
 // too, the increments being >= 0 and R(v) >= v - 1/2). tools/torch_norm_proto.c checks this model against
 // the sequential chain on random, tie-heavy, subnormal, overflow and NaN / inf data.
 //
-// The kernel. The 8 chains of a tensor run over tiles of 4096 elements (512 steps of each chain; two
-// tiles per 8192-element chunk, so tile id = 2 * chunk + half). One 256-thread block per tile, tiles taken
-// in ticket order; lane l of wave w reads elements w*1024 + 64*i + l (i < 16): always chain l & 7, 256 B
-// contiguous per wave-instruction, no alignment requirement. Each tile publishes, in its record, three
-// states (decoupled look-back):
+// Short tensors (<= kWalkMax elements): k_norm_walk, one wave per tensor running the chains in order, the
+// rows written to LDS chain-major so each chain reads 4 steps per ds_read_b128 ahead of its FMA chain.
+//
+// Long tensors: k_norm_torch. The 8 chains run over tiles of kTile = 16384 elements (2048 steps of each
+// chain; two chunks — one ticket per chunk, the tile's first chunk's block does the work), taken in ticket
+// order; lane l of wave w reads elements w * 64 * kRegs + 64 * i + l (i < kRegs): always chain l & 7,
+// 256 B contiguous per wave-instruction, no alignment requirement. Each tile publishes, in its record,
+// three kinds of values (decoupled look-back):
 //   1  fp64 sums of x^2 per chain (aggS);
 //   2  the fp64 inclusive prefix, and for each chain the integer totals of its steps under one or two
 //      candidate grids — the binade(s) the fp32 accumulator can be in at the tile's start, predicted from
@@ -29,13 +32,13 @@
 //      of randn, so the candidates span [S(1 - 1/8), S(1 + 2^-16)]); a tile with a tie, a step at or
 //      above 2^24 ulps, or a non-finite value has no valid total;
 //   3  the chain's exact fp32 accumulator after the tile.
-// A tile's exclusive state = the nearest predecessor in state 3 plus the totals of the state-2 tiles in
-// between, when their candidates include that state's grid and the sum stays below 2^24. If not (a
-// crossing into the next binade, a tie, a miss of the predictor) the tile waits for its predecessor's
-// state 3. Its own inclusive state is its exclusive state plus its total under the same rule; otherwise
-// lanes 0..7 run the tile's 512 steps sequentially with fmaf from LDS — the reference arithmetic
-// itself. Crossings are rare (about log2 of the chain length per chain, mostly in the first tiles), so
-// the kernel streams x once at HBM rate plus a few serial links.
+// A tile's exclusive state = the nearest predecessor with 3 published plus the totals of the tiles in
+// between for that accumulator's grid, when all of them hold one and the sum stays below 2^24. If not (a
+// crossing into the next binade, a tie, a miss of the predictor) the tile waits for the first tile from the
+// base's side that breaks it to publish 3, and looks again. Its own inclusive state is its exclusive state
+// plus its total under the same rule; otherwise lanes 0..7 run the tile's steps with fmaf from LDS — the
+// reference arithmetic itself. Tile size and round size were measured (profiles/r04/torch_norm/: C2
+// 4.5 ms at 4096-element tiles, 2.4 at 8192, 2.1 at 16384 with 512 threads, 3.2 at 32768).
 //
 // Hand-off between blocks: every published value is an 8-byte granule {tag, 32-bit value} written and read
 // with relaxed agent-scope atomics (global sc1 stores / loads: write-through, L1 bypassed), so the data is
@@ -59,14 +62,23 @@
 
 namespace adfl_tn {
 
-constexpr int kThreads = 256;
+#ifndef ADFL_TN_THREADS
+#define ADFL_TN_THREADS 512
+#endif
+constexpr int kThreads = ADFL_TN_THREADS;
 constexpr int kWaves = kThreads / 64;
-constexpr int kRegs = 16;                                       // dwords per lane
-constexpr int kTile = kThreads * kRegs;                         // 4096 elements, 512 steps per chain
-constexpr int kTilesPerChunk = ADFL_SLQ_CHUNK_ELEMS / kTile;    // 2
+#ifndef ADFL_TN_REGS
+#define ADFL_TN_REGS 32
+#endif
+constexpr int kRegs = ADFL_TN_REGS;                             // dwords per lane
+constexpr int kTile = kThreads * kRegs;                         // 16384 elements: 2048 steps per chain
+// a tile is part of a chunk (kTilesPerChunk tiles per chunk, one ticket each) or whole chunks (kChunksPerTile;
+// one ticket per chunk, the tile's first chunk does the work, the others exit)
+constexpr int kTilesPerChunk = kTile <= ADFL_SLQ_CHUNK_ELEMS ? ADFL_SLQ_CHUNK_ELEMS / kTile : 1;
+constexpr int kChunksPerTile = kTile >= ADFL_SLQ_CHUNK_ELEMS ? kTile / ADFL_SLQ_CHUNK_ELEMS : 1;
 constexpr int kWin = 8;                                         // predecessors per look-back round (x 8 chains)
 #ifndef ADFL_TN_BATCH
-#define ADFL_TN_BATCH 8
+#define ADFL_TN_BATCH 1
 #endif
 constexpr int kBatch = ADFL_TN_BATCH;                           // windows per look-back round (one round trip)
 constexpr int kMaxD = 64;                                       // predecessors whose candidates are kept
@@ -78,7 +90,7 @@ constexpr uint32_t kCodeNaN = 254, kCodeBad = 255;              // candidate cod
 constexpr long long kSpinCap = 1ll << 20;                       // polls (about 1 us each): a second
 constexpr unsigned long long kChain0 = 0x0101010101010101ull;  // ballot bits of the chain-0 lanes
 
-static_assert(kTilesPerChunk * kTile == ADFL_SLQ_CHUNK_ELEMS, "tiles split chunks evenly");
+static_assert(kTilesPerChunk * kTile == ADFL_SLQ_CHUNK_ELEMS * kChunksPerTile, "tiles and chunks nest");
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 
@@ -301,7 +313,8 @@ __global__ __launch_bounds__(kThreads) void k_norm_torch(const float* __restrict
     const int64_t nv = n >= 8 ? n - n % 8 : 0;
     const int64_t e0 = (int64_t)kc * ADFL_SLQ_CHUNK_ELEMS + (int64_t)h * kTile;
     const int len = (int)(nv - e0 <= 0 ? 0 : (nv - e0 < kTile ? nv - e0 : kTile));
-    const int ti = kc * kTilesPerChunk + h;  // tile index within the tensor
+    const int ti = kChunksPerTile > 1 ? kc / kChunksPerTile : kc * kTilesPerChunk + h;  // tile index in the tensor
+    if (kChunksPerTile > 1 && kc % kChunksPerTile != 0) goto finish;  // not a tile's first chunk
     if (n <= kWalkMax) goto finish;  // block-uniform: short tensors are k_norm_walk's
     {
     Rec* me = recs + t;
@@ -329,7 +342,9 @@ __global__ __launch_bounds__(kThreads) void k_norm_torch(const float* __restrict
     if (q == 0) s_part[wave][c][0] = S;
     __syncthreads();
     if (tid < 8) {
-      const double a = ((s_part[0][tid][0] + s_part[1][tid][0]) + s_part[2][tid][0]) + s_part[3][tid][0];
+      double a = s_part[0][tid][0];
+#pragma unroll
+      for (int w = 1; w < kWaves; ++w) a += s_part[w][tid][0];
       s_aggS[tid] = a;
       put(&me->aggS[tid], tag, __float_as_uint((float)a));
     }
@@ -346,8 +361,8 @@ __global__ __launch_bounds__(kThreads) void k_norm_torch(const float* __restrict
 #pragma unroll
           for (int j = 0; j < kBatch; ++j) {  // unconditional loads (clamped to the tensor's first tile)
             const int d = min((r * kBatch + j) * kWin + q, ti - 1);
-            gi[j] = get(&recs[t - 1 - d].inclS[c]);
-            ga[j] = get(&recs[t - 1 - d].aggS[c]);
+            gi[j] = get(&(me - kChunksPerTile * (1 + d))->inclS[c]);
+            ga[j] = get(&(me - kChunksPerTile * (1 + d))->aggS[c]);
           }
           bool ok = true, fnd = done;
 #pragma unroll
@@ -411,8 +426,13 @@ __global__ __launch_bounds__(kThreads) void k_norm_torch(const float* __restrict
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
         const int g = s_g[tid][k];
-        const double T = ((s_part[0][tid][1 + k] + s_part[1][tid][1 + k]) + s_part[2][tid][1 + k]) + s_part[3][tid][1 + k];
-        const bool tie = s_tie[0][tid][k] | s_tie[1][tid][k] | s_tie[2][tid][k] | s_tie[3][tid][k];
+        double T = s_part[0][tid][1 + k];
+        bool tie = s_tie[0][tid][k];
+#pragma unroll
+        for (int w = 1; w < kWaves; ++w) {
+          T += s_part[w][tid][1 + k];
+          tie |= s_tie[w][tid][k];
+        }
         const bool ok = g != kNoGrid && !tie && T < kTop;  // NaN fails too
         s_T[tid][k] = T;
         s_ok[tid][k] = ok;
@@ -444,9 +464,10 @@ __global__ __launch_bounds__(kThreads) void k_norm_torch(const float* __restrict
 #pragma unroll
               for (int j = 0; j < kBatch; ++j) {
                 const int d = min((r * kBatch + j) * kWin + q, ti - 1);
-                g3[j] = get(&recs[t - 1 - d].incl[c]);
-                c0[j] = get(&recs[t - 1 - d].cand[0][c]);
-                c1[j] = get(&recs[t - 1 - d].cand[1][c]);
+                const Rec* p = me - kChunksPerTile * (1 + d);
+                g3[j] = get(&p->incl[c]);
+                c0[j] = get(&p->cand[0][c]);
+                c1[j] = get(&p->cand[1][c]);
               }
               bool ok2 = true, fnd = found;
 #pragma unroll
@@ -549,7 +570,7 @@ __global__ __launch_bounds__(kThreads) void k_norm_torch(const float* __restrict
           }
           if (__all(ok) || s_err) break;
           if (!ok) {  // wait until that tile has published its accumulator
-            const Rec* p = recs + (t - 1 - dwait);
+            const Rec* p = me - kChunksPerTile * (1 + dwait);
             for (long long ns = 0; !has(get(&p->incl[c]), tag) && spin(ns, &s_err);) {
             }
           }
@@ -585,7 +606,7 @@ __global__ __launch_bounds__(kThreads) void k_norm_torch(const float* __restrict
     if (s_slow) {  // block-uniform: the chains in order, the reference arithmetic itself
       // staged chain-major (s_stage[c][step]); steps past len are zeros, which change nothing
 #pragma unroll
-      for (int i = 0; i < kRegs; ++i) s_stage[c * kStageStride + 128 * wave + 8 * i + q] = e[i];
+      for (int i = 0; i < kRegs; ++i) s_stage[c * kStageStride + 8 * kRegs * wave + 8 * i + q] = e[i];
       __syncthreads();
       if (tid < 8 && ((s_slow >> tid) & 1)) {
         float acc = s_excl[tid];
@@ -622,7 +643,7 @@ __global__ __launch_bounds__(kThreads) void k_norm_torch(const float* __restrict
     }
     if (tid < 8) put(&me->incl[tid], tag, __float_as_uint(s_inc[tid]));
     if (tid == 0) {
-      if (ti == ch.nchunks * kTilesPerChunk - 1) {  // the tensor's last tile: lane sum, tail, sqrt
+      if (ti == (ch.nchunks * kTilesPerChunk + kChunksPerTile - 1) / kChunksPerTile - 1) {  // last tile: lane sum, tail, sqrt
         const float* xs = x + tbase;
         float b = 0.0f;
         if (n < 8) {

@@ -107,17 +107,6 @@ int adfl_cnat_encode_batched(const float* d_x, const adfl_slq_chunk* d_chunks, i
                              int64_t workspace_bytes, int8_t* d_exps, int8_t* d_signs, float* d_norms,
                              void* stream);
 
-/* adfl_cnat_encode_batched's output in ONE launch, one block per chunk: the last block of each tensor (an
- * arrival counter) sums the tensor's chunk partials and does the norm == 0 rewrite. Every tensor must have at
- * most adfl_cnat_arrival_max_chunks() chunks (the caller checks; a longer one gets a wrong norm).
- * d_counters: one int32 per tensor, ZEROED ONCE when allocated (each launch leaves them zero); one set per
- * stream. */
-int adfl_cnat_encode_arrival(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, int bits,
-                             const float* d_uniforms, uint64_t seed, uint64_t counter, void* d_workspace,
-                             int64_t workspace_bytes, int32_t* d_counters, int8_t* d_exps, int8_t* d_signs,
-                             float* d_norms, void* stream);
-int64_t adfl_cnat_arrival_max_chunks(void);
-
 /* CNATChannel._dequantize_tensor (quant.py:537-545): out = fl(fl(norm*sign) * 2^e); 0 if norm == 0. */
 int adfl_cnat_dequantize_batched(const int8_t* d_exps, const int8_t* d_signs, const adfl_slq_chunk* d_chunks,
                                  int64_t nchunks, const float* d_norms, float* d_out, void* stream);

@@ -165,7 +165,7 @@ def test_torch_norms_abi_rejects_bad_arguments():
     x = torch.zeros(100, device=DEV)
     nrm = torch.empty(1, device=DEV)
     need = L.adfl_stoch_torch_norm_scratch_bytes(lay.nchunks)
-    assert need == 64 + 2 * 320
+    assert need >= 64 + 320 and (need - 64) % 320 == 0
     assert L.adfl_stoch_torch_norm_scratch_bytes(0) < 0
     buf = torch.zeros(need + 64, dtype=torch.uint8, device=DEV)
     ch = lay.device_chunks(DEV).data_ptr()

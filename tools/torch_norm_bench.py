@@ -57,7 +57,6 @@ def main():
         stoch.torch_norms(x, lay, norms=nrm)
         cnt = scr[24:64].cpu().view(torch.int64).tolist()
         out["lookback_error_retries_sequential_notfound_bad"] = cnt
-        out["tiles"] = 2 * lay.nchunks
         ref = stoch.norms_batched(x, lay, stoch.NORM_L2_TORCH)[0].clone()
         got = stoch.torch_norms(x, lay)
         out["lookback_equals_sequential"] = bool(torch.equal(ref.view(torch.int32), got.view(torch.int32)))
