@@ -528,9 +528,9 @@ __global__ __launch_bounds__(kBigBlock) void k_norm_finalize(const adfl_slq_chun
 // QSGD / CNAT norm, quant.py:226,512; restated and pinned to every golden norm in oracle/slq_oracle.c
 // oracle_torch_l2_norm): 8 fp32 lane accumulators acc[j] = fma(x[8i+j], x[8i+j], acc[j]) over i in order,
 // a left-to-right sum of the 8 lanes, then the n % 8 tail with fma; below 8 elements plain b + x*x.
-// The chains are sequential (n / 8 dependent FMAs per lane): here one wave serves one tensor
-// (adfl_tn::walk_tensor: a 32-row register ring keeps the loads ahead of the FMA chain). The tile-parallel
-// look-back kernel (adfl_stoch_norms_torch, torch_norm_lb.h) gives the same bits at streaming rate.
+// The chains are sequential (n / 8 dependent FMAs per lane): ADFL_NORM_L2_TORCH runs one block per tensor
+// (adfl_tn::k_norm_walk: four waves stream the tensor through LDS ahead of the FMA chain); the tile-parallel
+// look-back kernel (adfl_stoch_norms_torch, torch_norm_lb.h) gives the same bits for long tensors.
 __device__ __forceinline__ void fill_zero_norm(uint8_t* __restrict__ lv, int8_t* __restrict__ sg, int len,
                                                int t = threadIdx.x) {
   for (int i = t; i < len; i += kBlock) {
@@ -1240,7 +1240,8 @@ int adfl_stoch_norms_batched(const float* d_x, const adfl_slq_chunk* d_chunks, i
   if (!aligned16(d_x)) return ADFL_E_ALIGN;
   hipStream_t st = (hipStream_t)stream;
   if (mode == ADFL_NORM_L2_TORCH) {  // no workspace: one wave per tensor
-    hipLaunchKernelGGL(adfl_tn::k_norm_walk, dim3((unsigned)nchunks), dim3(64), 0, st, d_x, d_chunks, INT64_MAX, d_norms);
+    hipLaunchKernelGGL(adfl_tn::k_norm_walk, dim3((unsigned)nchunks), dim3(adfl_tn::kWalkThreads), 0, st, d_x, d_chunks,
+                       INT64_MAX, d_norms);
     return launch_status();
   }
   if (int s = check_ws(d_workspace, workspace_bytes, nchunks)) return s;
@@ -1270,8 +1271,8 @@ int adfl_stoch_norms_torch(const float* d_x, const adfl_slq_chunk* d_chunks, int
   if (kinds == 0) kinds = ADFL_TORCH_NORM_SHORT | ADFL_TORCH_NORM_LONG;
   hipStream_t st = (hipStream_t)stream;
   if (kinds & ADFL_TORCH_NORM_SHORT) {
-    hipLaunchKernelGGL(adfl_tn::k_norm_walk, dim3((unsigned)nchunks), dim3(64), 0, st, d_x, d_chunks,
-                       adfl_tn::kWalkMax, d_norms);
+    hipLaunchKernelGGL(adfl_tn::k_norm_walk, dim3((unsigned)nchunks), dim3(adfl_tn::kWalkThreads), 0, st, d_x,
+                       d_chunks, adfl_tn::kWalkMax, d_norms);
     if (int s = launch_status()) return s;
   }
   if (kinds & ADFL_TORCH_NORM_LONG) {

@@ -184,57 +184,70 @@ __device__ __forceinline__ double lane_total(const float (&e)[kRegs], int g, boo
   return T;
 }
 
-// One wave runs a whole tensor's 8 chains in order — the reference's loop itself — for tensors too short
-// for the tiles to pay. Rows of 64 elements (8 steps) stream through a 32-row register ring, are written
-// to LDS transposed (chain-major, lds[c][step]), and lane c < 8 reads its chain back 4 steps per
-// ds_read_b128: the dependent FMA chain (about 6.6 cycles per step, MI355X_MICROARCH.md) never waits on
-// a cross-lane shuffle, and the next 32 rows are in flight while a block of 256 steps is summed. lds:
-// kWalkLds floats of the caller's shared memory per wave. Returns b before the square root (torch's lane
-// sum and tail included; valid in every lane).
-constexpr int kRing = 32;                                 // rows (of 64 elements) per block
-constexpr int kWalkStride = kRing * 8 + 4;                // floats per chain row in LDS (+4: banks, 16 B)
-constexpr int kWalkLds = 8 * kWalkStride;
-constexpr int64_t kWalkMax = 1 << 16;                     // tensors up to this size are walked
+constexpr int64_t kWalkMax = 1 << 16;                     // tensors up to this size are walked (k_norm_walk)
 constexpr int kStageStride = kTile / 8 + 4;               // a slow tile staged chain-major (+4: banks, 16 B)
-static_assert(kWalkLds <= 8 * kStageStride, "the walker uses the tile staging buffer");
 
-__device__ __forceinline__ float walk_tensor(const float* __restrict__ xt, int64_t n, float* lds) {
-  const int lane = threadIdx.x & 63, c = lane & 7, q = lane >> 3;
-  float b = 0.0f;
+// One block per tensor of at most kWalkMax elements (the look-back kernel takes the longer ones) runs the
+// 8 chains in order — the reference's loop itself. Its four waves stream the tensor in 4096-element blocks
+// into an LDS double buffer, chain-major (buf[c][step]), so lane c < 8 of wave 0 reads its chain back 4
+// steps per ds_read_b128, eight reads ahead of the dependent FMAs (about 6.6 cycles per step,
+// MI355X_MICROARCH.md), while the next block's 16 KiB are in flight. A one-wave version with a 32-row
+// register ring (2 KiB in flight) took 56 us on C3; with cross-lane shuffles instead of the LDS
+// transpose 95 us, and with its loads under branches (an s_waitcnt vmcnt(0) after each) 312 us.
+constexpr int kWalkThreads = 256;
+constexpr int kWalkRegs = 16;
+constexpr int kWalkBlock = kWalkThreads * kWalkRegs;  // 4096 elements: 512 steps of each chain
+constexpr int kWalkBlockStride = kWalkBlock / 8 + 4;   // floats per chain row (+4: banks, 16-byte reads)
+
+__global__ __launch_bounds__(kWalkThreads) void k_norm_walk(const float* __restrict__ x,
+                                                           const adfl_slq_chunk* __restrict__ chunks,
+                                                           int64_t max_n, float* __restrict__ norms) {
+  __shared__ __attribute__((aligned(16))) float buf[2][8 * kWalkBlockStride];
+  const adfl_slq_chunk ch = chunks[blockIdx.x];
+  if ((int64_t)blockIdx.x != ch.first_chunk) return;
+  const int64_t n = (int64_t)(ch.nchunks - 1) * ADFL_SLQ_CHUNK_ELEMS + chunks[blockIdx.x + ch.nchunks - 1].len;
+  if (n > max_n) return;
+  const float* xt = x + ch.start;
+  const int tid = threadIdx.x, c = tid & 7, s0 = tid >> 3;
   if (n < 8) {
-    for (int64_t i = 0; i < n; ++i) {
-      const float sq = xt[i] * xt[i];
-      b = b + sq;
+    if (tid == 0) {
+      float b = 0.0f;
+      for (int64_t i = 0; i < n; ++i) {
+        const float sq = xt[i] * xt[i];
+        b = b + sq;
+      }
+      norms[ch.tensor] = (float)__builtin_sqrt((double)b);
     }
-    return b;
+    return;
   }
-  const int64_t nv = n - n % 8, rows = (nv + 63) / 64;  // the last row may be partial: zeros past nv
+  const int64_t nv = n - n % 8, nblocks = (nv + kWalkBlock - 1) / kWalkBlock;
+  // unconditional (clamped) loads keep a block's 16 of them in flight; elements past nv become zeros,
+  // which leave the accumulators unchanged (fmaf(0, 0, a) == a)
+  float r[kWalkRegs];
+  const auto load = [&](int64_t blk) {
+#pragma unroll
+    for (int i = 0; i < kWalkRegs; ++i) r[i] = xt[min(blk * kWalkBlock + i * kWalkThreads + tid, nv - 1)];
+  };
+  const auto stage = [&](int64_t blk, float* dst) {
+#pragma unroll
+    for (int i = 0; i < kWalkRegs; ++i)
+      dst[c * kWalkBlockStride + (kWalkThreads / 8) * i + s0] =
+          blk * kWalkBlock + i * kWalkThreads + tid < nv ? r[i] : 0.0f;
+  };
+  load(0);
+  stage(0, buf[0]);
+  __syncthreads();
   float acc = 0.0f;
-  // loads are unconditional (index clamped) so the compiler keeps the ring in flight (a load under a
-  // branch gets an s_waitcnt vmcnt(0) after it); elements past nv are replaced by zeros, which leave the
-  // accumulators unchanged (fmaf(0, 0, a) == a for every a)
-  const float* last = xt + (nv - 1);
-  float ring[kRing];
-#pragma unroll
-  for (int u = 0; u < kRing; ++u) {
-    const int64_t i = (int64_t)u * 64 + lane;
-    ring[u] = i < nv ? xt[i] : *last;
-  }
-  for (int64_t r0 = 0; r0 < rows; r0 += kRing) {
-#pragma unroll
-    for (int u = 0; u < kRing; ++u) {
-      const int64_t i = (r0 + u) * 64 + lane;
-      lds[c * kWalkStride + 8 * u + q] = i < nv ? ring[u] : 0.0f;
-      const int64_t in = i + (int64_t)kRing * 64;
-      ring[u] = in < nv ? xt[in] : *last;
-    }
-    if (lane < 8) {  // 8 float4 reads in flight ahead of the 32 FMAs they feed (double-buffered)
-      const float4* l4 = reinterpret_cast<const float4*>(lds + c * kWalkStride);
+  for (int64_t blk = 0; blk < nblocks; ++blk) {
+    const bool more = blk + 1 < nblocks;  // block-uniform
+    if (more) load(blk + 1);
+    if (tid < 8) {  // 8 float4 reads in flight ahead of the 32 FMAs they feed (double-buffered)
+      const float4* l4 = reinterpret_cast<const float4*>(buf[blk & 1] + c * kWalkBlockStride);
       float4 a[8], bb[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) a[k] = l4[k];
 #pragma unroll
-      for (int k0 = 0; k0 < kRing * 2; k0 += 16) {
+      for (int k0 = 0; k0 < kWalkBlock / 32; k0 += 16) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) bb[k] = l4[k0 + 8 + k];
 #pragma unroll
@@ -244,7 +257,7 @@ __device__ __forceinline__ float walk_tensor(const float* __restrict__ xt, int64
           acc = __builtin_fmaf(a[k].z, a[k].z, acc);
           acc = __builtin_fmaf(a[k].w, a[k].w, acc);
         }
-        if (k0 + 16 < kRing * 2) {
+        if (k0 + 16 < kWalkBlock / 32) {
 #pragma unroll
           for (int k = 0; k < 8; ++k) a[k] = l4[k0 + 16 + k];
         }
@@ -257,24 +270,18 @@ __device__ __forceinline__ float walk_tensor(const float* __restrict__ xt, int64
         }
       }
     }
+    if (more) stage(blk + 1, buf[(blk + 1) & 1]);
+    __syncthreads();
   }
-  b = __shfl(acc, 0, 64);
+  if (tid < 64) {  // wave 0: lane sum left to right, the n % 8 tail, sqrt
+    float b = __shfl(acc, 0, 64);
 #pragma unroll
-  for (int j = 1; j < 8; ++j) b = b + __shfl(acc, j, 64);
-  for (int64_t i = nv; i < n; ++i) b = __builtin_fmaf(xt[i], xt[i], b);
-  return b;
-}
-
-// One wave per tensor of at most kWalkMax elements (the look-back kernel takes the longer ones).
-__global__ __launch_bounds__(64) void k_norm_walk(const float* __restrict__ x, const adfl_slq_chunk* __restrict__ chunks,
-                                                 int64_t max_n, float* __restrict__ norms) {
-  __shared__ __attribute__((aligned(16))) float lds[kWalkLds];
-  const adfl_slq_chunk c = chunks[blockIdx.x];
-  if ((int64_t)blockIdx.x != c.first_chunk) return;
-  const int64_t n = (int64_t)(c.nchunks - 1) * ADFL_SLQ_CHUNK_ELEMS + chunks[blockIdx.x + c.nchunks - 1].len;
-  if (n > max_n) return;
-  const float b = walk_tensor(x + c.start, n, lds);
-  if (threadIdx.x == 0) norms[c.tensor] = (float)__builtin_sqrt((double)b);  // correctly rounded fp32 sqrt
+    for (int j = 1; j < 8; ++j) b = b + __shfl(acc, j, 64);
+    if (tid == 0) {
+      for (int64_t i = nv; i < n; ++i) b = __builtin_fmaf(xt[i], xt[i], b);
+      norms[ch.tensor] = (float)__builtin_sqrt((double)b);  // correctly rounded fp32 sqrt
+    }
+  }
 }
 
 __global__ __launch_bounds__(kThreads) void k_norm_torch(const float* __restrict__ x,

@@ -71,6 +71,10 @@ def main():
                 x, lay, 8, seed=1, levels=lv, signs=sg, norms=nrm, ws=ws, torch_norm=tn))
             out[f"cnat_encode_{k}_ms"] = timed(lambda: stoch.cnat_encode_batched(
                 x, lay, 8, seed=1, exps=ex, signs=sg, norms=nrm, ws=ws, torch_norm=tn))
+        # the quantize alone, given the norms (the part of a torch_norm=True QSGD encode after the norm)
+        tn = stoch.torch_norms(x, lay)
+        out["qsgd_quantize_given_norms_ms"] = timed(lambda: stoch.qsgd_quantize_batched(
+            x, lay, 8, tn, seed=1, levels=lv, signs=sg))
         for c in ("qsgd", "cnat"):
             out[f"{c}_torch_over_default"] = round(out[f"{c}_encode_torch_ms"] / out[f"{c}_encode_default_ms"], 4)
         res[name] = out
