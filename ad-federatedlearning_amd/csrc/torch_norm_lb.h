@@ -95,7 +95,8 @@ static_assert(kTilesPerChunk * kTile == ADFL_SLQ_CHUNK_ELEMS * kChunksPerTile, "
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 
 struct Header {
-  unsigned long long ticket, done, epoch, error, pad[4];  // pad[0], pad[1]: retry / sequential-tile counts
+  unsigned long long ticket, done, epoch, error;
+  unsigned long long stats[4];  // look-back retries, sequential tiles, far misses, failed compositions (tools)
 };
 
 struct Rec {                      // granules {tag << 32 | value}, one per chain
@@ -668,10 +669,10 @@ __global__ __launch_bounds__(kThreads) void k_norm_torch(const float* __restrict
       }
       if (s_err) __hip_atomic_store(&hdr->error, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       // counters for tools/torch_norm_bench.py: look-back retries, tiles walked sequentially
-      if (s_retry) __hip_atomic_fetch_add(&hdr->pad[0], (unsigned long long)s_retry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (s_slow) __hip_atomic_fetch_add(&hdr->pad[1], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (s_retry) __hip_atomic_fetch_add(&hdr->stats[0], (unsigned long long)s_retry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (s_slow) __hip_atomic_fetch_add(&hdr->stats[1], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       for (int k = 0; k < 2; ++k)
-        if (s_why[k]) __hip_atomic_fetch_add(&hdr->pad[2 + k], (unsigned long long)s_why[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (s_why[k]) __hip_atomic_fetch_add(&hdr->stats[2 + k], (unsigned long long)s_why[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     }
   }
