@@ -36,6 +36,8 @@ import subprocess
 import sys
 import time
 
+_T_START = time.perf_counter()  # bench_wall_s: process start to the line (the driver's run includes interpreter start)
+
 import torch
 
 REPO = os.path.dirname(os.path.abspath(__file__))
@@ -982,6 +984,7 @@ def main():
                                          for name, k in KERNEL_SYMBOLS.items() if (v := live.get(k)) is not None}
         else:
             line["roofline"]["traffic_live_error"] = note
+    line["bench_wall_s"] = round(time.perf_counter() - _T_START, 1)
     emit(line)
     if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
