@@ -196,8 +196,11 @@ constexpr int kStageStride = kTile / 8 + 4;               // a slow tile staged 
 // register ring (2 KiB in flight) took 56 us on C3; with cross-lane shuffles instead of the LDS
 // transpose 95 us, and with its loads under branches (an s_waitcnt vmcnt(0) after each) 312 us.
 constexpr int kWalkThreads = 256;
-constexpr int kWalkRegs = 16;
-constexpr int kWalkBlock = kWalkThreads * kWalkRegs;  // 4096 elements: 512 steps of each chain
+#ifndef ADFL_TN_WALK_REGS
+#define ADFL_TN_WALK_REGS 8
+#endif
+constexpr int kWalkRegs = ADFL_TN_WALK_REGS;
+constexpr int kWalkBlock = kWalkThreads * kWalkRegs;  // 2048 elements: 256 steps of each chain
 constexpr int kWalkBlockStride = kWalkBlock / 8 + 4;   // floats per chain row (+4: banks, 16-byte reads)
 
 __global__ __launch_bounds__(kWalkThreads) void k_norm_walk(const float* __restrict__ x,
