@@ -79,8 +79,9 @@ void stream_copy(char* d, const char* s, size_t n) {
 // (> 0x7f800000) wins — torch.max(torch.abs(t)) (quant.py:100), as the device kernels reduce it. Cloned for
 // AVX-512 / AVX2 with the loader's run-time dispatch: the default x86-64 target has no unsigned 32-bit max
 // (SSE4.1), and the scalar loop reduced 15 GB/s from cache against 110 GB/s with AVX-512 (this container).
-// (hipcc also parses this file in its gfx950 pass, which has no x86 clones: the attribute is host-pass only.)
-#if defined(__x86_64__) && !defined(__HIP_DEVICE_COMPILE__)
+// (hipcc also parses this file in its gfx950 pass, which has no x86 clones: the attribute is host-pass only;
+// a ThreadSanitizer build runs the ifunc resolver before its runtime is up and crashes, so it is left out.)
+#if defined(__x86_64__) && !defined(__HIP_DEVICE_COMPILE__) && !defined(__SANITIZE_THREAD__)
 #define ADFL_X86_CLONES __attribute__((target_clones("avx512f", "avx2", "default")))
 #else
 #define ADFL_X86_CLONES
