@@ -189,10 +189,10 @@ constexpr int64_t kWalkMax = 1 << 16;                     // tensors up to this 
 constexpr int kStageStride = kTile / 8 + 4;               // a slow tile staged chain-major (+4: banks, 16 B)
 
 // One block per tensor of at most kWalkMax elements (the look-back kernel takes the longer ones) runs the
-// 8 chains in order — the reference's loop itself. Its four waves stream the tensor in 4096-element blocks
-// into an LDS double buffer, chain-major (buf[c][step]), so lane c < 8 of wave 0 reads its chain back 4
-// steps per ds_read_b128, eight reads ahead of the dependent FMAs (about 6.6 cycles per step,
-// MI355X_MICROARCH.md), while the next block's 16 KiB are in flight. A one-wave version with a 32-row
+// 8 chains in order — the reference's loop itself. Its four waves stream the tensor in 2048-element blocks
+// into LDS buffers, chain-major (buf[c][step]), so lane c < 8 of wave 0 reads its chain back 4 steps
+// per ds_read_b128, eight reads ahead of the dependent FMAs (about 6.6 cycles per step,
+// MI355X_MICROARCH.md), while the next two blocks are in flight. A one-wave version with a 32-row
 // register ring (2 KiB in flight) took 56 us on C3; with cross-lane shuffles instead of the LDS
 // transpose 95 us, and with its loads under branches (an s_waitcnt vmcnt(0) after each) 312 us.
 constexpr int kWalkThreads = 256;
@@ -206,7 +206,7 @@ constexpr int kWalkBlockStride = kWalkBlock / 8 + 4;   // floats per chain row (
 __global__ __launch_bounds__(kWalkThreads) void k_norm_walk(const float* __restrict__ x,
                                                            const adfl_slq_chunk* __restrict__ chunks,
                                                            int64_t max_n, float* __restrict__ norms) {
-  __shared__ __attribute__((aligned(16))) float buf[2][8 * kWalkBlockStride];
+  __shared__ __attribute__((aligned(16))) float buf[3][8 * kWalkBlockStride];
   const adfl_slq_chunk ch = chunks[blockIdx.x];
   if ((int64_t)blockIdx.x != ch.first_chunk) return;
   const int64_t n = (int64_t)(ch.nchunks - 1) * ADFL_SLQ_CHUNK_ELEMS + chunks[blockIdx.x + ch.nchunks - 1].len;
@@ -225,56 +225,69 @@ __global__ __launch_bounds__(kWalkThreads) void k_norm_walk(const float* __restr
     return;
   }
   const int64_t nv = n - n % 8, nblocks = (nv + kWalkBlock - 1) / kWalkBlock;
-  // unconditional (clamped) loads keep a block's 16 of them in flight; elements past nv become zeros,
-  // which leave the accumulators unchanged (fmaf(0, 0, a) == a)
-  float r[kWalkRegs];
-  const auto load = [&](int64_t blk) {
-#pragma unroll
-    for (int i = 0; i < kWalkRegs; ++i) r[i] = xt[min(blk * kWalkBlock + i * kWalkThreads + tid, nv - 1)];
-  };
-  const auto stage = [&](int64_t blk, float* dst) {
+  // Buffer loads through a per-block descriptor whose range ends at nv: elements past it (and whole blocks
+  // past the end) read as zeros, which leave the accumulators unchanged (fmaf(0, 0, a) == a), so loads and
+  // stages carry no masks or branches. While block b is summed, block b + 1 is already in LDS (so the walk's
+  // reads run on into it without a stall), block b + 2 is staged from registers loaded one block earlier
+  // and block b + 3 loads (three LDS buffers, two register sets used alternately).
+  const auto load = [&](float (&r)[kWalkRegs], int64_t blk) {
+    const int64_t base = blk * kWalkBlock, left = nv - base;
+    const int bytes = left <= 0 ? 0 : (int)(min(left, (int64_t)kWalkBlock) * 4);
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xt + (left <= 0 ? 0 : base)), 0, bytes,
+                                                      0x00020000);
 #pragma unroll
     for (int i = 0; i < kWalkRegs; ++i)
-      dst[c * kWalkBlockStride + (kWalkThreads / 8) * i + s0] =
-          blk * kWalkBlock + i * kWalkThreads + tid < nv ? r[i] : 0.0f;
+      r[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (i * kWalkThreads + tid) * 4, 0, 0));
   };
-  load(0);
-  stage(0, buf[0]);
-  __syncthreads();
+  const auto stage = [&](const float (&r)[kWalkRegs], float* dst) {
+#pragma unroll
+    for (int i = 0; i < kWalkRegs; ++i) dst[c * kWalkBlockStride + (kWalkThreads / 8) * i + s0] = r[i];
+  };
+  // The walk: lanes 0-7 of wave 0 each run one chain through a ring of 16 float4 reads (64 steps) ahead of
+  // the FMAs; a read is issued as each group of 4 FMAs retires its slot, and the ring's reads run from the
+  // end of the block on into the head of the next one. sched_barrier keeps that order: left alone, the
+  // scheduler batched the 16 reads and left the LDS latency exposed once per 64 steps (36 us on C3).
+  constexpr int kGroups = kWalkBlock / 32, kRing = 16;
+  static_assert(kGroups % kRing == 0, "the ring must restart at the same slot every block");
   float acc = 0.0f;
-  for (int64_t blk = 0; blk < nblocks; ++blk) {
-    const bool more = blk + 1 < nblocks;  // block-uniform
-    if (more) load(blk + 1);
-    if (tid < 8) {  // 8 float4 reads in flight ahead of the 32 FMAs they feed (double-buffered)
-      const float4* l4 = reinterpret_cast<const float4*>(buf[blk & 1] + c * kWalkBlockStride);
-      float4 a[8], bb[8];
+  float4 ring[kRing];
+  const auto walk = [&](const float* cur, const float* nxt) {
+    if (tid < 8) {
+      const float4* l4 = reinterpret_cast<const float4*>(cur + c * kWalkBlockStride);
+      const float4* n4 = reinterpret_cast<const float4*>(nxt + c * kWalkBlockStride);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) a[k] = l4[k];
-#pragma unroll
-      for (int k0 = 0; k0 < kWalkBlock / 32; k0 += 16) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) bb[k] = l4[k0 + 8 + k];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          acc = __builtin_fmaf(a[k].x, a[k].x, acc);
-          acc = __builtin_fmaf(a[k].y, a[k].y, acc);
-          acc = __builtin_fmaf(a[k].z, a[k].z, acc);
-          acc = __builtin_fmaf(a[k].w, a[k].w, acc);
-        }
-        if (k0 + 16 < kWalkBlock / 32) {
-#pragma unroll
-          for (int k = 0; k < 8; ++k) a[k] = l4[k0 + 16 + k];
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          acc = __builtin_fmaf(bb[k].x, bb[k].x, acc);
-          acc = __builtin_fmaf(bb[k].y, bb[k].y, acc);
-          acc = __builtin_fmaf(bb[k].z, bb[k].z, acc);
-          acc = __builtin_fmaf(bb[k].w, bb[k].w, acc);
-        }
+      for (int j = 0; j < kGroups; ++j) {
+        const float4 v = ring[j % kRing];
+        acc = __builtin_fmaf(v.x, v.x, acc);
+        acc = __builtin_fmaf(v.y, v.y, acc);
+        acc = __builtin_fmaf(v.z, v.z, acc);
+        acc = __builtin_fmaf(v.w, v.w, acc);
+        ring[j % kRing] = j + kRing < kGroups ? l4[j + kRing] : n4[j + kRing - kGroups];
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
-    if (more) stage(blk + 1, buf[(blk + 1) & 1]);
+  };
+  float ra[kWalkRegs], rb[kWalkRegs];
+  load(ra, 0);
+  load(rb, 1);
+  stage(ra, buf[0]);
+  stage(rb, buf[1]);
+  load(ra, 2);
+  __syncthreads();
+  if (tid < 8) {
+    const float4* l4 = reinterpret_cast<const float4*>(buf[0] + c * kWalkBlockStride);
+#pragma unroll
+    for (int j = 0; j < kRing; ++j) ring[j] = l4[j];
+  }
+  for (int64_t blk = 0; blk < nblocks; blk += 2) {  // block-uniform control flow throughout
+    load(rb, blk + 3);
+    walk(buf[blk % 3], buf[(blk + 1) % 3]);
+    stage(ra, buf[(blk + 2) % 3]);
+    __syncthreads();
+    if (blk + 1 >= nblocks) break;
+    load(ra, blk + 4);
+    walk(buf[(blk + 1) % 3], buf[(blk + 2) % 3]);
+    stage(rb, buf[(blk + 3) % 3]);
     __syncthreads();
   }
   if (tid < 64) {  // wave 0: lane sum left to right, the n % 8 tail, sqrt
