@@ -4,8 +4,7 @@
 // The order. torch 2.10's CPU vector_norm(ord=2) over n >= 8 fp32 elements keeps 8 accumulators,
 // acc[j] = fmaf(x[8i+j], x[8i+j], acc[j]) for i in order, then sums them left to right and runs the n % 8
 // tail with fmaf (oracle/slq_oracle.c oracle_torch_l2_norm, pinned to every golden norm). Each chain is a
-// sequence of dependent roundings: one wave per tensor (k_norm_torch_order) runs at about one step per
-// cycle per tensor.
+// sequence of dependent roundings: run in order (k_norm_walk) it costs one dependent FMA latency per step.
 //
 // Why it parallelises. A step is RN32(acc + p) with p = x*x exact (48 bits: exact in fp64). While acc stays
 // in one binade, acc = A * u with u = 2^(g-23) the binade's ulp and A an integer below 2^24 (g = -126 also
@@ -17,7 +16,7 @@
 // too, the increments being >= 0 and R(v) >= v - 1/2). tools/torch_norm_proto.c checks this model against
 // the sequential chain on random, tie-heavy, subnormal, overflow and NaN / inf data.
 //
-// Short tensors (<= kWalkMax elements): k_norm_walk, one wave per tensor running the chains in order, the
+// Short tensors (<= kWalkMax elements): k_norm_walk, one block per tensor running the chains in order, the
 // rows written to LDS chain-major so each chain reads 4 steps per ds_read_b128 ahead of its FMA chain.
 //
 // Long tensors: k_norm_torch. The 8 chains run over tiles of kTile = 16384 elements (2048 steps of each
