@@ -1239,7 +1239,7 @@ int adfl_stoch_norms_batched(const float* d_x, const adfl_slq_chunk* d_chunks, i
   if (mode != ADFL_NORM_L2 && mode != ADFL_NORM_LINF && mode != ADFL_NORM_L2_TORCH) return ADFL_E_ARG;
   if (!aligned16(d_x)) return ADFL_E_ALIGN;
   hipStream_t st = (hipStream_t)stream;
-  if (mode == ADFL_NORM_L2_TORCH) {  // no workspace: one wave per tensor
+  if (mode == ADFL_NORM_L2_TORCH) {  // no workspace: one block per tensor
     hipLaunchKernelGGL(adfl_tn::k_norm_walk, dim3((unsigned)nchunks), dim3(adfl_tn::kWalkThreads), 0, st, d_x, d_chunks,
                        INT64_MAX, d_norms);
     return launch_status();

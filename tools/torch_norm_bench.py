@@ -1,7 +1,7 @@
 """Cost of the reference-order L2 norm against the default (fp64) one on C2 and C3, device-resident.
 
 Times (median of --reps, each after a 512 MiB read so x comes from HBM) of:
-  norm      norms_batched NORM_L2 (default) | torch_norms (look-back) | NORM_L2_TORCH (one wave per tensor)
+  norm      norms_batched NORM_L2 (default) | torch_norms (look-back) | NORM_L2_TORCH (one block per tensor, in order)
   encode    qsgd_encode_batched / cnat_encode_batched with torch_norm False | True (bits 8, in-kernel Philox)
 
     python tools/torch_norm_bench.py [--reps 21] [--no-seq]
