@@ -21,14 +21,19 @@ generate their uniforms from a Philox4x32-7 stream keyed by it. The uniforms are
 mt19937 draws, so individual rounding decisions differ from a reference run; their distribution is the
 same (and with injected uniforms the codec is bit-identical: tests/test_gpu_stoch.py).
 
-Norms: L2 norms are the correctly rounded fp32 norm (fp64 accumulation of fp32 squares); torch's fp32
-accumulation is less accurate. There is no CPU fallback: without the HIP library these raise.
+Norms: the L2 norm (QSGD, CNAT) is the reference's own, bit for bit: torch 2.10's CPU
+``torch.linalg.vector_norm`` order in the tensor's dtype (fp32 / bf16 / fp16 / fp64; fp16's split over
+``torch.get_num_threads()`` as the reference's call would make it), by csrc/torch_norm.hip. ADFL_STOCH_NORM=fp64
+in the environment switches to the correctly rounded norm (fp64 accumulation of the squares: faster on very
+large tensors, within torch's own summation error of the reference's). RQSGD's max / min norms are exact either
+way. There is no CPU fallback: without the HIP library these raise.
 
 fp16 / bf16 / fp64 tensors are encoded as the reference encodes them, in their own dtype's arithmetic (each
 op rounded to the dtype; uniforms on torch.rand's grid for the dtype): one bucket per dtype through the
 *_dt kernels (csrc/stoch_dtype.hip). Their payloads decode like fp32 ones (the reference decodes to fp32).
 """
 
+import os
 import time
 from typing import Dict, List, Tuple
 
@@ -41,6 +46,15 @@ from .channel import Channel, IdentityChannel
 from .quant import _PendingD2H, _aggregate_entries, _hand_out, _serialized, _stage_in, _stage_rows, _staging
 
 _CODECS = ("qsgd", "rqsgd", "cnat")
+
+
+def reference_norm() -> bool:
+    """The L2 norm mode of the QSGD / CNAT channels: True (default) = the reference's own norm, torch's CPU
+    order bit for bit; ADFL_STOCH_NORM=fp64 = the correctly rounded norm (fp64 accumulation)."""
+    mode = os.environ.get("ADFL_STOCH_NORM", "torch").lower()
+    if mode not in ("torch", "fp64"):
+        raise ValueError(f"ADFL_STOCH_NORM must be 'torch' (the reference's norm) or 'fp64', got {mode!r}")
+    return mode == "torch"
 
 
 def _require_codable(name: str, t: torch.Tensor, cls: str) -> None:
@@ -77,7 +91,7 @@ def _owned_host(buf: torch.Tensor, offsets, shapes: List[torch.Size]) -> List[to
 
 @_serialized
 def _encode_stoch(params: Parameters, names: List[str], codec: str, bits: int, uniforms=None, seed=None,
-                  torch_norm: bool = False):
+                  torch_norm: bool = True):
     """Encode the ndim > 1 fp32 tensors `names` of `params` in one bucketed pass.
 
     Returns {name: (data, signs, scale, scale_2)} with CPU tensors for CPU inputs (device tensors for
@@ -156,7 +170,8 @@ COUNTER_BASE = {torch.float32: 0, torch.float16: 1 << 40, torch.bfloat16: 2 << 4
 
 
 @_serialized
-def _encode_stoch_dt(params: Parameters, names: List[str], codec: str, bits: int, uniforms=None, seed=None):
+def _encode_stoch_dt(params: Parameters, names: List[str], codec: str, bits: int, uniforms=None, seed=None,
+                     torch_norm: bool = True):
     """Encode the ndim > 1 tensors `names` (all of one dtype: fp16 / bf16 / fp64) in one bucketed pass, in
     that dtype's arithmetic (adfl_stoch_encode_batched_dt). Same return as _encode_stoch; the norms are the
     dtype's values as Python floats (norm.item() of the reference's 0-dim norm tensor)."""
@@ -171,11 +186,16 @@ def _encode_stoch_dt(params: Parameters, names: List[str], codec: str, bits: int
         seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
     ws = st.buf("stoch_ws", lay.nchunks * 16, torch.uint8)
     u = uniforms if uniforms is not None and uniforms.dtype == dtype else None
-    lv, sg, norms, mins = sops.encode_batched_dt(codec, x_dev, lay, bits, uniforms=u, seed=seed,
-                                                 counter=COUNTER_BASE[dtype],
-                                                 levels=st.buf("s_levels", lay.total, torch.uint8).view(
-                                                     torch.int8 if codec == "cnat" else torch.uint8),
-                                                 signs=st.buf("s_signs", lay.total, torch.int8), ws=ws)
+    levels = st.buf("s_levels", lay.total, torch.uint8).view(torch.int8 if codec == "cnat" else torch.uint8)
+    signs = st.buf("s_signs", lay.total, torch.int8)
+    if codec != "rqsgd" and torch_norm:  # the reference's norm in the dtype, then the given-norm quantize
+        norms, _ = sops.reference_norms(x_dev, lay, out64=st.buf("s_norms64", lay.ntensors, torch.float64))
+        lv, sg = sops.quantize_batched_dt(codec, x_dev, lay, bits, norms, uniforms=u, seed=seed,
+                                          counter=COUNTER_BASE[dtype], levels=levels, signs=signs)
+        mins = None
+    else:
+        lv, sg, norms, mins = sops.encode_batched_dt(codec, x_dev, lay, bits, uniforms=u, seed=seed,
+                                                     counter=COUNTER_BASE[dtype], levels=levels, signs=signs, ws=ws)
     nm = torch.cat([norms, mins]) if mins is not None else norms
     on_cpu = [not t.is_cuda for t in tensors]
     shapes = [t.shape for t in tensors]
@@ -289,14 +309,11 @@ class _StochChannel(Channel):
     CODEC = "qsgd"
     NORM_BYTES = 4  # per quantized tensor: the norm (RQSGD: norm + minimum factor)
 
-    def __init__(self, bits: int, torch_norm: bool = False) -> None:
-        """torch_norm=True: the L2 norm (QSGD, CNAT) in torch's own fp32 reduction order, bit-identical to
-        the reference's torch.linalg.vector_norm (sequential per tensor: slower on large tensors). The
-        default is the correctly rounded norm (fp64 accumulation), within torch's own summation error of it."""
+    def __init__(self, bits: int) -> None:
+        """The reference's constructor (quant.py:145-147): the L2 norm is the reference's own (see the module
+        docstring; ADFL_STOCH_NORM=fp64 selects the correctly rounded one instead)."""
         self.bits = bits
         self.levels = 2 ** bits - 1
-        if torch_norm:
-            self.torch_norm = True  # only set when asked: the default object has the reference's attributes
 
     def on_server_send(self, params: Parameters) -> Tuple[CompressedParameters, float]:
         return self._send(params)
@@ -420,13 +437,13 @@ class _StochChannel(Channel):
             raise ValueError(f"{self.__class__.__name__}: injected uniforms ({uniforms.dtype}) cover one dtype bucket; "
                              f"this dict also holds {sorted(str(d) for d in {params[n].dtype for n in names})}")
         f32 = [n for n in names if params[n].dtype == torch.float32]
+        tn = reference_norm()
         encoded = (_encode_stoch(params, f32, self.CODEC, bits, uniforms if uniforms is None or
-                                 uniforms.dtype == torch.float32 else None, seed,
-                                 getattr(self, "torch_norm", False)) if f32 else {})
+                                 uniforms.dtype == torch.float32 else None, seed, tn) if f32 else {})
         for dtype in sops.DT_DTYPES:   # fp16 / bf16 / fp64: one bucket per dtype, in that dtype's arithmetic
             group = [n for n in names if params[n].dtype == dtype]
             if group:
-                encoded.update(_encode_stoch_dt(params, group, self.CODEC, bits, uniforms, seed))
+                encoded.update(_encode_stoch_dt(params, group, self.CODEC, bits, uniforms, seed, tn))
         q_params = QuantParameters({}, 0)
         pass_signs = torch.zeros(1, dtype=torch.uint8)  # passthrough entries' unused signs, one per call
         for name, param in params.items():

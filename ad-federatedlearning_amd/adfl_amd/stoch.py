@@ -22,7 +22,7 @@ from typing import Optional, Tuple
 import torch
 
 from . import _lib
-from ._lib import (CODEC_CNAT, CODEC_QSGD, CODEC_RQSGD, DTYPE_BF16, DTYPE_F16, DTYPE_F64, NORM_L2, NORM_L2_TORCH,
+from ._lib import (CODEC_CNAT, CODEC_QSGD, CODEC_RQSGD, DTYPE_BF16, DTYPE_F16, DTYPE_F32, DTYPE_F64, NORM_L2, NORM_L2_TORCH,
                    NORM_LINF, check)
 from .ops import BucketLayout, _dev, _stream
 
@@ -139,6 +139,46 @@ def torch_norms(flat: torch.Tensor, layout: BucketLayout, *, norms: Optional[tor
     return norms
 
 
+_REF_NORM_DTYPES = {torch.float32: DTYPE_F32, torch.float16: DTYPE_F16, torch.bfloat16: DTYPE_BF16,
+                    torch.float64: DTYPE_F64}
+
+
+def reference_norms(flat: torch.Tensor, layout: BucketLayout, *, threads: Optional[int] = None,
+                    out64: Optional[torch.Tensor] = None, out32: Optional[torch.Tensor] = None):
+    """Per-tensor ``torch.linalg.vector_norm(x, ord=2)`` of an fp32 / fp16 / bf16 / fp64 bucket, bit-identical
+    to torch 2.10's CPU kernel — the reference's QSGD / CNAT norm in the tensor's own dtype (quant.py:226,512)
+    — by adfl_torch_norms (csrc/torch_norm.hip: phases with no cross-block waits).
+
+    threads: the torch.get_num_threads() whose fp16 split is reproduced (default: this process's, which is
+    what the reference's own call would use). Returns (out64, out32): fp64 norms (the dtype's exact value)
+    and fp32 ones; pass either to fill it (the other stays None unless passed too); with neither, out64 is
+    allocated."""
+    if flat.dtype not in _REF_NORM_DTYPES:
+        raise ValueError(f"adfl_amd.stoch: reference_norms takes fp32 / fp16 / bf16 / fp64 buckets, got {flat.dtype}")
+    flat = _dev(flat, "flat")
+    if flat.numel() < layout.total:
+        raise ValueError("adfl_amd.stoch: flat buffer smaller than the layout")
+    dev = flat.device
+    if out64 is None and out32 is None:
+        out64 = torch.empty(layout.ntensors, dtype=torch.float64, device=dev)
+    for o, dt in ((out64, torch.float64), (out32, torch.float32)):
+        if o is not None and (o.dtype != dt or o.numel() < layout.ntensors or not o.is_contiguous() or o.device != dev):
+            raise ValueError(f"adfl_amd.stoch: norm outputs must be contiguous {dt} device tensors of >= ntensors")
+    if layout.nchunks == 0:
+        return out64, out32
+    L = _lib.load()
+    threads = torch.get_num_threads() if threads is None else int(threads)
+    short_max = L.adfl_torch_norm_short_max()
+    kinds = (1 if min(layout.sizes) <= short_max else 0) | (2 if max(layout.sizes) > short_max else 0)
+    need = L.adfl_torch_norm_scratch_bytes(layout.nchunks, layout.ntensors)
+    scratch = torch.empty(need, dtype=torch.uint8, device=dev)  # stream-ordered: no initialisation needed
+    check(L.adfl_torch_norms(_REF_NORM_DTYPES[flat.dtype], flat.data_ptr(), layout.device_chunks(dev).data_ptr(),
+                             layout.nchunks, layout.ntensors, kinds, threads, scratch.data_ptr(), need,
+                             out64.data_ptr() if out64 is not None else None,
+                             out32.data_ptr() if out32 is not None else None, _stream(dev)))
+    return out64, out32
+
+
 def _planes(layout, dev, levels, signs, ldtype):
     levels = torch.empty(layout.total, dtype=ldtype, device=dev) if levels is None else levels
     signs = torch.empty(layout.total, dtype=torch.int8, device=dev) if signs is None else signs
@@ -166,7 +206,8 @@ def qsgd_encode_batched(flat: torch.Tensor, layout: BucketLayout, bits: int, *,
                         norms: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None,
                         torch_norm: bool = False, resident: Optional[bool] = None):
     """QSGD encode of every tensor of a bucket: (levels u8, signs i8, L2 norms f32). torch_norm=True takes
-    the norm in torch's reduction order (the reference's norm bit for bit; slower, sequential per tensor).
+    the norm in torch's reduction order (the reference's norm bit for bit: reference_norms, then the
+    given-norm quantize); False, the one-launch encode's correctly rounded norm.
     resident: None = the one-launch register-resident encode whenever the layout allows it (same bytes as
     the multi-launch path), False = always the multi-launch path."""
     flat = _check_flat(flat, layout)
@@ -175,7 +216,7 @@ def qsgd_encode_batched(flat: torch.Tensor, layout: BucketLayout, bits: int, *,
     norms = torch.empty(layout.ntensors, dtype=torch.float32, device=dev) if norms is None else norms
     ws = _ws(ws, layout, dev)
     if torch_norm:
-        torch_norms(flat, layout, norms=norms)
+        reference_norms(flat, layout, out32=norms)
         qsgd_quantize_batched(flat, layout, bits, norms, uniforms=uniforms, seed=seed, counter=counter,
                               levels=levels, signs=signs)
         return levels, signs, norms
@@ -249,7 +290,7 @@ def cnat_encode_batched(flat: torch.Tensor, layout: BucketLayout, bits: int, *,
                                                     ws.numel(), exps.data_ptr(), signs.data_ptr(), norms.data_ptr(),
                                                     _stream(dev)))
     if torch_norm:
-        torch_norms(flat, layout, norms=norms)
+        reference_norms(flat, layout, out32=norms)
     return exps, signs, norms
 
 

@@ -1225,6 +1225,15 @@ inline int launch_resident(const float* d_x, const adfl_slq_chunk* d_chunks, int
 
 }  // namespace
 
+namespace adfl_tn {
+// The in-order walker for fp32 tensors of at most kWalkMax elements, for adfl_torch_norms (torch_norm.hip).
+int launch_walk(const float* x, const adfl_slq_chunk* chunks, int64_t nchunks, float* n32, double* n64,
+                hipStream_t st) {
+  hipLaunchKernelGGL(k_norm_walk, dim3((unsigned)nchunks), dim3(kWalkThreads), 0, st, x, chunks, kWalkMax, n32, n64);
+  return (int)hipGetLastError();
+}
+}  // namespace adfl_tn
+
 // ================================================================================================
 // C ABI
 // ================================================================================================
@@ -1241,7 +1250,7 @@ int adfl_stoch_norms_batched(const float* d_x, const adfl_slq_chunk* d_chunks, i
   hipStream_t st = (hipStream_t)stream;
   if (mode == ADFL_NORM_L2_TORCH) {  // no workspace: one block per tensor
     hipLaunchKernelGGL(adfl_tn::k_norm_walk, dim3((unsigned)nchunks), dim3(adfl_tn::kWalkThreads), 0, st, d_x, d_chunks,
-                       INT64_MAX, d_norms);
+                       INT64_MAX, d_norms, nullptr);
     return launch_status();
   }
   if (int s = check_ws(d_workspace, workspace_bytes, nchunks)) return s;
@@ -1272,7 +1281,7 @@ int adfl_stoch_norms_torch(const float* d_x, const adfl_slq_chunk* d_chunks, int
   hipStream_t st = (hipStream_t)stream;
   if (kinds & ADFL_TORCH_NORM_SHORT) {
     hipLaunchKernelGGL(adfl_tn::k_norm_walk, dim3((unsigned)nchunks), dim3(adfl_tn::kWalkThreads), 0, st, d_x,
-                       d_chunks, adfl_tn::kWalkMax, d_norms);
+                       d_chunks, adfl_tn::kWalkMax, d_norms, nullptr);
     if (int s = launch_status()) return s;
   }
   if (kinds & ADFL_TORCH_NORM_LONG) {

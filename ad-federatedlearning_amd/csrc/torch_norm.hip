@@ -1,0 +1,1309 @@
+// torch_norm.hip — torch 2.10's CPU L2 norm (torch.linalg.vector_norm(x, ord=2), the reference's QSGD / CNAT
+// scale: Src/ADFL/Channel/quant.py:226,512) of fp32 / bf16 / fp16 / fp64 tensors, bit for bit, in phases with
+// no cross-block waits.
+//
+// The orders (oracle/slq_oracle.c restates each; tests/test_torch_norm_dtypes.py pins them to torch itself):
+//   fp32  8 fp32 chains, element e into chain e % 8 for e < n - n % 8, acc = fmaf(x, x, acc) in order; lane
+//         sum left to right; the n % 8 tail as torch's compiled scalar loop runs it (a group of 4 rounded
+//         squares added in order when there are 4 or more, the rest with fmaf); fp32 sqrt.
+//   bf16  the same 8 fp32 chains over e < n - n % 16 (16-element vectors), tail with fmaf; sqrt, to bf16.
+//   fp16  at::parallel_for's split: nt = min(threads, ceil(n / 32768)) chunks (1 below 32768 elements or
+//         with one thread) of ceil(n / nt) elements, each one fp32 chain from 0; the chain sums added in
+//         order; sqrt, to fp16. `threads` is the caller's torch.get_num_threads().
+//   fp64  4 fp64 chains (e % 4, e < n - n % 4) with fma; lane sum; the tail with fma; fp64 sqrt.
+//   Every dtype: a one-element tensor's norm is |x| (no square, so no underflow).
+// Squares of fp16 / bf16 / fp32 values are exact in fp64 (and fp16 / bf16 ones in fp32), so every chain step
+// is acc <- RN(acc + p) with p exact: fp32 accumulators for fp32 / bf16 / fp16, fp64 ones for fp64.
+//
+// The integer model. While acc stays in one binade it is A * u (u the binade's ulp, A an integer below
+// 2^24 — 2^53 for fp64 — and above 2^23 / 2^52 unless the binade is the subnormal one) and a step that does
+// not leave the binade is A <- A + R(p / u), R = round half to even. A step whose p / u is not a tie adds
+// a constant k. A tie, p / u = f + 1/2, gives A + f rounded up to even: it depends on A's parity only.
+// So a run of steps is a pair of constants (Ke, Ko) — what it adds to an even / an odd A — and runs
+// compose associatively: (a then b).e = a.e + (a.e odd ? b.o : b.e), .o = a.o + (a.o even ? b.o : b.e).
+// A run is exact from A if A + its increment stays below 2^24 (increments are >= 0, so every partial sum
+// does too). Only a step that leaves the binade (a "crossing", about log2 of the norm's growth per chain),
+// a non-finite value, or a step of 2^24 ulps or more is not covered: the reference arithmetic (fma) runs it.
+//
+// Phases (long tensors: more than kShortMax elements), one launch each, every block independent:
+//   A  k_tn_stage<.., false>: per 8192-element chunk and chain, the fp64 sum S of x^2 (one read of x);
+//   B  k_tn_grids: per chain, the exclusive fp64 prefix of S over its tiles predicts the binade of the
+//      fp32 / fp64 accumulator at each tile's start: g_hi = binade of P (1 + 2^-8); the chain trails the
+//      exact prefix (fp32 chains of randn at 2^25 steps by about 7 %), so g_hi and g_hi - 1 are kept;
+//   C  k_tn_stage<.., true>: per chunk and chain, the maps (Ke, Ko) of its steps under g_hi and g_hi - 1
+//      (second read of x): staged chain-major through LDS so a lane holds 16 consecutive steps of a chain,
+//      lane maps composed in order across the wave;
+//   D  k_tn_resolve: one block per tensor, one wave per chain: the chain's tiles 64 at a time — pick each
+//      tile's map for the exact accumulator's binade, exclusive scan of the maps, and the first tile that
+//      is not covered (a crossing, a miss of the predictor) is resolved in detail: its steps in segments
+//      of 1024, lane maps under the current binade, scanned, the first uncovered lane runs its 16 steps
+//      with fma, and so on. Then the lane sum, tail, sqrt and rounding to the dtype.
+// Short tensors go straight to D with every tile resolved in detail.
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <hip/hip_fp16.h>
+
+#include <cstdint>
+
+#include "adfl_slq.h"
+#include "adfl_stoch.h"
+
+namespace adfl_tn {
+int launch_walk(const float* x, const adfl_slq_chunk* chunks, int64_t nchunks, float* n32, double* n64, hipStream_t st);
+}
+
+namespace adfl_tnx {
+
+#ifdef ADFL_TN_STATS  // tools/ref_norm_prof.py --stats builds: phase D counters per wave, printed per launch
+__device__ unsigned long long g_tn_stats[8][5];  // window descents, tiles in detail, segment rounds, cycles, cycles in detail
+#define TN_STAT(i, v) do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_tn_stats[(threadIdx.x >> 6) & 7][i], (unsigned long long)(v)); } while (0)
+#else
+#define TN_STAT(i, v) do { } while (0)
+#endif
+
+constexpr int kChunk = ADFL_SLQ_CHUNK_ELEMS;      // 8192: a tile is a chunk's steps of one chain
+constexpr int kSlots = 8;                         // records per chunk: one per chain (strided) or piece (fp16)
+constexpr int kLane = 16;                         // steps per lane
+constexpr int kSeg = 64 * kLane;                  // 1024 steps: one wave's segment
+constexpr int64_t kShortMax = 1 << 16;            // tensors up to this size skip phases A-C
+constexpr int64_t kGrain = 32768;                 // at::internal::GRAIN_SIZE
+constexpr int kMaxChains = 512;                   // fp16: chains (torch threads) per tensor the combine holds
+constexpr double kMagic = 6755399441055744.0;     // 1.5 * 2^52: (v + kMagic) - kMagic = rint(v), 0 <= v < 2^51
+constexpr int kTPL = 8;                           // phase D: tiles per lane
+constexpr int kWinTiles = 64 * kTPL;              // phase D: tiles per window
+
+__device__ __forceinline__ float fma_t(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+__device__ __forceinline__ double fma_t(double a, double b, double c) { return __builtin_fma(a, b, c); }
+__device__ __forceinline__ double pow2(int k) { return __longlong_as_double((long long)(k + 1023) << 52); }
+__device__ __forceinline__ bool odd(double v) { return floor(v * 0.5) * 2.0 != v; }  // v an integer
+
+// ---- accumulator types
+template <bool W> struct Acc;
+template <> struct Acc<false> {
+  using T = float;
+  static constexpr int kM = 23, kGmin = -126, kGmax = 127;
+  static constexpr double kTop = 16777216.0;  // 2^24
+};
+template <> struct Acc<true> {
+  using T = double;
+  static constexpr int kM = 52, kGmin = -1022, kGmax = 1023;
+  static constexpr double kTop = 9007199254740992.0;  // 2^53
+};
+
+__device__ __forceinline__ int grid_of(float a) {
+  const uint32_t ef = __float_as_uint(a) >> 23;
+  return ef <= 1u ? -126 : (int)ef - 127;
+}
+__device__ __forceinline__ int grid_of(double a) {
+  const uint64_t ef = (uint64_t)__double_as_longlong(a) >> 52;
+  return ef <= 1u ? -1022 : (int)ef - 1023;
+}
+__device__ __forceinline__ double a_of(float a) {  // the integer A of a finite accumulator >= 0 on its grid
+  const uint32_t b = __float_as_uint(a), m = b & 0x7fffffu;
+  return (double)((b >> 23) ? (m | 0x800000u) : m);
+}
+__device__ __forceinline__ double a_of(double a) {
+  const uint64_t b = (uint64_t)__double_as_longlong(a), m = b & ((1ull << 52) - 1);
+  return (double)(long long)((b >> 52) ? (m | (1ull << 52)) : m);
+}
+template <bool W> __device__ __forceinline__ typename Acc<W>::T rebuild(double A, int g);
+template <> __device__ __forceinline__ float rebuild<false>(double A, int g) { return (float)(A * pow2(g - 23)); }
+template <> __device__ __forceinline__ double rebuild<true>(double A, int g) { return (A * 0x1p-52) * pow2(g); }
+
+// the binade an accumulator near the exact value v >= 0 is predicted in
+template <bool W> __device__ __forceinline__ int grid_pred(double v) {
+  v *= 1.0 + 0x1p-8;
+  if (!(v < 0x1p127) && !W) return 127;
+  if (!W && v < 0x1p-125) return -126;
+  if (W && !(v < 0x1p1023)) return 1023;
+  if (W && v < 0x1p-1021) return -1022;
+  return (int)(((uint64_t)__double_as_longlong(v) >> 52) & 0x7ff) - 1023;
+}
+
+// ---- maps: what a run of steps adds to an even / an odd A
+struct Map {
+  double e, o;
+};
+__device__ __forceinline__ Map compose(Map a, Map b) {  // a, then b
+  return Map{a.e + (odd(a.e) ? b.o : b.e), a.o + (odd(a.o) ? b.e : b.o)};
+}
+__device__ __forceinline__ double apply(Map m, double A) { return A + (odd(A) ? m.o : m.e); }
+__device__ __forceinline__ Map shfl_up(Map m, int o) { return Map{__shfl_up(m.e, o, 64), __shfl_up(m.o, o, 64)}; }
+__device__ __forceinline__ Map shfl_xor(Map m, int o) { return Map{__shfl_xor(m.e, o, 64), __shfl_xor(m.o, o, 64)}; }
+
+// every lane: the composition of all 64 lanes' maps in lane order
+__device__ __forceinline__ Map wave_compose(Map m, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const Map p = shfl_xor(m, o);
+    m = (lane & o) ? compose(p, m) : compose(m, p);
+  }
+  return m;
+}
+// exclusive prefix (composition of the lanes before this one; identity on lane 0)
+__device__ __forceinline__ Map wave_excl(Map m, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const Map p = shfl_up(m, o);
+    if (lane >= o) m = compose(p, m);
+  }
+  const Map x = shfl_up(m, 1);
+  return lane == 0 ? Map{0.0, 0.0} : x;
+}
+__device__ __forceinline__ double wave_excl_sum(double v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double p = __shfl_up(v, o, 64);
+    if (lane >= o) v += p;
+  }
+  const double x = __shfl_up(v, 1, 64);
+  return lane == 0 ? 0.0 : x;
+}
+
+// ---- one step's increment on grid with ulp 2^-s (s = kM - g): k and whether it is a tie (then k = floor)
+__device__ __forceinline__ void inc_exact(float x, double sc, double& k, bool& tie) {
+  const double d = (double)x;
+  const double v = d * (d * sc);              // x^2 / u, exact (48 bits)
+  const double kd = (v + kMagic) - kMagic;    // rint; v >= 2^51 makes kd huge (not covered) — fine
+  const double fr = v - kd;
+  tie = __builtin_fabs(fr) == 0.5;
+  k = tie && fr < 0.0 ? kd - 1.0 : kd;
+}
+__device__ __forceinline__ void inc_exact(double x, double sc_unused, double& k, bool& tie, int s) {
+  // x^2 * 2^s as hi + lo without overflow or underflow of the scale: x' = x 2^(s >> 1), x'' = x' 2^(s & 1)
+  const double xa = x * pow2(s >> 1);
+  const double xb = (s & 1) ? xa * 2.0 : xa;
+  const double hi = xa * xb, lo = __fma_rn(xa, xb, -hi);
+  double kd = (hi + kMagic) - kMagic;
+  const double fr = hi - kd;
+  tie = false;
+  if (__builtin_fabs(fr) == 0.5) {
+    if (lo == 0.0) tie = true;
+    else if ((fr > 0.0) == (lo > 0.0)) kd += fr > 0.0 ? 1.0 : -1.0;
+  }
+  k = tie && fr < 0.0 ? kd - 1.0 : kd;
+  (void)sc_unused;
+}
+
+// A lane's map of its steps v[0..n) in order on grid g (exact tie handling): the slow path.
+template <bool W, typename E>
+__device__ __forceinline__ Map lane_map_exact(const E (&v)[kLane], int g) {
+  const int s = Acc<W>::kM - g;
+  const double sc = W ? 0.0 : pow2(s);
+  double se = 0.0, so = 1.0;
+#pragma unroll
+  for (int i = 0; i < kLane; ++i) {
+    double k;
+    bool tie;
+    if constexpr (W) inc_exact((double)v[i], sc, k, tie, s);
+    else inc_exact((float)v[i], sc, k, tie);
+    se += k;
+    so += k;
+    if (tie) {
+      se += odd(se) ? 1.0 : 0.0;
+      so += odd(so) ? 1.0 : 0.0;
+    }
+  }
+  return Map{se, so - 1.0};
+}
+
+// A lane's map on grid g: the fast path (no tie possible: one sum) for fp32 accumulators, the exact one
+// when any lane of the wave might hold a tie (4v or v an integer).
+template <bool W, typename E>
+__device__ __forceinline__ Map lane_map(const E (&v)[kLane], int g) {
+  if constexpr (W) {
+    return lane_map_exact<W>(v, g);
+  } else {
+    const double sc = pow2(23 - g);
+    double K = 0.0;
+    bool maybe = false;
+#pragma unroll
+    for (int i = 0; i < kLane; ++i) {
+      const double d = (double)v[i];
+      const double x2 = d * (d * sc);
+      const double w = x2 * 2.0;
+      K += (x2 + kMagic) - kMagic;
+      maybe |= ((w + kMagic) - kMagic) == w && w != 0.0;  // 2v an integer: a tie is possible
+    }
+    if (__ballot(maybe) == 0ull) return Map{K, K};
+    return maybe ? lane_map_exact<W>(v, g) : Map{K, K};
+  }
+}
+
+// The two candidate maps of phase C (grids g and g - 1) in one pass, fast path for fp32 accumulators.
+template <bool W, typename E>
+__device__ __forceinline__ void lane_maps2(const E (&v)[kLane], int g, Map& m0, Map& m1) {
+  if constexpr (W) {
+    m0 = lane_map_exact<W>(v, g);
+    m1 = g - 1 >= Acc<W>::kGmin ? lane_map_exact<W>(v, g - 1) : Map{__builtin_nan(""), __builtin_nan("")};
+  } else {
+    const double sc = pow2(23 - g);
+    double K0 = 0.0, K1 = 0.0;
+    bool maybe = false;
+#pragma unroll
+    for (int i = 0; i < kLane; ++i) {
+      const double d = (double)v[i];
+      const double x2 = d * (d * sc);
+      const double y = x2 * 2.0, w = x2 * 4.0;
+      K0 += (x2 + kMagic) - kMagic;
+      K1 += (y + kMagic) - kMagic;
+      maybe |= ((w + kMagic) - kMagic) == w && w != 0.0;
+    }
+    if (__ballot(maybe) != 0ull && maybe) {
+      m0 = lane_map_exact<W>(v, g);
+      m1 = lane_map_exact<W>(v, g - 1);
+    } else {
+      m0 = Map{K0, K0};
+      m1 = Map{K1, K1};
+    }
+    if (g - 1 < Acc<W>::kGmin) m1 = Map{__builtin_nan(""), __builtin_nan("")};
+  }
+}
+
+// ---- dtype traits
+template <int DT> struct Dt;
+template <> struct Dt<ADFL_DTYPE_F32> {
+  using S = float;
+  using E = float;
+  static constexpr int NC = 8, VB = 8;
+  static constexpr bool kContig = false, kWide = false;
+  __device__ static E ld(const void* x, int64_t i) { return ((const float*)x)[i]; }
+};
+template <> struct Dt<ADFL_DTYPE_BF16> {
+  using S = uint16_t;
+  using E = float;
+  static constexpr int NC = 8, VB = 16;
+  static constexpr bool kContig = false, kWide = false;
+  __device__ static E ld(const void* x, int64_t i) { return __uint_as_float((uint32_t)((const uint16_t*)x)[i] << 16); }
+};
+template <> struct Dt<ADFL_DTYPE_F16> {
+  using S = uint16_t;
+  using E = float;
+  static constexpr int NC = 1, VB = 1;
+  static constexpr bool kContig = true, kWide = false;
+  __device__ static E ld(const void* x, int64_t i) { return __half2float(__ushort_as_half(((const uint16_t*)x)[i])); }
+};
+template <> struct Dt<ADFL_DTYPE_F64> {
+  using S = double;
+  using E = double;
+  static constexpr int NC = 4, VB = 4;
+  static constexpr bool kContig = false, kWide = true;
+  __device__ static E ld(const void* x, int64_t i) { return ((const double*)x)[i]; }
+};
+
+// A tensor and its chains, from the chunk table.
+struct Tensor {
+  int64_t base;  // first element in the flat buffer
+  int64_t n;
+  int64_t nall;  // chunks in the table (records are chain-major: slot = k * nall + chunk)
+  int first;     // first chunk
+  int nch;       // chunks
+  int tensor;
+};
+__device__ __forceinline__ Tensor tensor_of(const adfl_slq_chunk* chunks, int ci, int64_t nall) {
+  const adfl_slq_chunk ch = chunks[ci];
+  Tensor t;
+  t.nall = nall;
+  t.first = ch.first_chunk;
+  t.nch = ch.nchunks;
+  t.tensor = ch.tensor;
+  t.base = ch.start - (int64_t)(ci - ch.first_chunk) * kChunk;
+  t.n = (int64_t)(ch.nchunks - 1) * kChunk + chunks[ch.first_chunk + ch.nchunks - 1].len;
+  return t;
+}
+
+// fp16: at::parallel_for's split of n elements over `threads`
+struct Split {
+  int64_t nt, cs;
+};
+__device__ __forceinline__ Split split_of(int64_t n, int threads) {
+  int64_t nt = 1;
+  if (n >= kGrain && threads > 1) {
+    nt = (n + kGrain - 1) / kGrain;
+    if (nt > threads) nt = threads;
+  }
+  return Split{nt, (n + nt - 1) / nt};
+}
+
+// Record slot of chunk ci's chain (strided) or piece (fp16) k: chain-major, so a chain's tiles are contiguous.
+__device__ __forceinline__ int64_t slot_of(int64_t ci, int k, int64_t nall) { return (int64_t)k * nall + ci; }
+
+// Chain c's tile t (strided: chunk t; fp16: the t-th chunk the chain touches): its record slot and steps.
+struct Tile {
+  int64_t slot, s0, s1;  // steps [s0, s1) of the chain
+};
+template <int DT>
+__device__ __forceinline__ int64_t chain_len(const Tensor& T, int c, Split sp) {
+  if constexpr (Dt<DT>::kContig) {
+    const int64_t a = (int64_t)c * sp.cs, b = a + sp.cs < T.n ? a + sp.cs : T.n;
+    return b > a ? b - a : 0;
+  } else {
+    return T.n >= Dt<DT>::VB ? (T.n - T.n % Dt<DT>::VB) / Dt<DT>::NC : 0;
+  }
+}
+template <int DT>
+__device__ __forceinline__ int64_t chain_tiles(const Tensor& T, int c, Split sp) {
+  const int64_t L = chain_len<DT>(T, c, sp);
+  if (L == 0) return 0;
+  if constexpr (Dt<DT>::kContig) {
+    const int64_t a = (int64_t)c * sp.cs;
+    return (a + L - 1) / kChunk - a / kChunk + 1;
+  } else {
+    constexpr int spc = kChunk / Dt<DT>::NC;
+    return (L + spc - 1) / spc;
+  }
+}
+template <int DT>
+__device__ __forceinline__ Tile tile_of(const Tensor& T, int c, Split sp, int64_t t) {
+  Tile r;
+  if constexpr (Dt<DT>::kContig) {
+    const int64_t a = (int64_t)c * sp.cs, b = a + sp.cs < T.n ? a + sp.cs : T.n;
+    const int64_t kc = a / kChunk + t;
+    const int64_t lo = kc * kChunk > a ? kc * kChunk : a, hi = (kc + 1) * kChunk < b ? (kc + 1) * kChunk : b;
+    r.slot = slot_of(T.first + kc, a > kc * kChunk ? 1 : 0, T.nall);
+    r.s0 = lo - a;
+    r.s1 = hi - a;
+  } else {
+    constexpr int spc = kChunk / Dt<DT>::NC;
+    const int64_t L = chain_len<DT>(T, c, sp);
+    r.slot = slot_of(T.first + t, c, T.nall);
+    r.s0 = t * spc;
+    r.s1 = (t + 1) * spc < L ? (t + 1) * spc : L;
+  }
+  return r;
+}
+template <int DT>
+__device__ __forceinline__ int64_t elem_of(const Tensor& T, int c, Split sp, int64_t s) {
+  if constexpr (Dt<DT>::kContig) return T.base + (int64_t)c * sp.cs + s;
+  else return T.base + s * Dt<DT>::NC + c;
+}
+
+// ---- records
+// Per chunk and chain (strided) or piece (fp16) — a "tile" of a chain: the predicted binade g (phase B) and
+// the tile's totals on g and g - 1 (phase C): k0 / k1 as fp32 integers (exact below 2^24; +inf where a step
+// is too large for the fast path — the tile is then resolved in detail), or, when the tile may hold a tie
+// (flag kSide), its exact maps in the side table (double4 {e0, o0, e1, o1}).
+struct Rec {
+  uint32_t w0, w1;
+};
+static_assert(sizeof(Rec) == 8, "record layout");
+constexpr uint32_t kSide = 1u;      // exact maps in the side table
+constexpr uint32_t kPad = 2u;       // phase D: past the chain's end (identity)
+constexpr uint32_t kNoK = 0xffffffu;  // a total of 2^24 - 1 or more (not covered)
+// fp32 accumulators: w0 = k0 | flags << 24, w1 = k1 | (g + 128) << 24; fp64 ones: w0 = flags << 24, w1 = g + 2048
+template <bool W> __device__ __forceinline__ Rec make_rec(double k0, double k1, int g, uint32_t flags) {
+  if constexpr (W) {
+    return Rec{flags << 24, (uint32_t)(g + 2048)};
+  } else {
+    const uint32_t a = k0 < (double)kNoK ? (uint32_t)k0 : kNoK, b = k1 < (double)kNoK ? (uint32_t)k1 : kNoK;
+    return Rec{a | (flags << 24), b | ((uint32_t)(g + 128) << 24)};
+  }
+}
+template <bool W> __device__ __forceinline__ int rec_g(Rec r) {
+  return W ? (int)(r.w1 & 0xfffu) - 2048 : (int)(r.w1 >> 24) - 128;
+}
+__device__ __forceinline__ uint32_t rec_flags(Rec r) { return r.w0 >> 24; }
+__device__ __forceinline__ double rec_k(Rec r, int j) {  // j = 0 / 1: the total on g / g - 1 (fp32 accumulators)
+  const uint32_t k = (j ? r.w1 : r.w0) & kNoK;
+  return k == kNoK ? __builtin_inf() : (double)k;
+}
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// A chunk's elements as 16-byte vectors from the aligned block holding its first element: element e of the
+// chunk is position (e + delta) % EPV of vector (e + delta) / EPV (tensors of compact buckets start anywhere).
+template <int DT> struct View {
+  using St = typename Dt<DT>::S;
+  static constexpr int EPV = 16 / (int)sizeof(St);
+  static constexpr int NV = (kChunk / EPV + 1 + 255) / 256;  // vectors per thread (256 threads)
+  const u32x4* vb;
+  int delta, nvec;
+  __device__ View(const void* x, int64_t first, int lim) {
+    const uintptr_t a = (uintptr_t)((const St*)x + first);
+    delta = (int)((a & 15) / sizeof(St));
+    vb = (const u32x4*)(a - (a & 15));
+    nvec = (delta + lim + EPV - 1) / EPV;
+  }
+  __device__ static typename Dt<DT>::E elem(const u32x4& r, int p) {
+    St el[EPV];
+    __builtin_memcpy(el, &r, 16);
+    if constexpr (DT == ADFL_DTYPE_F32 || DT == ADFL_DTYPE_F64) return el[p];
+    else if constexpr (DT == ADFL_DTYPE_BF16) return __uint_as_float((uint32_t)el[p] << 16);
+    else return __half2float(__ushort_as_half(el[p]));
+  }
+};
+
+// chunk geometry shared by phases A and C
+struct ChunkGeo {
+  int kc, len, lim, bnd;  // chunk index in the tensor, elements, elements that are chain steps, fp16 piece edge
+  int64_t c0e;
+};
+template <int DT>
+__device__ __forceinline__ ChunkGeo geo_of(const Tensor& T, int ci, Split sp) {
+  ChunkGeo g;
+  g.kc = ci - T.first;
+  g.c0e = (int64_t)g.kc * kChunk;
+  g.len = (int)(T.n - g.c0e < kChunk ? T.n - g.c0e : kChunk);
+  g.bnd = kChunk;
+  if constexpr (Dt<DT>::kContig) {
+    g.lim = g.len;
+    const int64_t b = (g.c0e / sp.cs + 1) * sp.cs - g.c0e;
+    g.bnd = b < g.len ? (int)b : kChunk;
+  } else {
+    const int64_t nv = T.n - T.n % Dt<DT>::VB;
+    g.lim = (int)(nv - g.c0e < g.len ? nv - g.c0e : g.len);
+  }
+  return g;
+}
+
+// ---- phase A: per chunk and chain (piece), the fp64 sum of x^2; also tfirst[t] = t's first chunk
+template <int DT>
+__global__ __launch_bounds__(256) void k_tn_sums(const void* __restrict__ x, const adfl_slq_chunk* __restrict__ chunks, int64_t nall,
+                                                 int threads, int* __restrict__ tfirst, double* __restrict__ S) {
+  using D = Dt<DT>;
+  using V = View<DT>;
+  constexpr int EPV = V::EPV, NV = V::NV;
+  __shared__ double s_red[4][8];
+  const int ci = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const Tensor T = tensor_of(chunks, ci, nall);
+  if (tid == 0 && ci == T.first) tfirst[T.tensor] = ci;
+  if (T.n <= kShortMax) return;
+  const Split sp = split_of(T.n, threads);
+  const ChunkGeo G = geo_of<DT>(T, ci, sp);
+  if (G.lim <= 0) return;  // a chunk of tail elements only: no tile
+  const V v(x, T.base + G.c0e, G.lim);
+  u32x4 r[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int f = tid + 256 * i;
+    r[i] = f < v.nvec ? v.vb[f] : u32x4{0u, 0u, 0u, 0u};
+  }
+  double acc[EPV], acc1 = 0.0;  // strided: per vector position; fp16: acc[0] / acc1 = piece 0 / 1
+#pragma unroll
+  for (int p = 0; p < EPV; ++p) acc[p] = 0.0;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int f = tid + 256 * i;
+#pragma unroll
+    for (int p = 0; p < EPV; ++p) {
+      const int e = f * EPV + p - v.delta;
+      const double d = (e >= 0 && e < G.lim) ? (double)V::elem(r[i], p) : 0.0;
+      if constexpr (D::kContig) {
+        if (e < G.bnd) acc[0] = __fma_rn(d, d, acc[0]);
+        else acc1 = __fma_rn(d, d, acc1);
+      } else {
+        acc[p] = __fma_rn(d, d, acc[p]);
+      }
+    }
+  }
+  if constexpr (D::kContig) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      acc[0] += __shfl_xor(acc[0], o, 64);
+      acc1 += __shfl_xor(acc1, o, 64);
+    }
+    if (lane == 0) {
+      s_red[wave][0] = acc[0];
+      s_red[wave][1] = acc1;
+    }
+    __syncthreads();
+    if (tid < 2 && (tid == 0 || G.bnd < G.len))
+      S[slot_of(ci, tid, T.nall)] = s_red[0][tid] + s_red[1][tid] + s_red[2][tid] + s_red[3][tid];
+  } else {
+    // lanes whose positions map to the same chains: tid % (NC / EPV) (NC / EPV = 2, or 1 for bf16)
+    constexpr int kCls = D::NC / EPV;
+#pragma unroll
+    for (int p = 0; p < EPV; ++p)
+#pragma unroll
+      for (int o = kCls; o < 64; o <<= 1) acc[p] += __shfl_xor(acc[p], o, 64);
+    if (lane < kCls) {
+#pragma unroll
+      for (int p = 0; p < EPV; ++p) {
+        const int c = ((lane * EPV + p - v.delta) % D::NC + D::NC) % D::NC;
+        s_red[wave][c] = acc[p];
+      }
+    }
+    __syncthreads();
+    if (tid < D::NC) S[slot_of(ci, tid, T.nall)] = s_red[0][tid] + s_red[1][tid] + s_red[2][tid] + s_red[3][tid];
+  }
+}
+
+// ---- phase B: per chain, the exclusive prefix of S over its tiles -> each tile's predicted binade (rec.g)
+// One 1024-thread block per chain (blockIdx.y strides the chains of fp16's split), 16 consecutive tiles per
+// thread held in registers: one round of loads, a block scan, one round of stores per 16384 tiles.
+constexpr int kGridThreads = 1024, kGridPer = 16;
+template <int DT>
+__global__ __launch_bounds__(kGridThreads) void k_tn_grids(const adfl_slq_chunk* __restrict__ chunks, int64_t nall,
+                                                           const int* __restrict__ tfirst, int threads,
+                                                           const double* __restrict__ S, Rec* __restrict__ recs) {
+  using D = Dt<DT>;
+  __shared__ double s_sum[kGridThreads / 64];
+  __shared__ double s_carry;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const Tensor T = tensor_of(chunks, tfirst[blockIdx.x], nall);
+  if (T.n <= kShortMax) return;
+  const Split sp = split_of(T.n, threads);
+  const int nchains = D::kContig ? (int)sp.nt : D::NC;
+  for (int c = blockIdx.y; c < nchains; c += gridDim.y) {
+    const int64_t nt = chain_tiles<DT>(T, c, sp);
+    double carry = 0.0;
+    for (int64_t base = 0; base < nt; base += (int64_t)kGridThreads * kGridPer) {
+      const int64_t t0 = base + (int64_t)tid * kGridPer;
+      double y[kGridPer];
+#pragma unroll
+      for (int j = 0; j < kGridPer; ++j) y[j] = t0 + j < nt ? S[tile_of<DT>(T, c, sp, t0 + j).slot] : 0.0;
+      double a = 0.0;
+#pragma unroll
+      for (int j = 0; j < kGridPer; ++j) a += y[j];
+      double incl = a;  // inclusive scan over the block: waves, then wave totals
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const double z = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += z;
+      }
+      if (lane == 63) s_sum[wave] = incl;
+      __syncthreads();
+      if (tid == 0) {
+        double r = carry;
+        for (int w = 0; w < kGridThreads / 64; ++w) {
+          const double v = s_sum[w];
+          s_sum[w] = r;
+          r += v;
+        }
+        s_carry = r;
+      }
+      __syncthreads();
+      double P = s_sum[wave] + incl - a;
+#pragma unroll
+      for (int j = 0; j < kGridPer; ++j) {
+        if (t0 + j < nt) recs[tile_of<DT>(T, c, sp, t0 + j).slot] = make_rec<D::kWide>(0.0, 0.0, grid_pred<D::kWide>(P), 0u);
+        P += y[j];
+      }
+      carry = s_carry;
+      __syncthreads();
+    }
+  }
+}
+
+// ---- phase C: per chunk and chain (piece), the totals on the predicted binades g and g - 1
+// Fast path, order-free: with hi = RN(x^2 / u) in the accumulator's type, k = rint(hi) is R(x^2 / u)
+// unless hi - k = +-1/2 (where the exact value decides, and a tie is possible) — and on g - 1, R(2 x^2 / u)
+// = 2 k + rint(2 (hi - k)), exact unless hi - k = +-1/4. A chunk where any lane meets one of those is listed
+// for k_tn_maps_exact: staged chain-major through LDS, each lane's 16 steps composed in order as maps.
+template <int DT>
+__device__ __forceinline__ void load_chunk(const View<DT>& v, int tid, u32x4 (&r)[View<DT>::NV]) {
+#pragma unroll
+  for (int i = 0; i < View<DT>::NV; ++i) {
+    const int f = tid + 256 * i;
+    r[i] = f < v.nvec ? v.vb[f] : u32x4{0u, 0u, 0u, 0u};
+  }
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void k_tn_maps(const void* __restrict__ x, const adfl_slq_chunk* __restrict__ chunks, int64_t nall,
+                                                 int threads, Rec* __restrict__ recs, double4* __restrict__ maps,
+                                                 int* __restrict__ exact_list) {
+  using D = Dt<DT>;
+  using V = View<DT>;
+  constexpr bool W = D::kWide;
+  using A_t = typename Acc<W>::T;
+  constexpr int EPV = V::EPV, NV = V::NV;
+  constexpr A_t kM = W ? (A_t)6755399441055744.0 : (A_t)12582912.0f;   // 1.5 * 2^52 / 1.5 * 2^23
+  constexpr A_t kBig = W ? (A_t)0x1p51 : (A_t)0x1p22;                   // hi at or above: rint by kM fails
+  __shared__ A_t s_k[4][8][3];
+  __shared__ int s_g[8];
+  const int ci = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const Tensor T = tensor_of(chunks, ci, nall);
+  if (T.n <= kShortMax) return;
+  const Split sp = split_of(T.n, threads);
+  const ChunkGeo G = geo_of<DT>(T, ci, sp);
+  if (G.lim <= 0) return;
+  const int npieces = D::kContig ? (G.bnd < G.len ? 2 : 1) : D::NC;
+  if (tid < npieces) s_g[tid] = rec_g<W>(recs[slot_of(ci, tid, T.nall)]);
+  const V v(x, T.base + G.c0e, G.lim);
+  u32x4 r[NV];
+  load_chunk<DT>(v, tid, r);
+  __syncthreads();
+  // per position (strided) or piece (fp16): scale of x so hi = x^2 / u on g: xs = x 2^(s >> 1), hi = xs xs (2)
+  constexpr int kP = D::kContig ? 2 : EPV;
+  A_t sa[kP], sb[kP];
+#pragma unroll
+  for (int p = 0; p < kP; ++p) {
+    const int c = D::kContig ? (p < npieces ? p : 0) : ((tid * EPV + p - v.delta) % D::NC + D::NC) % D::NC;
+    const int s = Acc<W>::kM - s_g[c];
+    sa[p] = (A_t)pow2(s >> 1);
+    sb[p] = (s & 1) ? (A_t)2 : (A_t)1;
+  }
+  A_t K0[kP], Dl[kP], mx[kP];
+#pragma unroll
+  for (int p = 0; p < kP; ++p) K0[p] = Dl[p] = mx[p] = (A_t)0;
+  bool slow = false;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int f = tid + 256 * i;
+#pragma unroll
+    for (int p = 0; p < EPV; ++p) {
+      const int e = f * EPV + p - v.delta;
+      const A_t xv = (e >= 0 && e < G.lim) ? (A_t)V::elem(r[i], p) : (A_t)0;
+      const int q = D::kContig ? (e < G.bnd ? 0 : 1) : p;
+      const A_t xs = xv * sa[q];
+      const A_t hi = xs * xs * sb[q];
+      const A_t k = (hi + kM) - kM;
+      const A_t rr = hi - k;
+      const A_t ar = __builtin_fabs(rr);
+      K0[q] += k;
+      Dl[q] += rr > (A_t)0.25 ? (A_t)1 : (rr < (A_t)-0.25 ? (A_t)-1 : (A_t)0);
+      mx[q] = (hi == hi) ? __builtin_fmax(mx[q], hi) : (A_t)__builtin_inf();  // NaN: not covered
+      slow |= (ar == (A_t)0.5) | (ar == (A_t)0.25);
+    }
+  }
+  if (__syncthreads_or(slow)) {
+    if (tid == 0) exact_list[atomicAdd(exact_list - 1, 1)] = ci;  // the count sits just before the list
+    return;
+  }
+  if constexpr (D::kContig) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        K0[p] += __shfl_xor(K0[p], o, 64);
+        Dl[p] += __shfl_xor(Dl[p], o, 64);
+        mx[p] = __builtin_fmax(mx[p], __shfl_xor(mx[p], o, 64));
+      }
+    if (lane < 2) {
+      s_k[wave][lane][0] = lane ? K0[1] : K0[0];
+      s_k[wave][lane][1] = lane ? Dl[1] : Dl[0];
+      s_k[wave][lane][2] = lane ? mx[1] : mx[0];
+    }
+  } else {
+    constexpr int kCls = D::NC / EPV;
+#pragma unroll
+    for (int p = 0; p < EPV; ++p)
+#pragma unroll
+      for (int o = kCls; o < 64; o <<= 1) {
+        K0[p] += __shfl_xor(K0[p], o, 64);
+        Dl[p] += __shfl_xor(Dl[p], o, 64);
+        mx[p] = __builtin_fmax(mx[p], __shfl_xor(mx[p], o, 64));
+      }
+    if (lane < kCls) {
+#pragma unroll
+      for (int p = 0; p < EPV; ++p) {
+        const int c = ((lane * EPV + p - v.delta) % D::NC + D::NC) % D::NC;
+        s_k[wave][c][0] = K0[p];
+        s_k[wave][c][1] = Dl[p];
+        s_k[wave][c][2] = mx[p];
+      }
+    }
+  }
+  __syncthreads();
+  if (tid < npieces) {
+    A_t k0 = 0, dl = 0, m = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      k0 += s_k[w][tid][0];
+      dl += s_k[w][tid][1];
+      m = __builtin_fmax(m, s_k[w][tid][2]);
+    }
+    const int g = s_g[tid];
+    const A_t k1 = 2 * k0 + dl;
+    const double inf = __builtin_inf();
+    const double e0 = m < kBig ? (double)k0 : inf;
+    const double e1 = (m < kBig && g - 1 >= Acc<W>::kGmin) ? (double)k1 : inf;
+    const int64_t slot = slot_of(ci, tid, T.nall);
+    if constexpr (W) {
+      maps[slot] = make_double4(e0, e0, e1, e1);
+      recs[slot] = make_rec<W>(0.0, 0.0, g, kSide);
+    } else {
+      recs[slot] = make_rec<W>(e0, e1, g, 0u);
+    }
+  }
+}
+
+// The listed chunks, exactly: chain-major staging (16 steps per lane block, +1 pad), maps composed in order.
+template <int DT>
+__global__ __launch_bounds__(256) void k_tn_maps_exact(const void* __restrict__ x, const adfl_slq_chunk* __restrict__ chunks, int64_t nall,
+                                                       int threads, Rec* __restrict__ recs, double4* __restrict__ maps,
+                                                       const int* __restrict__ exact_list) {
+  using D = Dt<DT>;
+  using V = View<DT>;
+  using E = typename D::E;
+  constexpr bool W = D::kWide;
+  constexpr int EPV = V::EPV, NV = V::NV;
+  constexpr int kLS = kLane + 1;
+  __shared__ E st[8 * 64 * kLS];  // 8 rows of 1024 steps (strided: chain-major; fp16: the chunk in order)
+  __shared__ double s_m[4][2][4];
+  __shared__ int s_g[8];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int count = exact_list[-1];
+  for (int li = blockIdx.x; li < count; li += gridDim.x) {
+    const int ci = exact_list[li];
+    const Tensor T = tensor_of(chunks, ci, nall);
+    const Split sp = split_of(T.n, threads);
+    const ChunkGeo G = geo_of<DT>(T, ci, sp);
+    const int npieces = D::kContig ? (G.bnd < G.len ? 2 : 1) : D::NC;
+    if (tid < npieces) s_g[tid] = rec_g<W>(recs[slot_of(ci, tid, T.nall)]);
+    const V v(x, T.base + G.c0e, G.lim);
+    u32x4 r[NV];
+    load_chunk<DT>(v, tid, r);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int f = tid + 256 * i;
+#pragma unroll
+      for (int p = 0; p < EPV; ++p) {
+        const int e = f * EPV + p - v.delta;
+        if (e >= 0 && e < G.lim) {
+          int row, sl;
+          if constexpr (D::kContig) {
+            row = e / kSeg;
+            sl = e % kSeg;
+          } else {  // steps per chain in a chunk: 1024 (NC 8) or 2048 (NC 4)
+            const int c = e % D::NC, s = e / D::NC;
+            row = D::NC == 8 ? c : c * 2 + s / kSeg;
+            sl = s % kSeg;
+          }
+          st[row * 64 * kLS + (sl / kLane) * kLS + sl % kLane] = V::elem(r[i], p);
+        }
+      }
+    }
+    __syncthreads();
+    // fp16: wave w composes rows 2w, 2w + 1 (elements [2048 w, 2048 w + 2048)) for each piece; strided: the
+    // rows w and w + 4 (fp32 / bf16: chains w, w + 4; fp64: halves of chains)
+    Map acc0[2] = {Map{0.0, 0.0}, Map{0.0, 0.0}}, acc1[2] = {Map{0.0, 0.0}, Map{0.0, 0.0}};
+    for (int h = 0; h < 2; ++h) {
+      const int row = D::kContig ? wave * 2 + h : wave + 4 * h;
+      E w[kLane];
+#pragma unroll
+      for (int i = 0; i < kLane; ++i) {
+        const int e = row * kSeg + lane * kLane + i;  // fp16: the chunk element; strided: the row's step
+        w[i] = (!D::kContig || e < G.lim) ? st[row * 64 * kLS + lane * kLS + i] : (E)0;
+      }
+      if constexpr (D::kContig) {
+        for (int pc = 0; pc < 2; ++pc) {  // steps outside a piece are zeros (identity)
+          E z[kLane];
+#pragma unroll
+          for (int i = 0; i < kLane; ++i) {
+            const int e = row * kSeg + lane * kLane + i;
+            z[i] = (pc == 0 ? e < G.bnd : e >= G.bnd) ? w[i] : (E)0;
+          }
+          const int g = s_g[pc < npieces ? pc : 0];
+          acc0[pc] = compose(acc0[pc], wave_compose(lane_map_exact<W>(z, g), lane));
+          acc1[pc] = compose(acc1[pc], wave_compose(lane_map_exact<W>(z, g - 1), lane));
+        }
+      } else {
+        const int g = s_g[D::NC == 8 ? row : row / 2];
+        // rows past the chunk's steps are zeros: LDS left from an earlier chunk must not count
+        const int c = D::NC == 8 ? row : row / 2, s0 = (D::NC == 8 ? 0 : (row % 2) * kSeg);
+#pragma unroll
+        for (int i = 0; i < kLane; ++i) {
+          const int e = (s0 + lane * kLane + i) * D::NC + c;
+          if (e >= G.lim) w[i] = (E)0;
+        }
+        const Map m0 = wave_compose(lane_map_exact<W>(w, g), lane);
+        const Map m1 = wave_compose(lane_map_exact<W>(w, g - 1), lane);
+        if (lane == 0) {
+          s_m[wave][h][0] = m0.e;
+          s_m[wave][h][1] = m0.o;
+          s_m[wave][h][2] = m1.e;
+          s_m[wave][h][3] = m1.o;
+        }
+      }
+    }
+    if constexpr (D::kContig) {
+      if (lane == 0)
+        for (int pc = 0; pc < 2; ++pc) {
+          s_m[wave][pc][0] = acc0[pc].e;
+          s_m[wave][pc][1] = acc0[pc].o;
+          s_m[wave][pc][2] = acc1[pc].e;
+          s_m[wave][pc][3] = acc1[pc].o;
+        }
+    }
+    __syncthreads();
+    if (tid < npieces) {
+      Map a0{0.0, 0.0}, a1{0.0, 0.0};
+      if constexpr (D::kContig) {
+        for (int w = 0; w < 4; ++w) {
+          a0 = compose(a0, Map{s_m[w][tid][0], s_m[w][tid][1]});
+          a1 = compose(a1, Map{s_m[w][tid][2], s_m[w][tid][3]});
+        }
+      } else if (D::NC == 8) {  // chain c = row c: wave c % 4, half c / 4
+        a0 = Map{s_m[tid % 4][tid / 4][0], s_m[tid % 4][tid / 4][1]};
+        a1 = Map{s_m[tid % 4][tid / 4][2], s_m[tid % 4][tid / 4][3]};
+      } else {  // NC 4: chain c = rows 2c, 2c + 1
+        const int r0 = 2 * tid, r1 = 2 * tid + 1;
+        a0 = compose(Map{s_m[r0 % 4][r0 / 4][0], s_m[r0 % 4][r0 / 4][1]}, Map{s_m[r1 % 4][r1 / 4][0], s_m[r1 % 4][r1 / 4][1]});
+        a1 = compose(Map{s_m[r0 % 4][r0 / 4][2], s_m[r0 % 4][r0 / 4][3]}, Map{s_m[r1 % 4][r1 / 4][2], s_m[r1 % 4][r1 / 4][3]});
+      }
+      const int g = s_g[tid];
+      if (g - 1 < Acc<W>::kGmin) a1 = Map{__builtin_inf(), __builtin_inf()};
+      const int64_t slot = slot_of(ci, tid, T.nall);
+      maps[slot] = make_double4(a0.e, a0.o, a1.e, a1.o);
+      recs[slot] = make_rec<W>(0.0, 0.0, g, kSide);
+    }
+    __syncthreads();
+  }
+}
+
+// ---- phase C2: window summaries. A window is kWinTiles consecutive tiles of a chain; its summary is the
+// composition of its tiles' maps on G = gw (every tile predicted on gw) and on gw - 1 (every tile predicted on
+// gw or gw - 1), gw the window's highest predicted binade; a map that does not exist is +inf. One wave per
+// window; grid (tensors, 8, 8): blockIdx.y strides chains, blockIdx.z and the wave stride windows.
+template <int DT>
+__global__ __launch_bounds__(256) void k_tn_windows(const adfl_slq_chunk* __restrict__ chunks, int64_t nall, const int* __restrict__ tfirst,
+                                                    int threads, const Rec* __restrict__ recs, const double4* __restrict__ maps,
+                                                    int* __restrict__ wing, double4* __restrict__ winmaps) {
+  using D = Dt<DT>;
+  constexpr bool W = D::kWide;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const Tensor T = tensor_of(chunks, tfirst[blockIdx.x], nall);
+  if (T.n <= kShortMax) return;
+  const Split sp = split_of(T.n, threads);
+  const int nchains = D::kContig ? (int)sp.nt : D::NC;
+  const int wstride = gridDim.z * 4;
+  for (int c = blockIdx.y; c < nchains; c += gridDim.y) {
+    const int64_t nt = chain_tiles<DT>(T, c, sp);
+    const int64_t nw = (nt + kWinTiles - 1) / kWinTiles;
+    for (int64_t w = blockIdx.z * 4 + wave; w < nw; w += wstride) {
+      const int64_t w0 = w * kWinTiles;
+      Rec r[kTPL];
+      int gmax = -0x7fffffff;
+#pragma unroll
+      for (int k = 0; k < kTPL; ++k) {
+        const int64_t t = w0 + lane * kTPL + k;
+        r[k] = t < nt ? recs[tile_of<DT>(T, c, sp, t).slot] : Rec{kPad << 24, 0u};
+        if (t < nt) gmax = max(gmax, rec_g<W>(r[k]));
+      }
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) gmax = max(gmax, __shfl_xor(gmax, o, 64));
+      Map a{0.0, 0.0}, b{0.0, 0.0};
+#pragma unroll
+      for (int k = 0; k < kTPL; ++k) {
+        const Rec q = r[k];
+        const uint32_t fl = rec_flags(q);
+        if (fl & kPad) continue;
+        const int g = rec_g<W>(q);
+        Map m0, m1;  // the tile's maps on g and g - 1
+        if (fl & kSide) {
+          const double4 m = maps[tile_of<DT>(T, c, sp, w0 + lane * kTPL + k).slot];
+          m0 = Map{m.x, m.y};
+          m1 = Map{m.z, m.w};
+        } else {
+          const double k0 = rec_k(q, 0), k1 = rec_k(q, 1);
+          m0 = Map{k0, k0};
+          m1 = Map{k1, k1};
+        }
+        const Map inf{__builtin_inf(), __builtin_inf()};
+        a = compose(a, g == gmax ? m0 : inf);                        // on gmax: j = g - gmax must be 0
+        b = compose(b, g == gmax ? m1 : (g == gmax - 1 ? m0 : inf));  // on gmax - 1: j = 1 or 0
+      }
+      a = wave_compose(a, lane);
+      b = wave_compose(b, lane);
+      if (lane == 0) {
+        const int64_t slot = tile_of<DT>(T, c, sp, w0).slot;
+        wing[slot] = gmax;
+        winmaps[slot] = make_double4(a.e, a.o, b.e, b.o);
+      }
+    }
+  }
+}
+
+// ---- phase D
+// A segment (<= 1024 steps, lane l holding steps 16 l .. 16 l + 15) run from the exact accumulator acc.
+template <int DT>
+__device__ __forceinline__ typename Acc<Dt<DT>::kWide>::T resolve_segment(const typename Dt<DT>::E (&v)[kLane],
+                                                                           typename Acc<Dt<DT>::kWide>::T acc, int lane) {
+  constexpr bool W = Dt<DT>::kWide;
+  using A_t = typename Acc<W>::T;
+  int start = 0;
+  for (;;) {
+    if (!__builtin_isfinite(acc)) {  // inf stays inf unless a NaN follows; NaN stays NaN
+      bool nan = false;
+#pragma unroll
+      for (int i = 0; i < kLane; ++i) nan |= __builtin_isnan(v[i]);
+      if (__ballot(nan && lane >= start)) acc = (A_t)__builtin_nan("");
+      return acc;
+    }
+    TN_STAT(2, 1);
+    const int G = grid_of(acc);
+    const double A = a_of(acc);
+    Map m = lane_map<W>(v, G);  // (wave-wide: it ballots)
+    if (lane < start) m = Map{0.0, 0.0};
+    const Map ex = wave_excl(m, lane);
+    const double Al = apply(ex, A);
+    const double out = apply(m, Al);
+    const bool bad = lane >= start && !(out < Acc<W>::kTop);
+    const unsigned long long ball = __ballot(bad);
+    if (ball == 0ull) return rebuild<W>(__shfl(out, 63, 64), G);
+    const int ls = __builtin_ctzll(ball);
+    const double As = __shfl(Al, ls, 64);
+    A_t a = rebuild<W>(As, G);
+    if (lane == ls) {
+#pragma unroll
+      for (int i = 0; i < kLane; ++i) a = fma_t(v[i], v[i], a);
+    }
+    acc = __shfl(a, ls, 64);
+    start = ls + 1;
+    if (start == 64) return acc;
+  }
+}
+
+template <int DT>
+__device__ __forceinline__ void load_seg(const void* x, const Tensor& T, int c, Split sp, int64_t s0, int64_t s1,
+                                         int lane, typename Dt<DT>::E (&v)[kLane]) {
+#pragma unroll
+  for (int i = 0; i < kLane; ++i) {
+    const int64_t s = s0 + lane * kLane + i;
+    v[i] = s < s1 ? Dt<DT>::ld(x, elem_of<DT>(T, c, sp, s)) : (typename Dt<DT>::E)0;
+  }
+}
+
+template <int DT>
+__device__ typename Acc<Dt<DT>::kWide>::T resolve_tile(const void* x, const Tensor& T, int c, Split sp, const Tile& tl,
+                                                       typename Acc<Dt<DT>::kWide>::T acc, int lane) {
+  typename Dt<DT>::E v[kLane];
+  TN_STAT(1, 1);
+#ifdef ADFL_TN_STATS
+  const long long c0 = clock64();
+#endif
+  for (int64_t s0 = tl.s0; s0 < tl.s1; s0 += kSeg) {
+    load_seg<DT>(x, T, c, sp, s0, s0 + kSeg < tl.s1 ? s0 + kSeg : tl.s1, lane, v);
+    acc = resolve_segment<DT>(v, acc, lane);
+  }
+#ifdef ADFL_TN_STATS
+  TN_STAT(4, clock64() - c0);
+#endif
+  return acc;
+}
+
+// One window (kWinTiles tiles of chain c from tile w0; lane l holds tiles l * kTPL ..) from the exact acc:
+// scan the tiles' maps on acc's binade; the first tile not covered (a crossing, a miss of the predictor, a
+// large step) is resolved in detail; and on from the tile after it.
+template <int DT>
+__device__ typename Acc<Dt<DT>::kWide>::T resolve_window(const void* x, const Tensor& T, int c, Split sp,
+                                                         const double* S, const Rec* recs, const double4* maps,
+                                                         int64_t w0, int64_t nt, typename Acc<Dt<DT>::kWide>::T acc,
+                                                         int lane) {
+  constexpr bool W = Dt<DT>::kWide;
+  using A_t = typename Acc<W>::T;
+  Rec r[kTPL];
+#pragma unroll
+  for (int k = 0; k < kTPL; ++k) {
+    const int64_t t = w0 + lane * kTPL + k;
+    r[k] = t < nt ? recs[tile_of<DT>(T, c, sp, t).slot] : Rec{kPad << 24, 0u};
+  }
+  int start = 0;  // window tiles before it are done
+  const int wlen = nt - w0 < kWinTiles ? (int)(nt - w0) : kWinTiles;
+  while (start < wlen) {
+    if (!__builtin_isfinite(acc)) {  // inf stays inf unless a NaN follows: the remaining tiles' sums say
+      bool nan = false;
+      for (int64_t u = w0 + start + lane; u < nt; u += 64) nan |= __builtin_isnan(S[tile_of<DT>(T, c, sp, u).slot]);
+      if (__ballot(nan)) acc = (A_t)__builtin_nan("");
+      return acc;
+    }
+    const int G = grid_of(acc);
+    const double A = a_of(acc);
+    bool side = false;
+#pragma unroll
+    for (int k = 0; k < kTPL; ++k) side |= (rec_flags(r[k]) & kSide) && lane * kTPL + k >= start;
+    const bool any_side = __ballot(side) != 0ull;
+    const auto tile_map = [&](int k) -> Map {
+      const Rec q = r[k];
+      const uint32_t fl = rec_flags(q);
+      if ((fl & kPad) || lane * kTPL + k < start) return Map{0.0, 0.0};
+      const int j = rec_g<W>(q) - G;
+      if (j != 0 && j != 1) return Map{__builtin_inf(), __builtin_inf()};
+      if (fl & kSide) {
+        const double4 m = maps[tile_of<DT>(T, c, sp, w0 + lane * kTPL + k).slot];
+        return j == 0 ? Map{m.x, m.y} : Map{m.z, m.w};
+      }
+      const double K = rec_k(q, j);
+      return Map{K, K};
+    };
+    double Al, out;
+    if (!any_side) {
+      double K = 0.0;
+#pragma unroll
+      for (int k = 0; k < kTPL; ++k) K += tile_map(k).e;
+      Al = A + wave_excl_sum(K, lane);
+      out = Al + K;
+    } else {
+      Map m{0.0, 0.0};
+#pragma unroll
+      for (int k = 0; k < kTPL; ++k) m = compose(m, tile_map(k));
+      Al = apply(wave_excl(m, lane), A);
+      out = apply(m, Al);
+    }
+    const unsigned long long ball = __ballot(!(out < Acc<W>::kTop));
+    if (ball == 0ull) return rebuild<W>(__shfl(out, 63, 64), G);
+    // the first tile not covered: each lane's first tile whose map leaves the binade from its Al
+    int kb = kTPL;
+    double Ab = Al;
+#pragma unroll
+    for (int k = 0; k < kTPL; ++k) {
+      if (kb == kTPL) {
+        const double nxt = apply(tile_map(k), Ab);
+        if (!(nxt < Acc<W>::kTop)) kb = k;
+        else Ab = nxt;
+      }
+    }
+    const int ls = __builtin_ctzll(ball);
+    const int tb = ls * kTPL + __shfl(kb, ls, 64);
+    acc = rebuild<W>(__shfl(Ab, ls, 64), G);
+    acc = resolve_tile<DT>(x, T, c, sp, tile_of<DT>(T, c, sp, w0 + tb), acc, lane);
+    start = tb + 1;
+  }
+  return acc;
+}
+
+template <int DT>
+__device__ typename Acc<Dt<DT>::kWide>::T resolve_chain(const void* x, const Tensor& T, int c, Split sp,
+                                                        const double* S, const Rec* recs, const double4* maps,
+                                                        const int* wing, const double4* winmaps, bool use_recs,
+                                                        int lane) {
+  constexpr bool W = Dt<DT>::kWide;
+  using A_t = typename Acc<W>::T;
+  const int64_t nt = chain_tiles<DT>(T, c, sp);
+  A_t acc = (A_t)0;
+  if (!use_recs) {
+    for (int64_t t = 0; t < nt; ++t) acc = resolve_tile<DT>(x, T, c, sp, tile_of<DT>(T, c, sp, t), acc, lane);
+    return acc;
+  }
+  // Windows 64 at a time (lane l: window wb + l), each as its summary map on acc's binade (phase C2); the
+  // first window not covered is resolved tile by tile (resolve_window), then on from the window after it.
+  const int64_t nw = (nt + kWinTiles - 1) / kWinTiles;
+  for (int64_t wb = 0; wb < nw; wb += 64) {
+    const int64_t w = wb + lane;
+    const bool valid = w < nw;
+    int gw = 0;
+    double4 wm = make_double4(0.0, 0.0, 0.0, 0.0);
+    if (valid) {
+      const int64_t slot = tile_of<DT>(T, c, sp, w * kWinTiles).slot;
+      gw = wing[slot];
+      wm = winmaps[slot];
+    }
+    int wstart = 0;
+    const int wlen = nw - wb < 64 ? (int)(nw - wb) : 64;
+    while (wstart < wlen) {
+      if (!__builtin_isfinite(acc)) {  // inf stays inf unless a NaN follows: the remaining tiles' sums say
+        bool nan = false;
+        for (int64_t u = (wb + wstart) * kWinTiles + lane; u < nt; u += 64)
+          nan |= __builtin_isnan(S[tile_of<DT>(T, c, sp, u).slot]);
+        if (__ballot(nan)) acc = (A_t)__builtin_nan("");
+        return acc;
+      }
+      const int G = grid_of(acc);
+      const double A = a_of(acc);
+      Map m{0.0, 0.0};
+      if (valid && lane >= wstart) {
+        const int j = gw - G;
+        m = j == 0 ? Map{wm.x, wm.y} : (j == 1 ? Map{wm.z, wm.w} : Map{__builtin_inf(), __builtin_inf()});
+      }
+      double Al, out;
+      if (__ballot(m.e != m.o) == 0ull) {
+        Al = A + wave_excl_sum(m.e, lane);
+        out = Al + m.e;
+      } else {
+        Al = apply(wave_excl(m, lane), A);
+        out = apply(m, Al);
+      }
+      const unsigned long long ball = __ballot(!(out < Acc<W>::kTop));
+      if (ball == 0ull) {
+        acc = rebuild<W>(__shfl(out, 63, 64), G);
+        break;
+      }
+      const int ls = __builtin_ctzll(ball);
+      acc = rebuild<W>(__shfl(Al, ls, 64), G);
+      TN_STAT(0, 1);
+      acc = resolve_window<DT>(x, T, c, sp, S, recs, maps, (wb + ls) * kWinTiles, nt, acc, lane);
+      wstart = ls + 1;
+    }
+  }
+  return acc;
+}
+
+__device__ __forceinline__ float rn_bf16(float f) {
+  const uint32_t b = __float_as_uint(f);
+  if (__builtin_isnan(f)) return __uint_as_float((b | 0x00400000u) & 0xffff0000u);
+  return __uint_as_float((b + 0x7fffu + ((b >> 16) & 1u)) & 0xffff0000u);
+}
+
+// One block per tensor (by_chunk: one per chunk, only tensors' first chunks work — layouts of short tensors
+// only, where phase A, which fills tfirst, did not run). skip_short: fp32 tensors up to kShortMax are the
+// in-order walker's (adfl_tn::launch_walk).
+template <int DT>
+__global__ __launch_bounds__(512) void k_tn_resolve(const void* __restrict__ x, const adfl_slq_chunk* __restrict__ chunks, int64_t nall,
+                                                    const int* __restrict__ tfirst, int by_chunk, int skip_short,
+                                                    int threads, const double* __restrict__ S, const Rec* __restrict__ recs,
+                                                    const double4* __restrict__ maps, const int* __restrict__ wing,
+                                                    const double4* __restrict__ winmaps, double* __restrict__ norms64,
+                                                    float* __restrict__ norms32) {
+  using D = Dt<DT>;
+  constexpr bool W = D::kWide;
+  using A_t = typename Acc<W>::T;
+  __shared__ A_t s_acc[D::kContig ? kMaxChains : 8];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int ci;
+  if (by_chunk) {
+    ci = blockIdx.x;
+    if (chunks[ci].first_chunk != ci) return;
+  } else {
+    ci = tfirst[blockIdx.x];
+  }
+  const Tensor T = tensor_of(chunks, ci, nall);
+  const bool long_ = T.n > kShortMax;
+  if (skip_short && !long_) return;
+  const Split sp = split_of(T.n, threads);
+  const int nchains = D::kContig ? (int)sp.nt : D::NC;
+#ifdef ADFL_TN_STATS
+  const long long c0 = clock64();
+#endif
+  for (int c = wave; c < nchains; c += 8) {
+    const A_t a = resolve_chain<DT>(x, T, c, sp, S, recs, maps, wing, winmaps, long_, lane);
+    if (lane == 0) s_acc[c] = a;
+  }
+#ifdef ADFL_TN_STATS
+  TN_STAT(3, clock64() - c0);
+#endif
+  __syncthreads();
+#ifdef ADFL_TN_STATS
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    for (int w = 0; w < 8; ++w) {
+      printf("tn_stats wave %d: windows %llu tiles %llu rounds %llu cycles %llu detail %llu\n", w, g_tn_stats[w][0],
+             g_tn_stats[w][1], g_tn_stats[w][2], g_tn_stats[w][3], g_tn_stats[w][4]);
+      for (int i = 0; i < 5; ++i) g_tn_stats[w][i] = 0;
+    }
+  }
+#endif
+  if (tid != 0) return;
+  double r;
+  if constexpr (D::kContig) {
+    float tot = 0.0f;
+    for (int c = 0; c < nchains; ++c) tot = tot + s_acc[c];
+    r = (double)__half2float(__float2half_rn((float)__builtin_sqrt((double)tot)));
+  } else {
+    const int64_t nv = T.n >= D::VB ? T.n - T.n % D::VB : 0;
+    A_t b = s_acc[0];  // (0 when there are no steps: fp32 below 8 elements, bf16 below 16)
+    for (int c = 1; c < D::NC; ++c) b = b + s_acc[c];
+    int64_t d = nv;
+    if (DT == ADFL_DTYPE_F32 && T.n - d >= 4) {  // torch's compiled tail: 4 rounded squares in order, then fma
+      for (int k = 0; k < 4; ++k) {
+        const float e = (float)D::ld(x, T.base + d + k);
+        const float sq = e * e;
+        b = b + sq;
+      }
+      d += 4;
+    }
+    for (int64_t i = d; i < T.n; ++i) {
+      const A_t e = (A_t)D::ld(x, T.base + i);
+      b = fma_t(e, e, b);
+    }
+    if constexpr (W) {
+      r = __builtin_sqrt((double)b);
+    } else {
+      const float s = (float)__builtin_sqrt((double)b);  // correctly rounded fp32 sqrt
+      r = DT == ADFL_DTYPE_BF16 ? (double)rn_bf16(s) : (double)s;
+    }
+  }
+  if (T.n == 1) r = __builtin_fabs((double)D::ld(x, T.base));  // torch: a one-element tensor's norm is |x|
+  if (norms64) norms64[T.tensor] = r;
+  if (norms32) norms32[T.tensor] = (float)r;
+}
+
+struct Scratch {
+  int* tfirst;
+  double* S;
+  Rec* recs;
+  double4* maps;
+  int* exact;  // [0] = count, then the chunk indices phase C lists for the exact path
+  int* wing;   // phase C2: window summaries, at the slot of the window's first tile
+  double4* winmaps;
+};
+inline int64_t align256(int64_t b) { return (b + 255) & ~(int64_t)255; }
+inline int64_t scratch_bytes(int64_t nchunks, int64_t ntensors) {
+  return align256(ntensors * 4) + align256(nchunks * kSlots * 8) + align256(nchunks * kSlots * (int64_t)sizeof(Rec)) +
+         align256(nchunks * kSlots * 32) + align256((nchunks + 1) * 4) + align256(nchunks * kSlots * 4) +
+         align256(nchunks * kSlots * 32);
+}
+inline Scratch carve(void* p, int64_t nchunks, int64_t ntensors) {
+  char* b = (char*)p;
+  Scratch s;
+  s.tfirst = (int*)b;
+  b += align256(ntensors * 4);
+  s.S = (double*)b;
+  b += align256(nchunks * kSlots * 8);
+  s.recs = (Rec*)b;
+  b += align256(nchunks * kSlots * (int64_t)sizeof(Rec));
+  s.maps = (double4*)b;
+  b += align256(nchunks * kSlots * 32);
+  s.exact = (int*)b;
+  b += align256((nchunks + 1) * 4);
+  s.wing = (int*)b;
+  b += align256(nchunks * kSlots * 4);
+  s.winmaps = (double4*)b;
+  return s;
+}
+
+template <int DT>
+int launch(const void* x, const adfl_slq_chunk* chunks, int64_t nchunks, int64_t ntensors, int32_t kinds,
+           int threads, void* scratch, double* n64, float* n32, hipStream_t st) {
+  const Scratch s = carve(scratch, nchunks, ntensors);
+  const bool any_long = (kinds & ADFL_TORCH_NORM_LONG) != 0, any_short = (kinds & ADFL_TORCH_NORM_SHORT) != 0;
+  const bool walk = DT == ADFL_DTYPE_F32;  // fp32 short tensors: the in-order walker
+  if (walk && any_short) {
+    if (int e = adfl_tn::launch_walk((const float*)x, chunks, nchunks, n32, n64, st)) return e;
+  }
+  if (any_long) {
+    k_tn_sums<DT><<<(unsigned)nchunks, 256, 0, st>>>(x, chunks, nchunks, threads, s.tfirst, s.S);
+    k_tn_grids<DT><<<dim3((unsigned)ntensors, 8), kGridThreads, 0, st>>>(chunks, nchunks, s.tfirst, threads, s.S, s.recs);
+    if (hipError_t e = hipMemsetAsync(s.exact, 0, 4, st)) return (int)e;
+    k_tn_maps<DT><<<(unsigned)nchunks, 256, 0, st>>>(x, chunks, nchunks, threads, s.recs, s.maps, s.exact + 1);
+    k_tn_maps_exact<DT><<<(unsigned)(nchunks < 256 ? nchunks : 256), 256, 0, st>>>(x, chunks, nchunks, threads, s.recs, s.maps,
+                                                                                   s.exact + 1);
+    k_tn_windows<DT><<<dim3((unsigned)ntensors, 8, 8), 256, 0, st>>>(chunks, nchunks, s.tfirst, threads, s.recs, s.maps, s.wing,
+                                                                     s.winmaps);
+    k_tn_resolve<DT><<<(unsigned)ntensors, 512, 0, st>>>(x, chunks, nchunks, s.tfirst, 0, walk, threads, s.S, s.recs, s.maps,
+                                                         s.wing, s.winmaps, n64, n32);
+  } else if (!walk) {
+    k_tn_resolve<DT><<<(unsigned)nchunks, 512, 0, st>>>(x, chunks, nchunks, s.tfirst, 1, 0, threads, s.S, s.recs, s.maps, s.wing,
+                                                        s.winmaps, n64, n32);
+  }
+  return (int)hipGetLastError();
+}
+
+}  // namespace adfl_tnx
+
+
+extern "C" {
+
+int64_t adfl_torch_norm_scratch_bytes(int64_t nchunks, int64_t ntensors) {
+  if (nchunks < 0 || ntensors < 0) return ADFL_E_ARG;
+  return adfl_tnx::scratch_bytes(nchunks, ntensors);
+}
+
+int64_t adfl_torch_norm_short_max(void) { return adfl_tnx::kShortMax; }
+
+int adfl_torch_norms(int32_t dtype, const void* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, int64_t ntensors,
+                     int32_t kinds, int32_t threads, void* d_scratch, int64_t scratch_bytes, double* d_norms64,
+                     float* d_norms32, void* stream) {
+  if (nchunks < 0 || ntensors < 0 || (nchunks > 0 && (!d_x || !d_chunks || !d_scratch)) || (!d_norms64 && !d_norms32))
+    return ADFL_E_ARG;
+  if (nchunks == 0) return ADFL_OK;
+  if (ntensors <= 0 || ntensors > nchunks || threads < 1 || threads > adfl_tnx::kMaxChains) return ADFL_E_ARG;
+  if (scratch_bytes < adfl_tnx::scratch_bytes(nchunks, ntensors)) return ADFL_E_WORKSPACE;
+  if (((uintptr_t)d_scratch & 255) != 0) return ADFL_E_ALIGN;
+  if (kinds == 0) kinds = ADFL_TORCH_NORM_SHORT | ADFL_TORCH_NORM_LONG;
+  hipStream_t st = (hipStream_t)stream;
+  switch (dtype) {
+    case ADFL_DTYPE_F32:
+      return adfl_tnx::launch<ADFL_DTYPE_F32>(d_x, d_chunks, nchunks, ntensors, kinds, threads, d_scratch, d_norms64, d_norms32, st);
+    case ADFL_DTYPE_BF16:
+      return adfl_tnx::launch<ADFL_DTYPE_BF16>(d_x, d_chunks, nchunks, ntensors, kinds, threads, d_scratch, d_norms64, d_norms32, st);
+    case ADFL_DTYPE_F16:
+      return adfl_tnx::launch<ADFL_DTYPE_F16>(d_x, d_chunks, nchunks, ntensors, kinds, threads, d_scratch, d_norms64, d_norms32, st);
+    case ADFL_DTYPE_F64:
+      return adfl_tnx::launch<ADFL_DTYPE_F64>(d_x, d_chunks, nchunks, ntensors, kinds, threads, d_scratch, d_norms64, d_norms32, st);
+    default:
+      return ADFL_E_ARG;
+  }
+}
+
+}  // extern "C"

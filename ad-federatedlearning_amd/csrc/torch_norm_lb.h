@@ -1,9 +1,10 @@
 // torch_norm_lb.h — torch's fp32 L2 norm (the reference's QSGD / CNAT norm, quant.py:226,512) bit for bit,
 // tile-parallel at streaming rate. Included by stoch_codec.hip (device code + launch helper).
 //
-// The order. torch 2.10's CPU vector_norm(ord=2) over n >= 8 fp32 elements keeps 8 accumulators,
+// The order. torch 2.10's CPU vector_norm(ord=2) over fp32 elements keeps 8 accumulators,
 // acc[j] = fmaf(x[8i+j], x[8i+j], acc[j]) for i in order, then sums them left to right and runs the n % 8
-// tail with fmaf (oracle/slq_oracle.c oracle_torch_l2_norm, pinned to every golden norm). Each chain is a
+// tail (tail_sum: a group of 4 rounded squares, then fmaf; oracle/slq_oracle.c oracle_torch_l2_norm,
+// pinned to torch itself). Each chain is a
 // sequence of dependent roundings: run in order (k_norm_walk) it costs one dependent FMA latency per step.
 //
 // Why it parallelises. A step is RN32(acc + p) with p = x*x exact (48 bits: exact in fp64). While acc stays
@@ -184,6 +185,22 @@ __device__ __forceinline__ double lane_total(const float (&e)[kRegs], int g, boo
   return T;
 }
 
+// The n % 8 tail after the lane sum, as torch's compiled scalar loop `b += x * x` runs it: a first group of 4
+// (when there are 4 or more) with each square rounded and added in order (an in-order vectorised reduction),
+// the rest with fma (oracle_torch_l2_norm). Also the whole sum below 8 elements, from b = 0.
+__device__ __forceinline__ float tail_sum(const float* x, int64_t d, int64_t n, float b) {
+  if (n - d >= 4) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float sq = x[d + k] * x[d + k];
+      b = b + sq;
+    }
+    d += 4;
+  }
+  for (int64_t i = d; i < n; ++i) b = __builtin_fmaf(x[i], x[i], b);
+  return b;
+}
+
 constexpr int64_t kWalkMax = 1 << 16;                     // tensors up to this size are walked (k_norm_walk)
 constexpr int kStageStride = kTile / 8 + 4;               // a slow tile staged chain-major (+4: banks, 16 B)
 
@@ -204,7 +221,8 @@ constexpr int kWalkBlockStride = kWalkBlock / 8 + 4;   // floats per chain row (
 
 __global__ __launch_bounds__(kWalkThreads) void k_norm_walk(const float* __restrict__ x,
                                                            const adfl_slq_chunk* __restrict__ chunks,
-                                                           int64_t max_n, float* __restrict__ norms) {
+                                                           int64_t max_n, float* __restrict__ norms,
+                                                           double* __restrict__ norms64 = nullptr) {
   __shared__ __attribute__((aligned(16))) float buf[3][8 * kWalkBlockStride];
   const adfl_slq_chunk ch = chunks[blockIdx.x];
   if ((int64_t)blockIdx.x != ch.first_chunk) return;
@@ -214,12 +232,10 @@ __global__ __launch_bounds__(kWalkThreads) void k_norm_walk(const float* __restr
   const int tid = threadIdx.x, c = tid & 7, s0 = tid >> 3;
   if (n < 8) {
     if (tid == 0) {
-      float b = 0.0f;
-      for (int64_t i = 0; i < n; ++i) {
-        const float sq = xt[i] * xt[i];
-        b = b + sq;
-      }
-      norms[ch.tensor] = (float)__builtin_sqrt((double)b);
+      const float b = tail_sum(xt, 0, n, 0.0f);
+      const float r = n == 1 ? __builtin_fabsf(xt[0]) : (float)__builtin_sqrt((double)b);  // one element: |x|
+      if (norms) norms[ch.tensor] = r;
+      if (norms64) norms64[ch.tensor] = r;
     }
     return;
   }
@@ -294,8 +310,10 @@ __global__ __launch_bounds__(kWalkThreads) void k_norm_walk(const float* __restr
 #pragma unroll
     for (int j = 1; j < 8; ++j) b = b + __shfl(acc, j, 64);
     if (tid == 0) {
-      for (int64_t i = nv; i < n; ++i) b = __builtin_fmaf(xt[i], xt[i], b);
-      norms[ch.tensor] = (float)__builtin_sqrt((double)b);  // correctly rounded fp32 sqrt
+      b = tail_sum(xt, nv, n, b);
+      const float r = (float)__builtin_sqrt((double)b);  // correctly rounded fp32 sqrt
+      if (norms) norms[ch.tensor] = r;
+      if (norms64) norms64[ch.tensor] = r;
     }
   }
 }
@@ -670,15 +688,12 @@ __global__ __launch_bounds__(kThreads) void k_norm_torch(const float* __restrict
         const float* xs = x + tbase;
         float b = 0.0f;
         if (n < 8) {
-          for (int64_t i = 0; i < n; ++i) {
-            const float sq = xs[i] * xs[i];
-            b = b + sq;
-          }
+          b = tail_sum(xs, 0, n, 0.0f);
         } else {
           b = s_inc[0];
 #pragma unroll
           for (int j = 1; j < 8; ++j) b = b + s_inc[j];
-          for (int64_t i = nv; i < n; ++i) b = __builtin_fmaf(xs[i], xs[i], b);
+          b = tail_sum(xs, nv, n, b);
         }
         norms[ch.tensor] = s_err ? __builtin_nanf("") : (float)__builtin_sqrt((double)b);
       }

@@ -48,7 +48,7 @@ int64_t adfl_stoch_workspace_bytes(int64_t nchunks);
  *   ADFL_NORM_LINF: d_norms[t] = max|x_t|, d_mins[t] = min|x_t| (ord=inf / -inf, quant.py:367,380);
  *                   NaN anywhere in x_t makes both NaN. d_mins may be NULL for ADFL_NORM_L2.
  *   ADFL_NORM_L2_TORCH: ||x_t||_2 bit-identical to torch 2.10's CPU vector_norm (its fp32 reduction order:
- *                   8 FMA lane accumulators, lane sum, FMA tail; plain multiply-add below 8 elements),
+ *                   8 FMA lane accumulators, lane sum, then the n % 8 tail: 4 rounded squares, then FMA),
  *                   i.e. the reference's own norm. One launch, no workspace (d_workspace may be NULL), but
  *                   sequential per tensor: about one element per cycle per tensor. */
 int adfl_stoch_norms_batched(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, int mode,
@@ -69,6 +69,27 @@ enum { ADFL_TORCH_NORM_SHORT = 1, ADFL_TORCH_NORM_LONG = 2 };
 int64_t adfl_stoch_torch_norm_walk_max(void);
 int adfl_stoch_norms_torch(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, int32_t kinds,
                            void* d_scratch, int64_t scratch_bytes, float* d_norms, void* stream);
+
+/* torch 2.10's CPU vector_norm(x, ord=2) — the reference's QSGD / CNAT norm (quant.py:226,512) — bit for bit
+ * for fp32, bf16, fp16 and fp64 buckets (dtype ADFL_DTYPE_*: d_x holds elements of that type, indexed by the
+ * chunk table), in phases with no cross-block waits (csrc/torch_norm.hip): per-tile fp64 sums, a per-chain
+ * prefix that predicts each tile's binade, per-tile exact integer maps under the predicted binades, and one
+ * block per tensor composing them, running the reference's fma only where an accumulator leaves its binade.
+ * Replaces adfl_stoch_norms_torch for every dtype. Orders restated: oracle/slq_oracle.c
+ * oracle_torch_l2_norm{,_bf16,_f16,_f64}.
+ *   threads: torch.get_num_threads() of the process whose norm is reproduced (fp16 tensors of >= 32768
+ *            elements are summed in that many contiguous pieces; 1..512; unused for the other dtypes).
+ *   kinds:   ADFL_TORCH_NORM_SHORT / _LONG as for adfl_stoch_norms_torch (tensors longer than
+ *            adfl_torch_norm_short_max() take the phased path); 0 = both.
+ *   outputs: d_norms64[t] = the norm as a double (the dtype's value: exact for every dtype) and / or
+ *            d_norms32[t] = (float) of it; either may be NULL, not both.
+ * d_scratch: adfl_torch_norm_scratch_bytes(nchunks, ntensors) bytes, 256-byte aligned, no initialisation.
+ * Four launches (one for layouts of short tensors only). */
+int64_t adfl_torch_norm_scratch_bytes(int64_t nchunks, int64_t ntensors);
+int64_t adfl_torch_norm_short_max(void);
+int adfl_torch_norms(int32_t dtype, const void* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks,
+                     int64_t ntensors, int32_t kinds, int32_t threads, void* d_scratch, int64_t scratch_bytes,
+                     double* d_norms64, float* d_norms32, void* stream);
 
 /* QSGD / RQSGD level quantization given per-tensor norms (quant.py:230-238 and :371-379), levels =
  * 2^bits - 1: scaled = fl(fl(levels*|x|) / norm); l = floor(scaled); q = u8(l + (u < scaled - l));

@@ -223,29 +223,108 @@ void oracle_slq_dequantize_mean_int4(const uint8_t* const* ps, const float* scal
 uint32_t oracle_f32_bits(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
 
 /* torch.linalg.vector_norm(x, ord=2) on an fp32 CPU tensor as torch 2.10 computes it (the reference's
- * QSGD / CNAT scale, Src/ADFL/Channel/quant.py:226,512), restated from its observed behaviour — pinned
- * bit for bit to every L2 norm in tests/golden/stoch.npz (the reference executed in place):
- *   n >= 8: the AVX2 norm kernel — 8 fp32 lane accumulators, acc[j] = fma(x[8i+j], x[8i+j], acc[j]) over
- *           i in order; then b = acc[0] + acc[1] + ... + acc[7] left to right; then the n % 8 tail
- *           elements b = fma(x, x, b) in order;
- *   n < 8:  b = b + x*x in order (separate multiply and add).
- *   result: the correctly rounded fp32 sqrt of b.
+ * QSGD / CNAT scale, Src/ADFL/Channel/quant.py:226,512), restated from its observed behaviour and pinned
+ * against torch itself (tests/test_torch_norm_dtypes.py) and every L2 norm in tests/golden/stoch.npz:
+ *   the vectorised kernel: 8 fp32 lane accumulators, acc[j] = fma(x[8i+j], x[8i+j], acc[j]) over the
+ *   n - n % 8 leading elements in order; b = acc[0] + acc[1] + ... + acc[7] left to right; then the n % 8
+ *   tail as the compiler emitted the scalar loop `b += x * x`: a first group of 4 (when the tail holds 4
+ *   or more) with the squares rounded and added in order (an in-order vectorised reduction), the rest
+ *   with fma. Below 8 elements the same rules with no lane accumulators (b starts at 0).
+ *   result: the correctly rounded fp32 sqrt of b. A one-element tensor's norm is |x| (every dtype).
  * fmaf() is C99's single-rounding fused multiply-add. */
 float oracle_torch_l2_norm(const float* x, int64_t n) {
-    float b = 0.0f;
-    if (n < 8) {
-        for (int64_t i = 0; i < n; ++i) {
-            const float sq = x[i] * x[i];
-            b = b + sq;
-        }
-        return sqrtf(b);
-    }
+    if (n == 1) return fabsf(x[0]);  /* a one-element tensor's norm is |x| (no square: no underflow) */
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const int64_t nv = n - n % 8;
     for (int64_t i = 0; i < nv; i += 8)
         for (int j = 0; j < 8; ++j) acc[j] = fmaf(x[i + j], x[i + j], acc[j]);
-    b = acc[0];
+    float b = acc[0];
     for (int j = 1; j < 8; ++j) b = b + acc[j];
-    for (int64_t i = nv; i < n; ++i) b = fmaf(x[i], x[i], b);
+    int64_t d = nv;
+    if (n - d >= 4) {
+        for (int k = 0; k < 4; ++k) {
+            const float sq = x[d + k] * x[d + k];
+            b = b + sq;
+        }
+        d += 4;
+    }
+    for (int64_t i = d; i < n; ++i) b = fmaf(x[i], x[i], b);
     return sqrtf(b);
+}
+
+/* The same norm for the reference's other float dtypes (QSGD / CNAT on an fp16 / bf16 / fp64 tensor,
+ * quant.py:226,512), torch 2.10's CPU kernels restated from their observed behaviour and pinned against
+ * torch itself (tests/test_torch_norm_dtypes.py, tests/golden/torch_norm_dt.npz). The fp32 sqrt is returned;
+ * the caller rounds it to the dtype (torch's round-to-nearest-even conversion). x*x of an fp16 / bf16 value
+ * is exact in fp32, so fused and separate multiply-add give the same steps.
+ *   bf16: the vectorised kernel over 16-element vectors: 8 fp32 lane accumulators, element e into lane e % 8
+ *         for e < n - n % 16, in order; lane sum left to right; the n % 16 tail added in order.
+ *   fp16: the generic reduction (binary_kernel_reduce): below 32768 elements or with one thread, one fp32
+ *         accumulator over every element in order; otherwise at::parallel_for's split — nt = min(threads,
+ *         ceil(n / 32768)) chunks of ceil(n / nt) elements, each summed in order from 0 — then the chunk
+ *         sums added in chunk order to 0. `threads` is torch.get_num_threads() of the calling process.
+ *   fp64: 4 fp64 FMA lane accumulators (element e into lane e % 4 for e < n - n % 4), lane sum left to
+ *         right, the n % 4 tail with fma (also below 4 elements); correctly rounded fp64 sqrt. */
+static float bf16_f(uint16_t h) { uint32_t u = (uint32_t)h << 16; float f; memcpy(&f, &u, 4); return f; }
+static float f16_f(uint16_t h) {
+    const uint32_t s = (uint32_t)(h >> 15) << 31, e = (h >> 10) & 0x1F, m = h & 0x3FF;
+    float f;
+    if (e == 0) {
+        f = ldexpf((float)m, -24);
+        if (s) f = -f;
+        return f;
+    }
+    uint32_t u = s | (e == 31 ? (0xFFu << 23) | (m << 13) : ((e + 112) << 23) | (m << 13));
+    memcpy(&f, &u, 4);
+    return f;
+}
+
+float oracle_torch_l2_norm_bf16(const uint16_t* x, int64_t n) {
+    if (n == 1) return fabsf(bf16_f(x[0]));
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int64_t nv = n - n % 16;
+    for (int64_t i = 0; i < nv; ++i) {
+        const float v = bf16_f(x[i]);
+        acc[i % 8] = fmaf(v, v, acc[i % 8]);
+    }
+    float b = acc[0];
+    for (int j = 1; j < 8; ++j) b = b + acc[j];
+    for (int64_t i = nv; i < n; ++i) {
+        const float v = bf16_f(x[i]);
+        b = fmaf(v, v, b);
+    }
+    return sqrtf(b);
+}
+
+float oracle_torch_l2_norm_f16(const uint16_t* x, int64_t n, int32_t threads) {
+    if (n == 1) return fabsf(f16_f(x[0]));
+    int64_t nt = 1;
+    if (n >= 32768 && threads > 1) {
+        nt = (n + 32767) / 32768;
+        if (nt > threads) nt = threads;
+    }
+    const int64_t cs = (n + nt - 1) / nt;
+    float tot = 0.0f;
+    for (int64_t t = 0; t < nt; ++t) {
+        const int64_t b0 = t * cs, e0 = b0 + cs < n ? b0 + cs : n;
+        float a = 0.0f;
+        for (int64_t i = b0; i < e0; ++i) {
+            const float v = f16_f(x[i]);
+            a = fmaf(v, v, a);
+        }
+        tot = tot + a;
+    }
+    return sqrtf(tot);
+}
+
+double oracle_torch_l2_norm_f64(const double* x, int64_t n) {
+    if (n == 1) return fabs(x[0]);
+    double acc[4] = {0, 0, 0, 0};
+    const int64_t nv = n - n % 4;
+    for (int64_t i = 0; i < nv; i += 4)
+        for (int j = 0; j < 4; ++j) acc[j] = fma(x[i + j], x[i + j], acc[j]);
+    double b = acc[0];
+    for (int j = 1; j < 4; ++j) b = b + acc[j];
+    for (int64_t i = nv; i < n; ++i) b = fma(x[i], x[i], b);
+    return sqrt(b);
 }

@@ -130,6 +130,31 @@ def l2_norm(x_raw, dt) -> float:
         return float(R(n32, dt))
 
 
+def torch_l2_norm(x_raw, dt, threads: int = 1) -> float:
+    """``torch.linalg.vector_norm(x, ord=2).item()`` on an fp16 / bf16 / fp64 CPU tensor bit for bit as torch
+    2.10 computes it (the reference's QSGD / CNAT norm in the tensor's dtype, quant.py:226,512): the C
+    restatements ``oracle_torch_l2_norm_{f16,bf16,f64}`` (oracle/slq_oracle.c), then torch's round-to-nearest
+    conversion of the fp32 sqrt to the dtype. ``threads``: torch.get_num_threads() of the process whose
+    norm is restated (fp16 tensors of >= 32768 elements are split across threads)."""
+    import ctypes
+    import slq_oracle
+    L = slq_oracle.lib()
+    raw = np.ascontiguousarray(np.asarray(x_raw).reshape(-1))
+    if dt == DT_F64:
+        fn = L.oracle_torch_l2_norm_f64
+        fn.argtypes, fn.restype = [ctypes.c_void_p, ctypes.c_int64], ctypes.c_double
+        a = raw.view(np.float64)
+        return float(fn(a.ctypes.data, a.size))
+    a = raw.view(np.uint16)
+    if dt == DT_BF16:
+        fn = L.oracle_torch_l2_norm_bf16
+        fn.argtypes, fn.restype = [ctypes.c_void_p, ctypes.c_int64], ctypes.c_float
+        return float(R(np.float32(fn(a.ctypes.data, a.size)), dt))
+    fn = L.oracle_torch_l2_norm_f16
+    fn.argtypes, fn.restype = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32], ctypes.c_float
+    return float(R(np.float32(fn(a.ctypes.data, a.size, int(threads))), dt))
+
+
 def linf_norm(x_raw, dt) -> float:
     a = np.abs(to_compute(x_raw, dt).reshape(-1))
     return float("nan") if np.isnan(a).any() else float(a.max())

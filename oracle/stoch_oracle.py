@@ -92,7 +92,8 @@ def l2_norm(x: np.ndarray) -> np.float32:
 def torch_l2_norm(x: np.ndarray) -> np.float32:
     """``torch.linalg.vector_norm(x, ord=2)`` bit for bit as torch 2.10's CPU kernel computes it (the
     reference's own QSGD / CNAT norm, quant.py:226,512): 8 fp32 FMA lane accumulators in order, left-to-
-    right lane sum, FMA tail; plain multiply-add below 8 elements (oracle/slq_oracle.c
+    right lane sum, then the n % 8 tail as torch's compiled loop runs it — a group of 4 rounded squares, then
+    FMA (oracle/slq_oracle.c
     ``oracle_torch_l2_norm``; pinned to every golden L2 norm by tests/test_stoch_golden.py)."""
     import ctypes
     import slq_oracle

@@ -401,32 +401,46 @@ def test_torch_order_norm_bucket_and_sizes(align):
         assert same_f32(got[i:i + 1], np.array([so.torch_l2_norm(x)], np.float32)), (i, x.size)
 
 
-@pytest.mark.parametrize("c", [c for c in CASES if c["codec"] == "qsgd"], ids=lambda c: c["name"])
-def test_default_norm_deviation_is_bounded(c):
-    """The DEFAULT norm (fp64 accumulation, correctly rounded) against the reference's fp32-accumulated
-    norm, nothing injected but the uniforms: (1) the scale differs from the reference's by at most torch's
-    own accumulation error, n * 2^-24 relative (2^-23 at least); (2) every level equals the oracle's level
-    for OUR norm — the norm is the only difference; (3) the levels that differ from the reference's differ
-    by one, at a rate bounded by levels * relative norm difference (the width of the moved rounding band)
-    plus a 3-sigma allowance. DESIGN.md §10 reports the measured rates."""
-    x, u, q_ref, _, _, norm, _ = load_case(c)
-    lay = ops.BucketLayout([x.size], align=1)
-    lv, _, nrm = stoch.qsgd_encode_batched(d(x), lay, c["bits"], uniforms=d(u))
-    mine = h(nrm)[0]
-    if not np.isfinite(norm) or norm == 0:
-        assert same_f32(np.array([mine]), np.array([norm], np.float32))
-        return
-    rel = abs(float(mine) - float(norm)) / float(norm)
-    assert rel <= max(x.size * 2.0 ** -24, 2.0 ** -23), (mine, norm)
-    levels = 2 ** c["bits"] - 1
-    q_mine, _ = so.qsgd_quantize(x.reshape(-1), levels, mine, u.reshape(-1))
-    got = h(lv)
-    np.testing.assert_array_equal(got, q_mine)
-    diff = got.astype(np.int32) - q_ref.reshape(-1).astype(np.int32)
-    assert np.all(np.abs(diff) <= 1)
-    rate = np.count_nonzero(diff) / x.size
-    expect = levels * rel
-    assert rate <= expect + 3 * np.sqrt(expect / x.size) + 1.0 / x.size, (rate, expect)
+@pytest.mark.parametrize("c", L2_CASES, ids=[c["name"] for c in L2_CASES])
+def test_default_channel_equals_reference_end_to_end(c):
+    """QSGDChannel(bits) / CNATChannel(bits), built with exactly the reference's constructor, on the golden
+    tensor with only the reference's uniforms injected: levels / exponents, signs, the scale (the reference's
+    own norm, quant.py:226,512, as its Python float — or the 0-dim tensor of the norm == 0 branch) and the
+    decoded floats are the reference's, bit for bit."""
+    x, u, q_ref, s_ref, d_ref, norm, _ = load_case(c)
+    cls = QSGDChannel if c["codec"] == "qsgd" else CNATChannel
+    ch = cls(c["bits"])
+    assert vars(ch) == {"bits": c["bits"], "levels": 2 ** c["bits"] - 1}  # the reference's attributes only
+    qp = ch._quantize_params({"w": torch.from_numpy(x.copy())}, c["bits"], uniforms=d(u))
+    p = qp.params["w"]
+    np.testing.assert_array_equal(p.data.numpy().reshape(-1).view(np.uint8), q_ref.reshape(-1).view(np.uint8))
+    np.testing.assert_array_equal(p.signs.numpy().reshape(-1), s_ref.reshape(-1))
+    assert str(p.data.dtype).replace("torch.", "") == c["q_dtype"]
+    if "tensor" in c["scale"]:
+        assert isinstance(p.scale, torch.Tensor) and float(p.scale) == float(norm)
+    else:
+        assert isinstance(p.scale, float)
+        assert same_f32(np.array([p.scale], np.float32), np.array([norm], np.float32)), (p.scale, norm)
+        assert p.scale == float(norm) or (np.isnan(p.scale) and np.isnan(norm))
+    dec, _ = ch.on_server_receive(qp)
+    assert same_f32(dec["w"].numpy().reshape(-1), d_ref.reshape(-1))
+
+
+@pytest.mark.parametrize("cls", [QSGDChannel, CNATChannel])
+def test_fp64_norm_switch(cls, monkeypatch):
+    """ADFL_STOCH_NORM=fp64 selects the correctly rounded norm (fp64 accumulation), which differs from the
+    reference's on a long tensor; unset, the scale is torch.linalg.vector_norm's bits."""
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(2048, 1024, generator=g) * 1e-3
+    ref = torch.linalg.vector_norm(x).item()
+    qp, _ = cls(8).on_client_send({"w": x})
+    assert qp.params["w"].scale == ref
+    monkeypatch.setenv("ADFL_STOCH_NORM", "fp64")
+    qp64, _ = cls(8).on_client_send({"w": x})
+    assert qp64.params["w"].scale == float(np.float32(so.l2_norm(x.numpy())))
+    monkeypatch.setenv("ADFL_STOCH_NORM", "bogus")
+    with pytest.raises(ValueError, match="ADFL_STOCH_NORM"):
+        cls(8).on_client_send({"w": x})
 
 
 @pytest.mark.parametrize("align", [1, 64])

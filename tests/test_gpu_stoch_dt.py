@@ -78,6 +78,33 @@ def test_kernels_match_reference_given_its_norm(c):
     assert same_f32(d.cpu().numpy(), d_ref.reshape(-1))
 
 
+L2_CASES = [c for c in CASES if c["codec"] != "rqsgd"]
+
+
+@pytest.mark.parametrize("c", L2_CASES, ids=[c["name"] for c in L2_CASES])
+def test_default_channel_equals_reference_end_to_end(c):
+    """QSGDChannel(bits) / CNATChannel(bits) with the reference's constructor on the golden fp16 / bf16 / fp64
+    tensor, only the uniforms injected: the norm is the reference's own in the dtype (torch's CPU order,
+    csrc/torch_norm.hip), so the bytes, signs, scale and decoded floats are the reference's bit for bit."""
+    n = c["name"]
+    x, u = ARR[f"{n}__x"], ARR[f"{n}__u"]
+    q_ref, s_ref, d_ref = ARR[f"{n}__q"], ARR[f"{n}__signs"], ARR[f"{n}__deq"]
+    norm = scale_value(c["scale"])
+    xt = to_torch(x, c["dtype"]).view(tuple(c["shape"]))
+    ch = CHANNELS[c["codec"]](c["bits"])
+    qp = ch._quantize_params({"w": xt}, c["bits"], uniforms=to_torch(u, c["dtype"]).to(DEV))
+    p = qp.params["w"]
+    np.testing.assert_array_equal(p.data.numpy().reshape(-1).view(np.uint8), q_ref.reshape(-1).view(np.uint8))
+    np.testing.assert_array_equal(p.signs.numpy().reshape(-1), s_ref.reshape(-1))
+    if c["scale"].get("tensor"):
+        assert isinstance(p.scale, torch.Tensor) and float(p.scale) == norm
+    else:
+        assert isinstance(p.scale, float) and (p.scale == norm or (np.isnan(p.scale) and np.isnan(norm))), \
+            (p.scale, norm)
+    dec, _ = ch.on_server_receive(qp)
+    assert same_f32(dec["w"].numpy().reshape(-1), d_ref.reshape(-1))
+
+
 def _bucket(dtname, sizes, seed, scale):
     rng = np.random.default_rng(seed)
     lay = ops.BucketLayout(sizes, align=1)   # compact: odd offsets
@@ -156,6 +183,8 @@ def test_channel_mixed_dtype_dict(codec):
             assert (p.data == 0).all() and (p.signs == 1).all() and (dec[name] == 0).all()
             continue
         assert isinstance(p.scale, float)
+        if codec != "rqsgd":   # the reference's own norm (quant.py:226,512), in the tensor's dtype
+            assert p.scale == torch.linalg.vector_norm(x).item(), name
         if x.dtype == torch.float32:
             continue
         dt = {torch.float16: do.DT_F16, torch.bfloat16: do.DT_BF16, torch.float64: do.DT_F64}[x.dtype]

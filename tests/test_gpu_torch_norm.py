@@ -5,7 +5,7 @@ The norm must equal the reference's — torch 2.10's CPU vector_norm, restated i
 that exercises every branch of the look-back kernel: binade crossings (every tensor's first tiles), ties
 (integer and short-mantissa data, where R(p/u) lands on a half), misses of the grid predictor (a chain
 whose values jump in scale), subnormal and overflowing squares, NaN and inf, empty tiles and the n % 8
-tail, tensors below 8 elements (plain multiply-add). Also against the sequential one-wave kernel
+tail, tensors below 8 elements. Also against the sequential one-wave kernel
 (norms_batched NORM_L2_TORCH), across repeated launches on one scratch (the epoch scheme) and two layouts
 sharing it.
 """
