@@ -82,7 +82,6 @@ _STAGING_LOCK = threading.Lock()
 
 
 def _staging() -> _DeviceStaging:
-    hostcopy.keep_host_heap()   # once per process (ADFL_KEEP_HOST_HEAP=0: off)
     idx = torch.cuda.current_device()
     with _STAGING_LOCK:
         st = _STAGING.get(idx)
@@ -177,12 +176,20 @@ def _ptrs(tensors: List[torch.Tensor]) -> np.ndarray:
     return np.fromiter((t.data_ptr() for t in tensors), dtype=np.uint64, count=len(tensors))
 
 
+def _host_heap(lay: ops.BucketLayout) -> None:
+    """A host-resident call: the process heap sized for this layout's fp32 outputs (hostcopy.keep_host_heap:
+    raised only as layouts grow; ADFL_KEEP_HOST_HEAP=0 leaves the allocator alone). Device-resident callers
+    never change the allocator."""
+    hostcopy.keep_host_heap(4 * lay.total, 4 * int(lay.sizes.max()))
+
+
 def _stage_in(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _DeviceStaging, key: str,
               dtype: torch.dtype) -> torch.Tensor:
     """The bucket on the device: one gather + one H2D for CPU tensors, one device gather otherwise."""
     dev_buf = st.buf(key, lay.total, dtype)
     kinds = {t.is_cuda for t in tensors}
     if kinds == {False}:
+        _host_heap(lay)
         host = st.buf(key + "_host", lay.total, dtype, pinned=True)
         es = host.element_size()
         if all(t.is_contiguous() and t.element_size() == es for t in tensors):
@@ -336,6 +343,7 @@ def _encode_host_dict(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _D
     objects). Then one encode launch, the payload D2H range by range with the native scatter behind it. The
     device's scales are checked against the host's (a mismatch rebuilds that output with the device's, which
     the payload was quantized with). Returns [(q, scale)] per tensor."""
+    _host_heap(lay)
     dev = st.device
     stream = torch.cuda.current_stream(dev)
     x_dev = st.buf("x", lay.total, torch.float32)

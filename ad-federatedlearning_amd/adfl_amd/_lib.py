@@ -70,9 +70,6 @@ SIGNATURES = {
     # adfl_stoch.h
     "adfl_stoch_workspace_bytes": (I64, [I64]),
     "adfl_stoch_norms_batched": (INT, [P, P, I64, INT, P, I64, P, P, P]),
-    "adfl_stoch_torch_norm_scratch_bytes": (I64, [I64]),
-    "adfl_stoch_norms_torch": (INT, [P, P, I64, I32, P, I64, P, P]),
-    "adfl_stoch_torch_norm_walk_max": (I64, []),
     "adfl_torch_norm_scratch_bytes": (I64, [I64, I64]),
     "adfl_torch_norm_short_max": (I64, []),
     "adfl_torch_norms": (INT, [I32, P, P, I64, I64, I32, I32, P, I64, P, P, P]),

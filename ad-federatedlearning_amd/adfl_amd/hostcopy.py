@@ -171,31 +171,58 @@ def advise_huge(tensors: Sequence[torch.Tensor], min_bytes: int = 4 << 20) -> No
 
 
 _M_TRIM_THRESHOLD, _M_MMAP_THRESHOLD = -1, -3   # glibc mallopt parameters (malloc.h)
-_heap_kept = None
+_GLIBC_MMAP_MIN = 128 << 10    # glibc's default mmap threshold
+_MMAP_CAP = 32 << 20
+_TRIM_CAP = 1 << 30
+_heap = {"enabled": None, "mmap": 0, "trim": 0}
+_libc_mallopt = None
 
 
-def keep_host_heap() -> bool:
-    """Keep freed host memory in the process heap instead of returning it to the kernel after every call:
-    glibc's mallopt(M_MMAP_THRESHOLD, 32 MiB) puts the channel's per-tensor outputs (ResNet-18's are about
-    180 KiB each, above glibc's 128 KiB default, so each was a fresh mmap: 256 page-fault storms and munmaps
-    per call) on the heap, and mallopt(M_TRIM_THRESHOLD, 1 GiB) keeps up to 1 GiB of freed heap resident. A
-    round's outputs then reuse the pages of the previous round's: no first-touch faults in the scatter, no
-    munmap on free, no mmap_lock contention between the allocating thread and the copying pool. Called once,
-    on the first host-resident channel call; ADFL_KEEP_HOST_HEAP=0 leaves the allocator as it is.
-    Returns whether the setting is in force."""
-    global _heap_kept
-    if _heap_kept is None:
-        _heap_kept = False
-        if os.environ.get("ADFL_KEEP_HOST_HEAP", "1") != "0":
-            try:
-                libc = ctypes.CDLL("libc.so.6")
-                libc.mallopt.argtypes = [ctypes.c_int, ctypes.c_int]
-                libc.mallopt.restype = ctypes.c_int
-                _heap_kept = bool(libc.mallopt(_M_MMAP_THRESHOLD, 32 << 20)) and \
-                    bool(libc.mallopt(_M_TRIM_THRESHOLD, 1 << 30))
-            except (OSError, AttributeError):
-                _heap_kept = False
-    return _heap_kept
+def _mallopt(param: int, value: int) -> bool:
+    global _libc_mallopt
+    if _libc_mallopt is None:
+        try:
+            libc = ctypes.CDLL("libc.so.6")
+            libc.mallopt.argtypes = [ctypes.c_int, ctypes.c_int]
+            libc.mallopt.restype = ctypes.c_int
+            _libc_mallopt = libc.mallopt
+        except (OSError, AttributeError):
+            _libc_mallopt = False
+    return bool(_libc_mallopt) and bool(_libc_mallopt(param, value))
+
+
+def keep_host_heap(working_set: int = 0, largest: int = 0) -> bool:
+    """Keep the channel's freed host outputs in the process heap, sized from its working set.
+
+    The channel's per-tensor outputs (ResNet-18's are about 180 KiB each, above glibc's 128 KiB mmap
+    threshold) would each be a fresh mmap: first-touch page faults in the scatter, an munmap on free, and
+    mmap_lock contention with the copying pool. This sets, PROCESS-WIDE (glibc mallopt; it also turns off
+    glibc's dynamic thresholds):
+      M_MMAP_THRESHOLD = `largest` (the biggest output, bytes) rounded up to a power of two, between 128 KiB
+                         and 32 MiB — so those outputs come from the heap;
+      M_TRIM_THRESHOLD = 2 x `working_set` (one call's output bytes), at most 1 GiB — so at most that much
+                         freed heap stays resident between rounds.
+    Both are only ever raised, as the largest layout seen grows (no setting before the first host-resident
+    call). A round's outputs then reuse the previous round's pages. ADFL_KEEP_HOST_HEAP=0 in the environment
+    leaves the allocator untouched. Returns whether the settings are in force."""
+    if _heap["enabled"] is None:
+        _heap["enabled"] = os.environ.get("ADFL_KEEP_HOST_HEAP", "1") != "0"
+    if not _heap["enabled"] or working_set <= 0:
+        return bool(_heap["mmap"])
+    mmap = _GLIBC_MMAP_MIN
+    while mmap < min(int(largest), _MMAP_CAP):
+        mmap <<= 1
+    trim = min(2 * int(working_set), _TRIM_CAP)
+    if mmap > _heap["mmap"] and _mallopt(_M_MMAP_THRESHOLD, mmap):
+        _heap["mmap"] = mmap
+    if trim > _heap["trim"] and _mallopt(_M_TRIM_THRESHOLD, trim):
+        _heap["trim"] = trim
+    return bool(_heap["mmap"])
+
+
+def heap_settings() -> dict:
+    """The (mmap, trim) thresholds keep_host_heap has set in this process (0: untouched)."""
+    return {"mmap": _heap["mmap"], "trim": _heap["trim"]}
 
 
 def _cpulist(text: str):
@@ -221,21 +248,32 @@ def device_cpus(device: "torch.device") -> "list[int]":
     return [c for c in cpus if c in allowed] if len(cpus) < os.cpu_count() else []
 
 
-_bound = {}
+_bound = {}          # device -> the CPUs of its NUMA node (what on_cpus uses for its pinned buffers)
+_pool_cpus = None    # what the one process-wide copy pool is pinned to
 
 
 def bind_to_device(device: "torch.device") -> "list[int]":
-    """Pin the copy pool's workers to the GPU's NUMA node (once per process; ADFL_HOST_BIND=0: never). The
-    pinned staging buckets are allocated from a thread on that node too (on_cpus). Returns the CPUs used."""
+    """Pin the copy pool's workers to the GPU's NUMA node (ADFL_HOST_BIND=0: never). The pool is one per
+    process: with one device it runs on that device's node; once a process stages for devices on different
+    nodes it is re-pinned to the union of their nodes (not to whichever device came last), so no device's
+    staging is left on a far node alone. The pinned staging buckets are allocated from a thread on each
+    device's own node (on_cpus). Returns the CPUs of this device's node."""
+    global _pool_cpus
     key = (device.type, device.index)
     if key not in _bound:
         cpus = device_cpus(device) if os.environ.get("ADFL_HOST_BIND", "1") != "0" else []
-        if cpus:
-            arr = np.asarray(cpus, dtype=np.int32)
-            if _host_lib().adfl_host_bind(arr.ctypes.data, len(arr)) != 0:
-                cpus = []
         _bound[key] = cpus
+        want = sorted(set().union(*[set(c) for c in _bound.values() if c]))
+        if want and want != _pool_cpus:
+            arr = np.asarray(want, dtype=np.int32)
+            if _host_lib().adfl_host_bind(arr.ctypes.data, len(arr)) == 0:
+                _pool_cpus = want
     return _bound[key]
+
+
+def pool_cpus() -> "list[int] | None":
+    """The CPUs the copy pool is pinned to (None: not pinned)."""
+    return _pool_cpus
 
 
 class on_cpus:

@@ -105,37 +105,13 @@ def norms_batched(flat: torch.Tensor, layout: BucketLayout, mode: int = NORM_L2,
     return norms, mins
 
 
-_TORCH_NORM_SCRATCH = {}  # (device index, stream handle) -> zeroed-once scratch of adfl_stoch_norms_torch
-
-
-def _torch_norm_scratch(layout: BucketLayout, dev) -> torch.Tensor:
-    """The look-back scratch for this device and stream: zeroed when allocated, then reused as is (each launch
-    leaves it ready for the next); grown, zeroed again, when a larger layout needs more."""
-    need = _lib.load().adfl_stoch_torch_norm_scratch_bytes(max(layout.nchunks, 1))
-    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
-    buf = _TORCH_NORM_SCRATCH.get(key)
-    if buf is None or buf.numel() < need:
-        buf = torch.zeros(need, dtype=torch.uint8, device=dev)
-        _TORCH_NORM_SCRATCH[key] = buf
-    return buf
-
-
 def torch_norms(flat: torch.Tensor, layout: BucketLayout, *, norms: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Per-tensor ||x||_2 bit-identical to torch's CPU vector_norm (the reference's QSGD / CNAT norm,
-    quant.py:226,512) at streaming rate: adfl_stoch_norms_torch, one pass with a look-back across each
-    tensor's tiles (csrc/torch_norm_lb.h). Same bits as norms_batched(..., NORM_L2_TORCH), the sequential
-    one-wave-per-tensor kernel."""
+    """Per-tensor ||x||_2 of an fp32 bucket bit-identical to torch's CPU vector_norm (the reference's QSGD /
+    CNAT norm, quant.py:226,512): reference_norms' fp32 output. Same bits as norms_batched(...,
+    NORM_L2_TORCH), the in-order kernel."""
     flat = _check_flat(flat, layout)
-    dev = flat.device
-    norms = torch.empty(layout.ntensors, dtype=torch.float32, device=dev) if norms is None else norms
-    if layout.nchunks == 0:
-        return norms
-    scratch = _torch_norm_scratch(layout, dev)
-    L = _lib.load()
-    walk_max = L.adfl_stoch_torch_norm_walk_max()
-    kinds = (1 if min(layout.sizes) <= walk_max else 0) | (2 if max(layout.sizes) > walk_max else 0)
-    check(L.adfl_stoch_norms_torch(flat.data_ptr(), layout.device_chunks(dev).data_ptr(), layout.nchunks, kinds,
-                                   scratch.data_ptr(), scratch.numel(), _dev(norms, "norms").data_ptr(), _stream(dev)))
+    norms = torch.empty(layout.ntensors, dtype=torch.float32, device=flat.device) if norms is None else norms
+    reference_norms(flat, layout, out32=_dev(norms, "norms"))
     return norms
 
 

@@ -33,7 +33,7 @@
 #include "adfl_stoch.h"
 #include "cnat_log2_table.h"
 #include "philox.h"
-#include "torch_norm_lb.h"
+#include "torch_norm_walk.h"
 #include "torch_sum_order.h"
 
 namespace {
@@ -530,7 +530,7 @@ __global__ __launch_bounds__(kBigBlock) void k_norm_finalize(const adfl_slq_chun
 // a left-to-right sum of the 8 lanes, then the n % 8 tail with fma; below 8 elements plain b + x*x.
 // The chains are sequential (n / 8 dependent FMAs per lane): ADFL_NORM_L2_TORCH runs one block per tensor
 // (adfl_tn::k_norm_walk: four waves stream the tensor through LDS ahead of the FMA chain); the tile-parallel
-// look-back kernel (adfl_stoch_norms_torch, torch_norm_lb.h) gives the same bits for long tensors.
+// phased kernels (adfl_torch_norms, torch_norm.hip) give the same bits for long tensors.
 __device__ __forceinline__ void fill_zero_norm(uint8_t* __restrict__ lv, int8_t* __restrict__ sg, int len,
                                                int t = threadIdx.x) {
   for (int i = t; i < len; i += kBlock) {
@@ -1266,35 +1266,6 @@ int adfl_stoch_norms_batched(const float* d_x, const adfl_slq_chunk* d_chunks, i
   return launch_finalize<ADFL_NORM_LINF>(d_chunks, nchunks, d_workspace, d_norms, d_mins, st);
 }
 
-int64_t adfl_stoch_torch_norm_scratch_bytes(int64_t nchunks) {
-  return nchunks < 1 ? (int64_t)ADFL_E_ARG : adfl_tn::scratch_bytes(nchunks);
-}
-
-int adfl_stoch_norms_torch(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, int32_t kinds,
-                           void* d_scratch, int64_t scratch_bytes, float* d_norms, void* stream) {
-  if (!d_x || !d_norms || !d_scratch || bad_table(d_chunks, nchunks)) return ADFL_E_ARG;
-  const int64_t ntiles = nchunks * adfl_tn::kTilesPerChunk;
-  if (ntiles > 0x7fffffff) return ADFL_E_ARG;
-  if (scratch_bytes < adfl_tn::scratch_bytes(nchunks)) return ADFL_E_WORKSPACE;
-  if (reinterpret_cast<uintptr_t>(d_scratch) % 64) return ADFL_E_ALIGN;
-  if (kinds == 0) kinds = ADFL_TORCH_NORM_SHORT | ADFL_TORCH_NORM_LONG;
-  hipStream_t st = (hipStream_t)stream;
-  if (kinds & ADFL_TORCH_NORM_SHORT) {
-    hipLaunchKernelGGL(adfl_tn::k_norm_walk, dim3((unsigned)nchunks), dim3(adfl_tn::kWalkThreads), 0, st, d_x,
-                       d_chunks, adfl_tn::kWalkMax, d_norms, nullptr);
-    if (int s = launch_status()) return s;
-  }
-  if (kinds & ADFL_TORCH_NORM_LONG) {
-    auto* hdr = static_cast<adfl_tn::Header*>(d_scratch);
-    auto* recs = reinterpret_cast<adfl_tn::Rec*>(static_cast<char*>(d_scratch) + sizeof(adfl_tn::Header));
-    hipLaunchKernelGGL(adfl_tn::k_norm_torch, dim3((unsigned)ntiles), dim3(adfl_tn::kThreads), 0, st, d_x, d_chunks,
-                       ntiles, hdr, recs, d_norms);
-    return launch_status();
-  }
-  return ADFL_OK;
-}
-
-int64_t adfl_stoch_torch_norm_walk_max(void) { return adfl_tn::kWalkMax; }
 
 int adfl_qsgd_quantize_batched(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, int bits,
                                const float* d_norms, const float* d_uniforms, uint64_t seed, uint64_t counter,

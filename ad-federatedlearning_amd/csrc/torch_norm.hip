@@ -56,7 +56,8 @@ namespace adfl_tnx {
 
 #ifdef ADFL_TN_STATS  // tools/ref_norm_prof.py --stats builds: phase D counters per wave, printed per launch
 __device__ unsigned long long g_tn_stats[8][5];  // window descents, tiles in detail, segment rounds, cycles, cycles in detail
-#define TN_STAT(i, v) do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_tn_stats[(threadIdx.x >> 6) & 7][i], (unsigned long long)(v)); } while (0)
+__device__ unsigned long long g_tn_statsB[8][4];  // phase B: cycles in loads + sums, block scan, stores, total
+#define TN_STAT(i, v) do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_tn_stats[blockIdx.y & 7][i], (unsigned long long)(v)); } while (0)
 #else
 #define TN_STAT(i, v) do { } while (0)
 #endif
@@ -476,7 +477,8 @@ __global__ __launch_bounds__(256) void k_tn_sums(const void* __restrict__ x, con
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int f = tid + 256 * i;
-    r[i] = f < v.nvec ? v.vb[f] : u32x4{0u, 0u, 0u, 0u};
+    const u32x4 q = v.vb[f < v.nvec ? f : v.nvec - 1];  // unconditional (index clamped): all loads in flight
+    r[i] = f < v.nvec ? q : u32x4{0u, 0u, 0u, 0u};
   }
   double acc[EPV], acc1 = 0.0;  // strided: per vector position; fp16: acc[0] / acc1 = piece 0 / 1
 #pragma unroll
@@ -547,14 +549,27 @@ __global__ __launch_bounds__(kGridThreads) void k_tn_grids(const adfl_slq_chunk*
   for (int c = blockIdx.y; c < nchains; c += gridDim.y) {
     const int64_t nt = chain_tiles<DT>(T, c, sp);
     double carry = 0.0;
+#ifdef ADFL_TN_STATS
+    const long long b0 = clock64();
+    long long bl = 0, bs = 0, bw = 0;
+#endif
     for (int64_t base = 0; base < nt; base += (int64_t)kGridThreads * kGridPer) {
+#ifdef ADFL_TN_STATS
+      const long long q0 = clock64();
+#endif
       const int64_t t0 = base + (int64_t)tid * kGridPer;
       double y[kGridPer];
 #pragma unroll
-      for (int j = 0; j < kGridPer; ++j) y[j] = t0 + j < nt ? S[tile_of<DT>(T, c, sp, t0 + j).slot] : 0.0;
+      for (int j = 0; j < kGridPer; ++j) {  // unconditional (index clamped) so the loads are all in flight
+        const double v = S[tile_of<DT>(T, c, sp, t0 + j < nt ? t0 + j : nt - 1).slot];
+        y[j] = t0 + j < nt ? v : 0.0;
+      }
       double a = 0.0;
 #pragma unroll
       for (int j = 0; j < kGridPer; ++j) a += y[j];
+#ifdef ADFL_TN_STATS
+      const long long q1 = clock64();
+#endif
       double incl = a;  // inclusive scan over the block: waves, then wave totals
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
@@ -573,6 +588,9 @@ __global__ __launch_bounds__(kGridThreads) void k_tn_grids(const adfl_slq_chunk*
         s_carry = r;
       }
       __syncthreads();
+#ifdef ADFL_TN_STATS
+      const long long q2 = clock64();
+#endif
       double P = s_sum[wave] + incl - a;
 #pragma unroll
       for (int j = 0; j < kGridPer; ++j) {
@@ -581,7 +599,21 @@ __global__ __launch_bounds__(kGridThreads) void k_tn_grids(const adfl_slq_chunk*
       }
       carry = s_carry;
       __syncthreads();
+#ifdef ADFL_TN_STATS
+      const long long q3 = clock64();
+      bl += q1 - q0;
+      bs += q2 - q1;
+      bw += q3 - q2;
+#endif
     }
+#ifdef ADFL_TN_STATS
+    if (tid == 0) {
+      atomicAdd(&g_tn_statsB[c & 7][0], (unsigned long long)bl);
+      atomicAdd(&g_tn_statsB[c & 7][1], (unsigned long long)bs);
+      atomicAdd(&g_tn_statsB[c & 7][2], (unsigned long long)bw);
+      atomicAdd(&g_tn_statsB[c & 7][3], (unsigned long long)(clock64() - b0));
+    }
+#endif
   }
 }
 
@@ -595,7 +627,8 @@ __device__ __forceinline__ void load_chunk(const View<DT>& v, int tid, u32x4 (&r
 #pragma unroll
   for (int i = 0; i < View<DT>::NV; ++i) {
     const int f = tid + 256 * i;
-    r[i] = f < v.nvec ? v.vb[f] : u32x4{0u, 0u, 0u, 0u};
+    const u32x4 q = v.vb[f < v.nvec ? f : v.nvec - 1];  // unconditional (index clamped): all loads in flight
+    r[i] = f < v.nvec ? q : u32x4{0u, 0u, 0u, 0u};
   }
 }
 
@@ -610,8 +643,8 @@ __global__ __launch_bounds__(256) void k_tn_maps(const void* __restrict__ x, con
   constexpr int EPV = V::EPV, NV = V::NV;
   constexpr A_t kM = W ? (A_t)6755399441055744.0 : (A_t)12582912.0f;   // 1.5 * 2^52 / 1.5 * 2^23
   constexpr A_t kBig = W ? (A_t)0x1p51 : (A_t)0x1p22;                   // hi at or above: rint by kM fails
-  __shared__ A_t s_k[4][8][3];
-  __shared__ int s_g[8];
+  __shared__ A_t s_k[4][8][4];
+  __shared__ int s_g[8], s_slow;
   const int ci = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const Tensor T = tensor_of(chunks, ci, nall);
   if (T.n <= kShortMax) return;
@@ -634,10 +667,9 @@ __global__ __launch_bounds__(256) void k_tn_maps(const void* __restrict__ x, con
     sa[p] = (A_t)pow2(s >> 1);
     sb[p] = (s & 1) ? (A_t)2 : (A_t)1;
   }
-  A_t K0[kP], Dl[kP], mx[kP];
+  A_t K0[kP], Dl[kP], mx[kP], fl[kP];  // fl: 1 where a square's rounding may hide a tie (max-reduced)
 #pragma unroll
-  for (int p = 0; p < kP; ++p) K0[p] = Dl[p] = mx[p] = (A_t)0;
-  bool slow = false;
+  for (int p = 0; p < kP; ++p) K0[p] = Dl[p] = mx[p] = fl[p] = (A_t)0;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int f = tid + 256 * i;
@@ -654,13 +686,10 @@ __global__ __launch_bounds__(256) void k_tn_maps(const void* __restrict__ x, con
       K0[q] += k;
       Dl[q] += rr > (A_t)0.25 ? (A_t)1 : (rr < (A_t)-0.25 ? (A_t)-1 : (A_t)0);
       mx[q] = (hi == hi) ? __builtin_fmax(mx[q], hi) : (A_t)__builtin_inf();  // NaN: not covered
-      slow |= (ar == (A_t)0.5) | (ar == (A_t)0.25);
+      if ((ar == (A_t)0.5) | (ar == (A_t)0.25)) fl[q] = (A_t)1;
     }
   }
-  if (__syncthreads_or(slow)) {
-    if (tid == 0) exact_list[atomicAdd(exact_list - 1, 1)] = ci;  // the count sits just before the list
-    return;
-  }
+  if (tid == 0) s_slow = 0;
   if constexpr (D::kContig) {
 #pragma unroll
     for (int p = 0; p < 2; ++p)
@@ -669,11 +698,13 @@ __global__ __launch_bounds__(256) void k_tn_maps(const void* __restrict__ x, con
         K0[p] += __shfl_xor(K0[p], o, 64);
         Dl[p] += __shfl_xor(Dl[p], o, 64);
         mx[p] = __builtin_fmax(mx[p], __shfl_xor(mx[p], o, 64));
+        fl[p] = __builtin_fmax(fl[p], __shfl_xor(fl[p], o, 64));
       }
     if (lane < 2) {
       s_k[wave][lane][0] = lane ? K0[1] : K0[0];
       s_k[wave][lane][1] = lane ? Dl[1] : Dl[0];
       s_k[wave][lane][2] = lane ? mx[1] : mx[0];
+      s_k[wave][lane][3] = lane ? fl[1] : fl[0];
     }
   } else {
     constexpr int kCls = D::NC / EPV;
@@ -684,6 +715,7 @@ __global__ __launch_bounds__(256) void k_tn_maps(const void* __restrict__ x, con
         K0[p] += __shfl_xor(K0[p], o, 64);
         Dl[p] += __shfl_xor(Dl[p], o, 64);
         mx[p] = __builtin_fmax(mx[p], __shfl_xor(mx[p], o, 64));
+        fl[p] = __builtin_fmax(fl[p], __shfl_xor(fl[p], o, 64));
       }
     if (lane < kCls) {
 #pragma unroll
@@ -692,23 +724,27 @@ __global__ __launch_bounds__(256) void k_tn_maps(const void* __restrict__ x, con
         s_k[wave][c][0] = K0[p];
         s_k[wave][c][1] = Dl[p];
         s_k[wave][c][2] = mx[p];
+        s_k[wave][c][3] = fl[p];
       }
     }
   }
   __syncthreads();
   if (tid < npieces) {
-    A_t k0 = 0, dl = 0, m = 0;
+    A_t k0 = 0, dl = 0, m = 0, f = 0;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
       k0 += s_k[w][tid][0];
       dl += s_k[w][tid][1];
       m = __builtin_fmax(m, s_k[w][tid][2]);
+      f = __builtin_fmax(f, s_k[w][tid][3]);
     }
     const int g = s_g[tid];
     const A_t k1 = 2 * k0 + dl;
     const double inf = __builtin_inf();
     const double e0 = m < kBig ? (double)k0 : inf;
     const double e1 = (m < kBig && g - 1 >= Acc<W>::kGmin) ? (double)k1 : inf;
+    // a possible tie matters only where a total can still be covered (below 2^24 / 2^53)
+    if (f > 0 && (e0 < Acc<W>::kTop || e1 < Acc<W>::kTop)) s_slow = 1;
     const int64_t slot = slot_of(ci, tid, T.nall);
     if constexpr (W) {
       maps[slot] = make_double4(e0, e0, e1, e1);
@@ -717,6 +753,8 @@ __global__ __launch_bounds__(256) void k_tn_maps(const void* __restrict__ x, con
       recs[slot] = make_rec<W>(e0, e1, g, 0u);
     }
   }
+  __syncthreads();
+  if (tid == 0 && s_slow) exact_list[atomicAdd(exact_list - 1, 1)] = ci;  // the count sits just before the list
 }
 
 // The listed chunks, exactly: chain-major staging (16 steps per lane block, +1 pad), maps composed in order.
@@ -869,7 +907,8 @@ __global__ __launch_bounds__(256) void k_tn_windows(const adfl_slq_chunk* __rest
 #pragma unroll
       for (int k = 0; k < kTPL; ++k) {
         const int64_t t = w0 + lane * kTPL + k;
-        r[k] = t < nt ? recs[tile_of<DT>(T, c, sp, t).slot] : Rec{kPad << 24, 0u};
+        const Rec q = recs[tile_of<DT>(T, c, sp, t < nt ? t : nt - 1).slot];  // clamped: loads in flight
+        r[k] = t < nt ? q : Rec{kPad << 24, 0u};
         if (t < nt) gmax = max(gmax, rec_g<W>(r[k]));
       }
 #pragma unroll
@@ -952,7 +991,8 @@ __device__ __forceinline__ void load_seg(const void* x, const Tensor& T, int c, 
 #pragma unroll
   for (int i = 0; i < kLane; ++i) {
     const int64_t s = s0 + lane * kLane + i;
-    v[i] = s < s1 ? Dt<DT>::ld(x, elem_of<DT>(T, c, sp, s)) : (typename Dt<DT>::E)0;
+    const typename Dt<DT>::E e = Dt<DT>::ld(x, elem_of<DT>(T, c, sp, s < s1 ? s : s1 - 1));  // clamped
+    v[i] = s < s1 ? e : (typename Dt<DT>::E)0;
   }
 }
 
@@ -988,7 +1028,8 @@ __device__ typename Acc<Dt<DT>::kWide>::T resolve_window(const void* x, const Te
 #pragma unroll
   for (int k = 0; k < kTPL; ++k) {
     const int64_t t = w0 + lane * kTPL + k;
-    r[k] = t < nt ? recs[tile_of<DT>(T, c, sp, t).slot] : Rec{kPad << 24, 0u};
+    const Rec q = recs[tile_of<DT>(T, c, sp, t < nt ? t : nt - 1).slot];  // clamped: loads in flight
+    r[k] = t < nt ? q : Rec{kPad << 24, 0u};
   }
   int start = 0;  // window tiles before it are done
   const int wlen = nt - w0 < kWinTiles ? (int)(nt - w0) : kWinTiles;
@@ -1073,13 +1114,9 @@ __device__ typename Acc<Dt<DT>::kWide>::T resolve_chain(const void* x, const Ten
   for (int64_t wb = 0; wb < nw; wb += 64) {
     const int64_t w = wb + lane;
     const bool valid = w < nw;
-    int gw = 0;
-    double4 wm = make_double4(0.0, 0.0, 0.0, 0.0);
-    if (valid) {
-      const int64_t slot = tile_of<DT>(T, c, sp, w * kWinTiles).slot;
-      gw = wing[slot];
-      wm = winmaps[slot];
-    }
+    const int64_t wslot = tile_of<DT>(T, c, sp, (valid ? w : nw - 1) * kWinTiles).slot;  // clamped
+    const int gw = wing[wslot];
+    const double4 wm = winmaps[wslot];
     int wstart = 0;
     const int wlen = nw - wb < 64 ? (int)(nw - wb) : 64;
     while (wstart < wlen) {
@@ -1126,21 +1163,19 @@ __device__ __forceinline__ float rn_bf16(float f) {
   return __uint_as_float((b + 0x7fffu + ((b >> 16) & 1u)) & 0xffff0000u);
 }
 
-// One block per tensor (by_chunk: one per chunk, only tensors' first chunks work — layouts of short tensors
-// only, where phase A, which fills tfirst, did not run). skip_short: fp32 tensors up to kShortMax are the
-// in-order walker's (adfl_tn::launch_walk).
+// Phase D, one wave per chain: grid (tensors, 8) — by_chunk: (chunks, 8), only tensors' first chunks work
+// (layouts of short tensors only, where phase A, which fills tfirst, did not run); blockIdx.y strides the
+// chains (one chain per CU, so eight chains of one tensor do not share a SIMD). skip_short: fp32 tensors up
+// to kShortMax are the in-order walker's (adfl_tn::launch_walk). Each chain's exact accumulator goes to
+// chain_acc[tensor][chain] for k_tn_finish.
 template <int DT>
-__global__ __launch_bounds__(512) void k_tn_resolve(const void* __restrict__ x, const adfl_slq_chunk* __restrict__ chunks, int64_t nall,
-                                                    const int* __restrict__ tfirst, int by_chunk, int skip_short,
-                                                    int threads, const double* __restrict__ S, const Rec* __restrict__ recs,
-                                                    const double4* __restrict__ maps, const int* __restrict__ wing,
-                                                    const double4* __restrict__ winmaps, double* __restrict__ norms64,
-                                                    float* __restrict__ norms32) {
+__global__ __launch_bounds__(64) void k_tn_chains(const void* __restrict__ x, const adfl_slq_chunk* __restrict__ chunks, int64_t nall,
+                                                  const int* __restrict__ tfirst, int by_chunk, int skip_short,
+                                                  int threads, const double* __restrict__ S, const Rec* __restrict__ recs,
+                                                  const double4* __restrict__ maps, const int* __restrict__ wing,
+                                                  const double4* __restrict__ winmaps, double* __restrict__ chain_acc) {
   using D = Dt<DT>;
-  constexpr bool W = D::kWide;
-  using A_t = typename Acc<W>::T;
-  __shared__ A_t s_acc[D::kContig ? kMaxChains : 8];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lane = threadIdx.x;
   int ci;
   if (by_chunk) {
     ci = blockIdx.x;
@@ -1156,33 +1191,57 @@ __global__ __launch_bounds__(512) void k_tn_resolve(const void* __restrict__ x, 
 #ifdef ADFL_TN_STATS
   const long long c0 = clock64();
 #endif
-  for (int c = wave; c < nchains; c += 8) {
-    const A_t a = resolve_chain<DT>(x, T, c, sp, S, recs, maps, wing, winmaps, long_, lane);
-    if (lane == 0) s_acc[c] = a;
+  for (int c = blockIdx.y; c < nchains; c += gridDim.y) {
+    const double a = (double)resolve_chain<DT>(x, T, c, sp, S, recs, maps, wing, winmaps, long_, lane);
+    if (lane == 0) chain_acc[(int64_t)T.tensor * kMaxChains + c] = a;
   }
 #ifdef ADFL_TN_STATS
   TN_STAT(3, clock64() - c0);
 #endif
-  __syncthreads();
+}
+
+// The lane sum (strided) or the chain sums in order (fp16), the tail, sqrt, rounding to the dtype.
+template <int DT>
+__global__ __launch_bounds__(64) void k_tn_finish(const void* __restrict__ x, const adfl_slq_chunk* __restrict__ chunks, int64_t nall,
+                                                  const int* __restrict__ tfirst, int by_chunk, int skip_short,
+                                                  int threads, const double* __restrict__ chain_acc,
+                                                  double* __restrict__ norms64, float* __restrict__ norms32) {
+  using D = Dt<DT>;
+  constexpr bool W = D::kWide;
+  using A_t = typename Acc<W>::T;
+  if (threadIdx.x != 0) return;
+  int ci;
+  if (by_chunk) {
+    ci = blockIdx.x;
+    if (chunks[ci].first_chunk != ci) return;
+  } else {
+    ci = tfirst[blockIdx.x];
+  }
+  const Tensor T = tensor_of(chunks, ci, nall);
+  if (skip_short && T.n <= kShortMax) return;
 #ifdef ADFL_TN_STATS
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
+  if (blockIdx.x == 0) {
     for (int w = 0; w < 8; ++w) {
-      printf("tn_stats wave %d: windows %llu tiles %llu rounds %llu cycles %llu detail %llu\n", w, g_tn_stats[w][0],
+      printf("tn_stats chain %d: windows %llu tiles %llu rounds %llu cycles %llu detail %llu\n", w, g_tn_stats[w][0],
              g_tn_stats[w][1], g_tn_stats[w][2], g_tn_stats[w][3], g_tn_stats[w][4]);
       for (int i = 0; i < 5; ++i) g_tn_stats[w][i] = 0;
+      printf("tn_statsB chain %d: loads %llu scan %llu stores %llu total %llu\n", w, g_tn_statsB[w][0],
+             g_tn_statsB[w][1], g_tn_statsB[w][2], g_tn_statsB[w][3]);
+      for (int i = 0; i < 4; ++i) g_tn_statsB[w][i] = 0;
     }
   }
 #endif
-  if (tid != 0) return;
+  const Split sp = split_of(T.n, threads);
+  const double* ca = chain_acc + (int64_t)T.tensor * kMaxChains;
   double r;
   if constexpr (D::kContig) {
     float tot = 0.0f;
-    for (int c = 0; c < nchains; ++c) tot = tot + s_acc[c];
+    for (int c = 0; c < (int)sp.nt; ++c) tot = tot + (float)ca[c];
     r = (double)__half2float(__float2half_rn((float)__builtin_sqrt((double)tot)));
   } else {
     const int64_t nv = T.n >= D::VB ? T.n - T.n % D::VB : 0;
-    A_t b = s_acc[0];  // (0 when there are no steps: fp32 below 8 elements, bf16 below 16)
-    for (int c = 1; c < D::NC; ++c) b = b + s_acc[c];
+    A_t b = (A_t)ca[0];  // (0 when there are no steps: fp32 below 8 elements, bf16 below 16)
+    for (int c = 1; c < D::NC; ++c) b = b + (A_t)ca[c];
     int64_t d = nv;
     if (DT == ADFL_DTYPE_F32 && T.n - d >= 4) {  // torch's compiled tail: 4 rounded squares in order, then fma
       for (int k = 0; k < 4; ++k) {
@@ -1216,12 +1275,13 @@ struct Scratch {
   int* exact;  // [0] = count, then the chunk indices phase C lists for the exact path
   int* wing;   // phase C2: window summaries, at the slot of the window's first tile
   double4* winmaps;
+  double* chain_acc;  // phase D: each chain's exact accumulator, [tensor][kMaxChains]
 };
 inline int64_t align256(int64_t b) { return (b + 255) & ~(int64_t)255; }
 inline int64_t scratch_bytes(int64_t nchunks, int64_t ntensors) {
   return align256(ntensors * 4) + align256(nchunks * kSlots * 8) + align256(nchunks * kSlots * (int64_t)sizeof(Rec)) +
          align256(nchunks * kSlots * 32) + align256((nchunks + 1) * 4) + align256(nchunks * kSlots * 4) +
-         align256(nchunks * kSlots * 32);
+         align256(nchunks * kSlots * 32) + align256(ntensors * kMaxChains * 8);
 }
 inline Scratch carve(void* p, int64_t nchunks, int64_t ntensors) {
   char* b = (char*)p;
@@ -1239,6 +1299,8 @@ inline Scratch carve(void* p, int64_t nchunks, int64_t ntensors) {
   s.wing = (int*)b;
   b += align256(nchunks * kSlots * 4);
   s.winmaps = (double4*)b;
+  b += align256(nchunks * kSlots * 32);
+  s.chain_acc = (double*)b;
   return s;
 }
 
@@ -1260,11 +1322,13 @@ int launch(const void* x, const adfl_slq_chunk* chunks, int64_t nchunks, int64_t
                                                                                    s.exact + 1);
     k_tn_windows<DT><<<dim3((unsigned)ntensors, 8, 8), 256, 0, st>>>(chunks, nchunks, s.tfirst, threads, s.recs, s.maps, s.wing,
                                                                      s.winmaps);
-    k_tn_resolve<DT><<<(unsigned)ntensors, 512, 0, st>>>(x, chunks, nchunks, s.tfirst, 0, walk, threads, s.S, s.recs, s.maps,
-                                                         s.wing, s.winmaps, n64, n32);
+    k_tn_chains<DT><<<dim3((unsigned)ntensors, 8), 64, 0, st>>>(x, chunks, nchunks, s.tfirst, 0, walk, threads, s.S, s.recs,
+                                                                 s.maps, s.wing, s.winmaps, s.chain_acc);
+    k_tn_finish<DT><<<(unsigned)ntensors, 64, 0, st>>>(x, chunks, nchunks, s.tfirst, 0, walk, threads, s.chain_acc, n64, n32);
   } else if (!walk) {
-    k_tn_resolve<DT><<<(unsigned)nchunks, 512, 0, st>>>(x, chunks, nchunks, s.tfirst, 1, 0, threads, s.S, s.recs, s.maps, s.wing,
-                                                        s.winmaps, n64, n32);
+    k_tn_chains<DT><<<dim3((unsigned)nchunks, 8), 64, 0, st>>>(x, chunks, nchunks, s.tfirst, 1, 0, threads, s.S, s.recs,
+                                                                s.maps, s.wing, s.winmaps, s.chain_acc);
+    k_tn_finish<DT><<<(unsigned)nchunks, 64, 0, st>>>(x, chunks, nchunks, s.tfirst, 1, 0, threads, s.chain_acc, n64, n32);
   }
   return (int)hipGetLastError();
 }

@@ -679,6 +679,90 @@ def extra_pcie(dev, lib, steps: int) -> dict:
                                              "before each timed call", "parity": bool(dict_ok)}}
 
 
+def extra_stoch_c3(dev, lib, steps: int) -> dict:
+    """The stochastic channels the reference's experiments run (QSGDChannel(8) beside SLQChannel(8),
+    Src/main.py:229,488) on C3, with the reference's own L2 norm (torch's CPU vector_norm order,
+    csrc/torch_norm.hip; quant.py:226,512): (1) host to host, QSGDChannel(8) / CNATChannel(8) built with the
+    reference's constructor, on_client_send then on_server_receive of a CPU state dict of 256 weights
+    (11,689,512 fp32, equal layout) + 256 biases — medians of the calls; (2) device-resident, the bucket's
+    encode (norm + levels + signs, Philox uniforms) timed by HIP events, the Infinity Cache flushed before each.
+    parity: every weight's scale equals torch.linalg.vector_norm of the tensor (the reference's scale), and every
+    decoded tensor equals the reference's _dequantize_tensor arithmetic on the payload (quant.py:243-252,
+    :537-545); the device encode's norms equal torch's. (The levels themselves follow the Philox stream, not
+    torch's mt19937 draws, so they are compared to a reference run only statistically — tests/.)"""
+    from adfl_amd import ops, stoch
+    from adfl_amd.Channel import CNATChannel, QSGDChannel
+    base, rem = divmod(RESNET18_PARAMS, 256)
+    sizes = [base + (1 if i < rem else 0) for i in range(256)]
+    g = torch.Generator().manual_seed(13)
+    params = {}
+    for i, m in enumerate(sizes):
+        params[f"layer{i}.weight"] = torch.randn(1, m, generator=g) * 1e-3
+        params[f"layer{i}.bias"] = torch.randn(64, generator=g) * 1e-3
+    ref_norms = {k: torch.linalg.vector_norm(t).item() for k, t in params.items() if t.ndim > 1}
+    out = {"workload": "C3: a CPU state dict of 256 weights (11,689,512 fp32, equal layout) + 256 biases, bits=8, "
+                       "the reference's L2 norm"}
+    for name, cls in (("qsgd", QSGDChannel), ("cnat", CNATChannel)):
+        ch = cls(8)
+        enc_t, dec_t = [], []
+        qp = dp = None
+        for k in range(3 + max(steps, 5)):
+            dp = qp = None
+            t1 = time.perf_counter()
+            qp, _ = ch.on_client_send(params)
+            t2 = time.perf_counter()
+            dp, _ = ch.on_server_receive(qp)
+            t3 = time.perf_counter()
+            if k >= 3:
+                enc_t.append(t2 - t1)
+                dec_t.append(t3 - t2)
+        ok = True
+        for k, t in params.items():
+            p = qp.params[k]
+            if t.ndim <= 1:
+                ok = ok and torch.equal(dp[k], t)
+                continue
+            ok = ok and p.scale == ref_norms[k]
+            if name == "qsgd":   # quant.py:251-252
+                want = (p.scale * p.data.float() / ch.levels) * p.signs.float()
+            else:                # quant.py:545
+                want = p.scale * p.signs.float() * (2 ** p.data.float())
+            ok = ok and torch.equal(dp[k].view(torch.int32), want.view(torch.int32))
+        e_ms, d_ms = _median(enc_t) * 1e3, _median(dec_t) * 1e3
+        out[f"{name}_host"] = {"encode_ms": round(e_ms, 3), "decode_ms": round(d_ms, 3),
+                               "round_trip_ms": round(e_ms + d_ms, 3), "rounds": len(enc_t), "parity": bool(ok)}
+    # device-resident encodes of the same bucket (norm in torch's order + levels + signs)
+    lay = ops.BucketLayout(sizes, align=1)
+    xc = torch.cat([params[f"layer{i}.weight"].view(-1) for i in range(256)])
+    x = xc.to(dev)
+    lv = torch.empty(lay.total, dtype=torch.uint8, device=dev)
+    sg = torch.empty(lay.total, dtype=torch.int8, device=dev)
+    nrm = torch.empty(lay.ntensors, device=dev)
+    ws = stoch.workspace(lay, dev)
+    junk = torch.ones(128 << 20, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    want = torch.tensor([ref_norms[f"layer{i}.weight"] for i in range(256)], dtype=torch.float32)
+    for name in ("qsgd", "cnat"):
+        def enc():
+            if name == "qsgd":
+                stoch.qsgd_encode_batched(x, lay, 8, seed=1, levels=lv, signs=sg, norms=nrm, ws=ws, torch_norm=True)
+            else:
+                stoch.cnat_encode_batched(x, lay, 8, seed=1, exps=lv.view(torch.int8), signs=sg, norms=nrm, ws=ws,
+                                          torch_norm=True)
+        enc()
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(max(steps, 10))]
+        for e in evs:
+            junk.amax()
+            e[0].record(stream)
+            enc()
+            e[1].record(stream)
+        torch.cuda.synchronize()
+        ms = _median([e[0].elapsed_time(e[1]) for e in evs])
+        out[f"{name}_device_encode"] = {"ms": round(ms, 4), "GiB_per_s": round(lay.total * 4 / GIB / (ms * 1e-3), 1),
+                                        "parity": bool(torch.equal(nrm.cpu().view(torch.int32), want.view(torch.int32)))}
+    return out
+
+
 _FP_MUL = -7046029254386353131        # 0x9E3779B97F4A7C15 as int64 (golden-ratio multiplier)
 
 
@@ -968,7 +1052,8 @@ def main():
     if args.extras == "on" or (args.extras == "auto" and world == 1):
         # BASELINE's other single-GPU configs and the host-inclusive rate, after the timed headline (never in
         # `value`); each carries its own parity against the reference's ATen ops
-        for key, fn, st in (("c3", extra_c3, 20), ("c5_int4", extra_c5, 10), ("pcie", extra_pcie, 5)):
+        for key, fn, st in (("c3", extra_c3, 20), ("c5_int4", extra_c5, 10), ("pcie", extra_pcie, 5),
+                            ("stoch_c3", extra_stoch_c3, 5)):
             try:
                 line[key] = fn(dev, lib, st)
             except Exception as e:  # noqa: BLE001

@@ -55,32 +55,20 @@ int adfl_stoch_norms_batched(const float* d_x, const adfl_slq_chunk* d_chunks, i
                              void* d_workspace, int64_t workspace_bytes, float* d_norms, float* d_mins,
                              void* stream);
 
-/* ADFL_NORM_L2_TORCH's norms (the same bits: torch 2.10's CPU vector_norm, quant.py:226,512) at streaming
- * rate: one pass over x in 4096-element tiles with a decoupled look-back across each tensor's tiles (the
- * reduction is exact integer arithmetic while an accumulator stays in one binade; csrc/torch_norm_lb.h).
- * d_scratch: adfl_stoch_torch_norm_scratch_bytes(nchunks) bytes of device memory, 64-byte aligned, ZEROED
- * ONCE when allocated and then reused as is (each launch leaves it ready for the next); launches that may
- * run concurrently need scratches of their own (one per stream). One launch. */
-int64_t adfl_stoch_torch_norm_scratch_bytes(int64_t nchunks);
-/* kinds: which tensors the bucket holds, so a launch with nothing to do is skipped — ADFL_TORCH_NORM_SHORT
- * (some of at most adfl_stoch_torch_norm_walk_max() elements: one wave walks each, the reference loop with
- * its loads kept ahead of the FMA chain) | ADFL_TORCH_NORM_LONG (some longer: the tile look-back); 0 = both. */
 enum { ADFL_TORCH_NORM_SHORT = 1, ADFL_TORCH_NORM_LONG = 2 };
-int64_t adfl_stoch_torch_norm_walk_max(void);
-int adfl_stoch_norms_torch(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, int32_t kinds,
-                           void* d_scratch, int64_t scratch_bytes, float* d_norms, void* stream);
 
 /* torch 2.10's CPU vector_norm(x, ord=2) — the reference's QSGD / CNAT norm (quant.py:226,512) — bit for bit
  * for fp32, bf16, fp16 and fp64 buckets (dtype ADFL_DTYPE_*: d_x holds elements of that type, indexed by the
  * chunk table), in phases with no cross-block waits (csrc/torch_norm.hip): per-tile fp64 sums, a per-chain
  * prefix that predicts each tile's binade, per-tile exact integer maps under the predicted binades, and one
  * block per tensor composing them, running the reference's fma only where an accumulator leaves its binade.
- * Replaces adfl_stoch_norms_torch for every dtype. Orders restated: oracle/slq_oracle.c
+ * Orders restated: oracle/slq_oracle.c
  * oracle_torch_l2_norm{,_bf16,_f16,_f64}.
  *   threads: torch.get_num_threads() of the process whose norm is reproduced (fp16 tensors of >= 32768
  *            elements are summed in that many contiguous pieces; 1..512; unused for the other dtypes).
- *   kinds:   ADFL_TORCH_NORM_SHORT / _LONG as for adfl_stoch_norms_torch (tensors longer than
- *            adfl_torch_norm_short_max() take the phased path); 0 = both.
+ *   kinds:   which tensors the bucket holds, so launches with nothing to do are skipped:
+ *            ADFL_TORCH_NORM_SHORT (some of at most adfl_torch_norm_short_max() elements: fp32 ones are walked
+ *            in order, one block per tensor) | ADFL_TORCH_NORM_LONG (some longer: the phased path); 0 = both.
  *   outputs: d_norms64[t] = the norm as a double (the dtype's value: exact for every dtype) and / or
  *            d_norms32[t] = (float) of it; either may be NULL, not both.
  * d_scratch: adfl_torch_norm_scratch_bytes(nchunks, ntensors) bytes, 256-byte aligned, no initialisation.

@@ -1,5 +1,5 @@
 """Device time of the reference-order L2 norm (stoch.reference_norms, csrc/torch_norm.hip) on C2 / C3 for each
-dtype, against the fp64 default norm and round 4's look-back kernel (fp32), plus per-kernel splits.
+dtype, against the fp64 norm (fp32), and the QSGD / CNAT encodes with either norm.
 
     python tools/ref_norm_bench.py [--reps 21] [--dtypes f32,bf16,f16,f64]
 """
@@ -58,10 +58,14 @@ def main():
                 nrm = torch.empty(lay.ntensors, device=dev)
                 ws = stoch.workspace(lay, dev)
                 out["default_fp64_norm_ms"] = timed(lambda: stoch.norms_batched(x, lay, stoch.NORM_L2, norms=nrm, ws=ws))
-                out["r4_lookback_ms"] = timed(lambda: stoch.torch_norms(x, lay, norms=nrm))
-                old = stoch.torch_norms(x, lay).double()
-                new, _ = stoch.reference_norms(x, lay)
-                out["equals_r4_lookback"] = bool(torch.equal(old, new))
+                qs = torch.empty(lay.total, dtype=torch.uint8, device=dev)
+                sg = torch.empty(lay.total, dtype=torch.int8, device=dev)
+                for tn in (False, True):
+                    k = "reference" if tn else "fp64"
+                    out[f"qsgd_encode_{k}_norm_ms"] = timed(lambda: stoch.qsgd_encode_batched(
+                        x, lay, 8, seed=1, levels=qs, signs=sg, norms=nrm, ws=ws, torch_norm=tn))
+                    out[f"cnat_encode_{k}_norm_ms"] = timed(lambda: stoch.cnat_encode_batched(
+                        x, lay, 8, seed=1, exps=qs.view(torch.int8), signs=sg, norms=nrm, ws=ws, torch_norm=tn))
             res[f"{name} {dn}"] = out
             print(name, dn, json.dumps(out), flush=True)
     print(json.dumps(res))
