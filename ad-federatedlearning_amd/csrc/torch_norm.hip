@@ -44,6 +44,7 @@
 #include <hip/hip_fp16.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "adfl_slq.h"
 #include "adfl_stoch.h"
@@ -55,8 +56,9 @@ int launch_walk(const float* x, const adfl_slq_chunk* chunks, int64_t nchunks, f
 namespace adfl_tnx {
 
 #ifdef ADFL_TN_STATS  // tools/ref_norm_prof.py --stats builds: phase D counters per wave, printed per launch
-__device__ unsigned long long g_tn_stats[8][5];  // window descents, tiles in detail, segment rounds, cycles, cycles in detail
-__device__ unsigned long long g_tn_statsB[8][4];  // phase B: cycles in loads + sums, block scan, stores, total
+__device__ unsigned long long g_tn_stats[8][10];  // window descents, tiles in detail, segment rounds, cycles, cycles in
+// detail, cycles waiting for segment loads, cycles in window descents, window scans, exact-path segment rounds,
+// cycles in segments
 #define TN_STAT(i, v) do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_tn_stats[blockIdx.y & 7][i], (unsigned long long)(v)); } while (0)
 #else
 #define TN_STAT(i, v) do { } while (0)
@@ -208,59 +210,6 @@ __device__ __forceinline__ Map lane_map_exact(const E (&v)[kLane], int g) {
   return Map{se, so - 1.0};
 }
 
-// A lane's map on grid g: the fast path (no tie possible: one sum) for fp32 accumulators, the exact one
-// when any lane of the wave might hold a tie (4v or v an integer).
-template <bool W, typename E>
-__device__ __forceinline__ Map lane_map(const E (&v)[kLane], int g) {
-  if constexpr (W) {
-    return lane_map_exact<W>(v, g);
-  } else {
-    const double sc = pow2(23 - g);
-    double K = 0.0;
-    bool maybe = false;
-#pragma unroll
-    for (int i = 0; i < kLane; ++i) {
-      const double d = (double)v[i];
-      const double x2 = d * (d * sc);
-      const double w = x2 * 2.0;
-      K += (x2 + kMagic) - kMagic;
-      maybe |= ((w + kMagic) - kMagic) == w && w != 0.0;  // 2v an integer: a tie is possible
-    }
-    if (__ballot(maybe) == 0ull) return Map{K, K};
-    return maybe ? lane_map_exact<W>(v, g) : Map{K, K};
-  }
-}
-
-// The two candidate maps of phase C (grids g and g - 1) in one pass, fast path for fp32 accumulators.
-template <bool W, typename E>
-__device__ __forceinline__ void lane_maps2(const E (&v)[kLane], int g, Map& m0, Map& m1) {
-  if constexpr (W) {
-    m0 = lane_map_exact<W>(v, g);
-    m1 = g - 1 >= Acc<W>::kGmin ? lane_map_exact<W>(v, g - 1) : Map{__builtin_nan(""), __builtin_nan("")};
-  } else {
-    const double sc = pow2(23 - g);
-    double K0 = 0.0, K1 = 0.0;
-    bool maybe = false;
-#pragma unroll
-    for (int i = 0; i < kLane; ++i) {
-      const double d = (double)v[i];
-      const double x2 = d * (d * sc);
-      const double y = x2 * 2.0, w = x2 * 4.0;
-      K0 += (x2 + kMagic) - kMagic;
-      K1 += (y + kMagic) - kMagic;
-      maybe |= ((w + kMagic) - kMagic) == w && w != 0.0;
-    }
-    if (__ballot(maybe) != 0ull && maybe) {
-      m0 = lane_map_exact<W>(v, g);
-      m1 = lane_map_exact<W>(v, g - 1);
-    } else {
-      m0 = Map{K0, K0};
-      m1 = Map{K1, K1};
-    }
-    if (g - 1 < Acc<W>::kGmin) m1 = Map{__builtin_nan(""), __builtin_nan("")};
-  }
-}
-
 // ---- dtype traits
 template <int DT> struct Dt;
 template <> struct Dt<ADFL_DTYPE_F32> {
@@ -410,6 +359,12 @@ __device__ __forceinline__ double rec_k(Rec r, int j) {  // j = 0 / 1: the total
 }
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// x streams through phases A and C once each (1 GiB on C2, beyond the Infinity Cache): non-temporal loads
+// (measured: phase A 190 -> 171 us on C2)
+// (global address space, so they are global_load, not flat_load, and do not count on lgkmcnt)
+__device__ __forceinline__ u32x4 ld_x(const u32x4* p) {
+  return __builtin_nontemporal_load((const __attribute__((address_space(1))) u32x4*)p);
+}
 
 // A chunk's elements as 16-byte vectors from the aligned block holding its first element: element e of the
 // chunk is position (e + delta) % EPV of vector (e + delta) / EPV (tensors of compact buckets start anywhere).
@@ -477,7 +432,7 @@ __global__ __launch_bounds__(256) void k_tn_sums(const void* __restrict__ x, con
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int f = tid + 256 * i;
-    const u32x4 q = v.vb[f < v.nvec ? f : v.nvec - 1];  // unconditional (index clamped): all loads in flight
+    const u32x4 q = ld_x(v.vb + (f < v.nvec ? f : v.nvec - 1));  // unconditional (index clamped): all loads in flight
     r[i] = f < v.nvec ? q : u32x4{0u, 0u, 0u, 0u};
   }
   double acc[EPV], acc1 = 0.0;  // strided: per vector position; fp16: acc[0] / acc1 = piece 0 / 1
@@ -530,90 +485,77 @@ __global__ __launch_bounds__(256) void k_tn_sums(const void* __restrict__ x, con
   }
 }
 
-// ---- phase B: per chain, the exclusive prefix of S over its tiles -> each tile's predicted binade (rec.g)
-// One 1024-thread block per chain (blockIdx.y strides the chains of fp16's split), 16 consecutive tiles per
-// thread held in registers: one round of loads, a block scan, one round of stores per 16384 tiles.
-constexpr int kGridThreads = 1024, kGridPer = 16;
+// ---- phase B: per chain, the exclusive prefix P of S at each tile -> the tile's predicted binade (rec.g).
+// P is only a prediction (a tile whose binade it misses is not covered and is resolved in detail), so its
+// summation order is free: B1 sums each window's S, B2 adds the windows before it to a scan inside the
+// window. One wave per window (lane l: tiles l * kTPL ..), grid (tensors, 8, 8): blockIdx.y strides the
+// chains, blockIdx.z and the wave the windows.
 template <int DT>
-__global__ __launch_bounds__(kGridThreads) void k_tn_grids(const adfl_slq_chunk* __restrict__ chunks, int64_t nall,
-                                                           const int* __restrict__ tfirst, int threads,
-                                                           const double* __restrict__ S, Rec* __restrict__ recs) {
+__global__ __launch_bounds__(256) void k_tn_winsums(const adfl_slq_chunk* __restrict__ chunks, int64_t nall,
+                                                    const int* __restrict__ tfirst, int threads,
+                                                    const double* __restrict__ S, double* __restrict__ wsum) {
   using D = Dt<DT>;
-  __shared__ double s_sum[kGridThreads / 64];
-  __shared__ double s_carry;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const Tensor T = tensor_of(chunks, tfirst[blockIdx.x], nall);
   if (T.n <= kShortMax) return;
   const Split sp = split_of(T.n, threads);
   const int nchains = D::kContig ? (int)sp.nt : D::NC;
+  const int wstride = gridDim.z * 4;
   for (int c = blockIdx.y; c < nchains; c += gridDim.y) {
     const int64_t nt = chain_tiles<DT>(T, c, sp);
-    double carry = 0.0;
-#ifdef ADFL_TN_STATS
-    const long long b0 = clock64();
-    long long bl = 0, bs = 0, bw = 0;
-#endif
-    for (int64_t base = 0; base < nt; base += (int64_t)kGridThreads * kGridPer) {
-#ifdef ADFL_TN_STATS
-      const long long q0 = clock64();
-#endif
-      const int64_t t0 = base + (int64_t)tid * kGridPer;
-      double y[kGridPer];
-#pragma unroll
-      for (int j = 0; j < kGridPer; ++j) {  // unconditional (index clamped) so the loads are all in flight
-        const double v = S[tile_of<DT>(T, c, sp, t0 + j < nt ? t0 + j : nt - 1).slot];
-        y[j] = t0 + j < nt ? v : 0.0;
-      }
+    const int64_t nw = (nt + kWinTiles - 1) / kWinTiles;
+    for (int64_t w = blockIdx.z * 4 + wave; w < nw; w += wstride) {
+      const int64_t w0 = w * kWinTiles;
       double a = 0.0;
 #pragma unroll
-      for (int j = 0; j < kGridPer; ++j) a += y[j];
-#ifdef ADFL_TN_STATS
-      const long long q1 = clock64();
-#endif
-      double incl = a;  // inclusive scan over the block: waves, then wave totals
+      for (int k = 0; k < kTPL; ++k) {
+        const int64_t t = w0 + lane * kTPL + k;
+        const double v = S[tile_of<DT>(T, c, sp, t < nt ? t : nt - 1).slot];  // clamped: loads in flight
+        a += t < nt ? v : 0.0;
+      }
 #pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const double z = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += z;
-      }
-      if (lane == 63) s_sum[wave] = incl;
-      __syncthreads();
-      if (tid == 0) {
-        double r = carry;
-        for (int w = 0; w < kGridThreads / 64; ++w) {
-          const double v = s_sum[w];
-          s_sum[w] = r;
-          r += v;
-        }
-        s_carry = r;
-      }
-      __syncthreads();
-#ifdef ADFL_TN_STATS
-      const long long q2 = clock64();
-#endif
-      double P = s_sum[wave] + incl - a;
+      for (int o = 1; o < 64; o <<= 1) a += __shfl_xor(a, o, 64);
+      if (lane == 0) wsum[tile_of<DT>(T, c, sp, w0).slot] = a;
+    }
+  }
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void k_tn_grids(const adfl_slq_chunk* __restrict__ chunks, int64_t nall,
+                                                  const int* __restrict__ tfirst, int threads, const double* __restrict__ S,
+                                                  const double* __restrict__ wsum, Rec* __restrict__ recs) {
+  using D = Dt<DT>;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const Tensor T = tensor_of(chunks, tfirst[blockIdx.x], nall);
+  if (T.n <= kShortMax) return;
+  const Split sp = split_of(T.n, threads);
+  const int nchains = D::kContig ? (int)sp.nt : D::NC;
+  const int wstride = gridDim.z * 4;
+  for (int c = blockIdx.y; c < nchains; c += gridDim.y) {
+    const int64_t nt = chain_tiles<DT>(T, c, sp);
+    const int64_t nw = (nt + kWinTiles - 1) / kWinTiles;
+    for (int64_t w = blockIdx.z * 4 + wave; w < nw; w += wstride) {
+      const int64_t w0 = w * kWinTiles;
+      double y[kTPL], a = 0.0;
 #pragma unroll
-      for (int j = 0; j < kGridPer; ++j) {
-        if (t0 + j < nt) recs[tile_of<DT>(T, c, sp, t0 + j).slot] = make_rec<D::kWide>(0.0, 0.0, grid_pred<D::kWide>(P), 0u);
-        P += y[j];
+      for (int k = 0; k < kTPL; ++k) {
+        const int64_t t = w0 + lane * kTPL + k;
+        const double v = S[tile_of<DT>(T, c, sp, t < nt ? t : nt - 1).slot];  // clamped: loads in flight
+        y[k] = t < nt ? v : 0.0;
+        a += y[k];
       }
-      carry = s_carry;
-      __syncthreads();
-#ifdef ADFL_TN_STATS
-      const long long q3 = clock64();
-      bl += q1 - q0;
-      bs += q2 - q1;
-      bw += q3 - q2;
-#endif
+      double base = 0.0;  // the windows before this one
+      for (int64_t j = lane; j < w; j += 64) base += wsum[tile_of<DT>(T, c, sp, j * kWinTiles).slot];
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) base += __shfl_xor(base, o, 64);
+      double P = base + wave_excl_sum(a, lane);
+#pragma unroll
+      for (int k = 0; k < kTPL; ++k) {
+        const int64_t t = w0 + lane * kTPL + k;
+        if (t < nt) recs[tile_of<DT>(T, c, sp, t).slot] = make_rec<D::kWide>(0.0, 0.0, grid_pred<D::kWide>(P), 0u);
+        P += y[k];
+      }
     }
-#ifdef ADFL_TN_STATS
-    if (tid == 0) {
-      atomicAdd(&g_tn_statsB[c & 7][0], (unsigned long long)bl);
-      atomicAdd(&g_tn_statsB[c & 7][1], (unsigned long long)bs);
-      atomicAdd(&g_tn_statsB[c & 7][2], (unsigned long long)bw);
-      atomicAdd(&g_tn_statsB[c & 7][3], (unsigned long long)(clock64() - b0));
-    }
-#endif
   }
 }
 
@@ -627,7 +569,7 @@ __device__ __forceinline__ void load_chunk(const View<DT>& v, int tid, u32x4 (&r
 #pragma unroll
   for (int i = 0; i < View<DT>::NV; ++i) {
     const int f = tid + 256 * i;
-    const u32x4 q = v.vb[f < v.nvec ? f : v.nvec - 1];  // unconditional (index clamped): all loads in flight
+    const u32x4 q = ld_x(v.vb + (f < v.nvec ? f : v.nvec - 1));  // unconditional (index clamped): all loads in flight
     r[i] = f < v.nvec ? q : u32x4{0u, 0u, 0u, 0u};
   }
 }
@@ -642,9 +584,13 @@ __global__ __launch_bounds__(256) void k_tn_maps(const void* __restrict__ x, con
   using A_t = typename Acc<W>::T;
   constexpr int EPV = V::EPV, NV = V::NV;
   constexpr A_t kM = W ? (A_t)6755399441055744.0 : (A_t)12582912.0f;   // 1.5 * 2^52 / 1.5 * 2^23
-  constexpr A_t kBig = W ? (A_t)0x1p51 : (A_t)0x1p22;                   // hi at or above: rint by kM fails
-  __shared__ A_t s_k[4][8][4];
-  __shared__ int s_g[8], s_slow;
+  constexpr A_t kBig = W ? (A_t)0x1p50 : (A_t)0x1p21;                   // hi at or above: rint(2 hi) by kM fails
+  // the largest square (NaN: not covered): fp32 as its bit pattern (squares are >= +0, NaN's pattern is above
+  // +inf's, so an unsigned max propagates it in one instruction); fp64 by value, NaN replaced by +inf
+  using M_t = typename std::conditional<W, double, uint32_t>::type;
+  __shared__ A_t s_k[4][8][2];
+  __shared__ M_t s_mx[4][8];
+  __shared__ int s_g[8], s_slow, s_fl[4][8];
   const int ci = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const Tensor T = tensor_of(chunks, ci, nall);
   if (T.n <= kShortMax) return;
@@ -652,10 +598,10 @@ __global__ __launch_bounds__(256) void k_tn_maps(const void* __restrict__ x, con
   const ChunkGeo G = geo_of<DT>(T, ci, sp);
   if (G.lim <= 0) return;
   const int npieces = D::kContig ? (G.bnd < G.len ? 2 : 1) : D::NC;
-  if (tid < npieces) s_g[tid] = rec_g<W>(recs[slot_of(ci, tid, T.nall)]);
   const V v(x, T.base + G.c0e, G.lim);
   u32x4 r[NV];
-  load_chunk<DT>(v, tid, r);
+  load_chunk<DT>(v, tid, r);  // first: the record load below must not hold the chunk's loads back
+  if (tid < npieces) s_g[tid] = rec_g<W>(recs[slot_of(ci, tid, T.nall)]);
   __syncthreads();
   // per position (strided) or piece (fp16): scale of x so hi = x^2 / u on g: xs = x 2^(s >> 1), hi = xs xs (2)
   constexpr int kP = D::kContig ? 2 : EPV;
@@ -667,84 +613,113 @@ __global__ __launch_bounds__(256) void k_tn_maps(const void* __restrict__ x, con
     sa[p] = (A_t)pow2(s >> 1);
     sb[p] = (s & 1) ? (A_t)2 : (A_t)1;
   }
-  A_t K0[kP], Dl[kP], mx[kP], fl[kP];  // fl: 1 where a square's rounding may hide a tie (max-reduced)
+  // per element: k = rint(hi) and k1 = rint(2 hi) (the totals on g and g - 1), the largest hi, and whether
+  // |hi - k| is 1/2 or 1/4 (a tie on g or g - 1 the rounding of hi may hide: the chunk goes to the exact path)
+  A_t K0[kP], K1[kP];
+  M_t mx[kP];
+  bool fl[kP];
 #pragma unroll
-  for (int p = 0; p < kP; ++p) K0[p] = Dl[p] = mx[p] = fl[p] = (A_t)0;
+  for (int p = 0; p < kP; ++p) {
+    K0[p] = K1[p] = (A_t)0;
+    mx[p] = (M_t)0;
+    fl[p] = false;
+  }
+  const auto step = [&](A_t xv, int q) {
+    const A_t xs = xv * sa[q];
+    const A_t hi = xs * xs * sb[q];
+    const A_t k = (hi + kM) - kM;
+    const A_t rr = hi - k;
+    const A_t ar = __builtin_fabs(rr);
+    K0[q] += k;
+    K1[q] += (hi * (A_t)2 + kM) - kM;
+    if constexpr (W) mx[q] = (hi == hi) ? __builtin_fmax(mx[q], hi) : (M_t)__builtin_inf();
+    else mx[q] = max(mx[q], __float_as_uint(hi));
+    fl[q] |= (ar == (A_t)0.5) | (ar == (A_t)0.25);
+  };
+  if (v.delta == 0 && G.lim == kChunk && G.bnd >= G.len) {  // a whole chunk of one piece: no masks
 #pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int f = tid + 256 * i;
+    for (int i = 0; i < NV; ++i)
 #pragma unroll
-    for (int p = 0; p < EPV; ++p) {
-      const int e = f * EPV + p - v.delta;
-      const A_t xv = (e >= 0 && e < G.lim) ? (A_t)V::elem(r[i], p) : (A_t)0;
-      const int q = D::kContig ? (e < G.bnd ? 0 : 1) : p;
-      const A_t xs = xv * sa[q];
-      const A_t hi = xs * xs * sb[q];
-      const A_t k = (hi + kM) - kM;
-      const A_t rr = hi - k;
-      const A_t ar = __builtin_fabs(rr);
-      K0[q] += k;
-      Dl[q] += rr > (A_t)0.25 ? (A_t)1 : (rr < (A_t)-0.25 ? (A_t)-1 : (A_t)0);
-      mx[q] = (hi == hi) ? __builtin_fmax(mx[q], hi) : (A_t)__builtin_inf();  // NaN: not covered
-      if ((ar == (A_t)0.5) | (ar == (A_t)0.25)) fl[q] = (A_t)1;
+      for (int p = 0; p < EPV; ++p) step((A_t)V::elem(r[i], p), D::kContig ? 0 : p);
+  } else {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int f = tid + 256 * i;
+#pragma unroll
+      for (int p = 0; p < EPV; ++p) {
+        const int e = f * EPV + p - v.delta;
+        step((e >= 0 && e < G.lim) ? (A_t)V::elem(r[i], p) : (A_t)0, D::kContig ? (e < G.bnd ? 0 : 1) : p);
+      }
     }
   }
   if (tid == 0) s_slow = 0;
+  const auto mx_max = [](M_t a, M_t b) -> M_t {
+    if constexpr (W) return __builtin_fmax(a, b);
+    else return max(a, b);
+  };
   if constexpr (D::kContig) {
 #pragma unroll
-    for (int p = 0; p < 2; ++p)
+    for (int p = 0; p < 2; ++p) {
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
         K0[p] += __shfl_xor(K0[p], o, 64);
-        Dl[p] += __shfl_xor(Dl[p], o, 64);
-        mx[p] = __builtin_fmax(mx[p], __shfl_xor(mx[p], o, 64));
-        fl[p] = __builtin_fmax(fl[p], __shfl_xor(fl[p], o, 64));
+        K1[p] += __shfl_xor(K1[p], o, 64);
+        mx[p] = mx_max(mx[p], __shfl_xor(mx[p], o, 64));
       }
+      fl[p] = __ballot(fl[p]) != 0ull;
+    }
     if (lane < 2) {
       s_k[wave][lane][0] = lane ? K0[1] : K0[0];
-      s_k[wave][lane][1] = lane ? Dl[1] : Dl[0];
-      s_k[wave][lane][2] = lane ? mx[1] : mx[0];
-      s_k[wave][lane][3] = lane ? fl[1] : fl[0];
+      s_k[wave][lane][1] = lane ? K1[1] : K1[0];
+      s_mx[wave][lane] = lane ? mx[1] : mx[0];
+      s_fl[wave][lane] = lane ? fl[1] : fl[0];
     }
   } else {
     constexpr int kCls = D::NC / EPV;
 #pragma unroll
-    for (int p = 0; p < EPV; ++p)
+    for (int p = 0; p < EPV; ++p) {
 #pragma unroll
       for (int o = kCls; o < 64; o <<= 1) {
         K0[p] += __shfl_xor(K0[p], o, 64);
-        Dl[p] += __shfl_xor(Dl[p], o, 64);
-        mx[p] = __builtin_fmax(mx[p], __shfl_xor(mx[p], o, 64));
-        fl[p] = __builtin_fmax(fl[p], __shfl_xor(fl[p], o, 64));
+        K1[p] += __shfl_xor(K1[p], o, 64);
+        mx[p] = mx_max(mx[p], __shfl_xor(mx[p], o, 64));
       }
+      // lanes of one class (lane % kCls) hold the same chains: the flag per class from the wave's ballot
+      const unsigned long long b = __ballot(fl[p]);
+      fl[p] = (b & (kCls == 1 ? ~0ull : (0x5555555555555555ull << (lane & 1)))) != 0ull;
+    }
     if (lane < kCls) {
 #pragma unroll
       for (int p = 0; p < EPV; ++p) {
         const int c = ((lane * EPV + p - v.delta) % D::NC + D::NC) % D::NC;
         s_k[wave][c][0] = K0[p];
-        s_k[wave][c][1] = Dl[p];
-        s_k[wave][c][2] = mx[p];
-        s_k[wave][c][3] = fl[p];
+        s_k[wave][c][1] = K1[p];
+        s_mx[wave][c] = mx[p];
+        s_fl[wave][c] = fl[p];
       }
     }
   }
   __syncthreads();
   if (tid < npieces) {
-    A_t k0 = 0, dl = 0, m = 0, f = 0;
+    A_t k0 = 0, k1 = 0;
+    M_t m = 0;
+    bool f = false;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
       k0 += s_k[w][tid][0];
-      dl += s_k[w][tid][1];
-      m = __builtin_fmax(m, s_k[w][tid][2]);
-      f = __builtin_fmax(f, s_k[w][tid][3]);
+      k1 += s_k[w][tid][1];
+      m = mx_max(m, s_mx[w][tid]);
+      f |= s_fl[w][tid] != 0;
     }
     const int g = s_g[tid];
-    const A_t k1 = 2 * k0 + dl;
+    bool big;
+    if constexpr (W) big = !(m < kBig);
+    else big = m >= __float_as_uint(kBig);
     const double inf = __builtin_inf();
-    const double e0 = m < kBig ? (double)k0 : inf;
-    const double e1 = (m < kBig && g - 1 >= Acc<W>::kGmin) ? (double)k1 : inf;
+    const double e0 = big ? inf : (double)k0;
+    const double e1 = (!big && g - 1 >= Acc<W>::kGmin) ? (double)k1 : inf;
     // a possible tie matters only where a total can still be covered (below 2^24 / 2^53)
-    if (f > 0 && (e0 < Acc<W>::kTop || e1 < Acc<W>::kTop)) s_slow = 1;
+    if (f && (e0 < Acc<W>::kTop || e1 < Acc<W>::kTop)) s_slow = 1;
     const int64_t slot = slot_of(ci, tid, T.nall);
     if constexpr (W) {
       maps[slot] = make_double4(e0, e0, e1, e1);
@@ -947,6 +922,10 @@ __global__ __launch_bounds__(256) void k_tn_windows(const adfl_slq_chunk* __rest
 
 // ---- phase D
 // A segment (<= 1024 steps, lane l holding steps 16 l .. 16 l + 15) run from the exact accumulator acc.
+// fp32 accumulators, no tie possible in the wave: each lane's steps add a constant on the binade G and one
+// on G + 1 — both summed in one pass and scanned together, so the usual segment (one crossing) costs one
+// round: the first lane that leaves G runs its steps with fma, and the lanes after it are checked on G + 1
+// from the sums' differences. Otherwise (ties, two crossings, non-finite values) maps, lane by lane.
 template <int DT>
 __device__ __forceinline__ typename Acc<Dt<DT>::kWide>::T resolve_segment(const typename Dt<DT>::E (&v)[kLane],
                                                                            typename Acc<Dt<DT>::kWide>::T acc, int lane) {
@@ -964,7 +943,52 @@ __device__ __forceinline__ typename Acc<Dt<DT>::kWide>::T resolve_segment(const 
     TN_STAT(2, 1);
     const int G = grid_of(acc);
     const double A = a_of(acc);
-    Map m = lane_map<W>(v, G);  // (wave-wide: it ballots)
+    if constexpr (!W) {
+      const double sc = pow2(23 - G);
+      double K0 = 0.0, K1 = 0.0;
+      bool maybe = false;
+#pragma unroll
+      for (int i = 0; i < kLane; ++i) {
+        const double d = (double)v[i];
+        const double x2 = d * (d * sc), h = x2 * 0.5, w = x2 * 2.0;
+        K0 += (x2 + kMagic) - kMagic;
+        K1 += (h + kMagic) - kMagic;
+        maybe |= ((w + kMagic) - kMagic) == w && w != 0.0;  // 2v an integer: a tie is possible (on G or G + 1)
+      }
+      if (__ballot(maybe) == 0ull) {
+        if (lane < start) K0 = K1 = 0.0;
+        double I0 = K0, I1 = K1;  // inclusive scans
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const double p0 = __shfl_up(I0, o, 64), p1 = __shfl_up(I1, o, 64);
+          if (lane >= o) {
+            I0 += p0;
+            I1 += p1;
+          }
+        }
+        const double out = A + I0, Al = out - K0;
+        const unsigned long long ball = __ballot(lane >= start && !(out < Acc<W>::kTop));
+        if (ball == 0ull) return rebuild<W>(__shfl(out, 63, 64), G);
+        const int ls = __builtin_ctzll(ball);
+        A_t a = rebuild<W>(__shfl(Al, ls, 64), G);
+        if (lane == ls) {
+#pragma unroll
+          for (int i = 0; i < kLane; ++i) a = fma_t(v[i], v[i], a);
+        }
+        acc = __shfl(a, ls, 64);
+        start = ls + 1;
+        if (start == 64) return acc;
+        // on from lane ls + 1 on G + 1: the K1 sums of lanes ls + 1 .. (exact while the total is below 2^53)
+        if (__builtin_isfinite(acc) && grid_of(acc) == G + 1 && G + 1 <= Acc<W>::kGmax &&
+            __shfl(I1, 63, 64) < 0x1p52) {
+          const double out1 = a_of(acc) + (I1 - __shfl(I1, ls, 64));
+          if (__ballot(lane > ls && !(out1 < Acc<W>::kTop)) == 0ull) return rebuild<W>(__shfl(out1, 63, 64), G + 1);
+        }
+        continue;
+      }
+    }
+    TN_STAT(8, 1);
+    Map m = lane_map_exact<W>(v, G);
     if (lane < start) m = Map{0.0, 0.0};
     const Map ex = wave_excl(m, lane);
     const double Al = apply(ex, A);
@@ -1006,7 +1030,23 @@ __device__ typename Acc<Dt<DT>::kWide>::T resolve_tile(const void* x, const Tens
 #endif
   for (int64_t s0 = tl.s0; s0 < tl.s1; s0 += kSeg) {
     load_seg<DT>(x, T, c, sp, s0, s0 + kSeg < tl.s1 ? s0 + kSeg : tl.s1, lane, v);
+#ifdef ADFL_TN_STATS
+    {
+      const long long l0 = clock64();
+      float z = 0.0f;
+#pragma unroll
+      for (int i = 0; i < kLane; ++i) z += (float)v[i];
+      __asm__ volatile("" ::"v"(z));
+      TN_STAT(5, clock64() - l0);
+    }
+#endif
+#ifdef ADFL_TN_STATS
+    const long long r0 = clock64();
+#endif
     acc = resolve_segment<DT>(v, acc, lane);
+#ifdef ADFL_TN_STATS
+    TN_STAT(9, clock64() - r0);
+#endif
   }
 #ifdef ADFL_TN_STATS
   TN_STAT(4, clock64() - c0);
@@ -1025,15 +1065,19 @@ __device__ typename Acc<Dt<DT>::kWide>::T resolve_window(const void* x, const Te
   constexpr bool W = Dt<DT>::kWide;
   using A_t = typename Acc<W>::T;
   Rec r[kTPL];
+  double4 mp[kTPL];  // the side maps (read for every tile, so the loads are all in flight; used where kSide)
 #pragma unroll
   for (int k = 0; k < kTPL; ++k) {
     const int64_t t = w0 + lane * kTPL + k;
-    const Rec q = recs[tile_of<DT>(T, c, sp, t < nt ? t : nt - 1).slot];  // clamped: loads in flight
+    const int64_t slot = tile_of<DT>(T, c, sp, t < nt ? t : nt - 1).slot;  // clamped: loads in flight
+    const Rec q = recs[slot];
+    mp[k] = maps[slot];
     r[k] = t < nt ? q : Rec{kPad << 24, 0u};
   }
   int start = 0;  // window tiles before it are done
   const int wlen = nt - w0 < kWinTiles ? (int)(nt - w0) : kWinTiles;
   while (start < wlen) {
+    TN_STAT(7, 1);
     if (!__builtin_isfinite(acc)) {  // inf stays inf unless a NaN follows: the remaining tiles' sums say
       bool nan = false;
       for (int64_t u = w0 + start + lane; u < nt; u += 64) nan |= __builtin_isnan(S[tile_of<DT>(T, c, sp, u).slot]);
@@ -1052,10 +1096,7 @@ __device__ typename Acc<Dt<DT>::kWide>::T resolve_window(const void* x, const Te
       if ((fl & kPad) || lane * kTPL + k < start) return Map{0.0, 0.0};
       const int j = rec_g<W>(q) - G;
       if (j != 0 && j != 1) return Map{__builtin_inf(), __builtin_inf()};
-      if (fl & kSide) {
-        const double4 m = maps[tile_of<DT>(T, c, sp, w0 + lane * kTPL + k).slot];
-        return j == 0 ? Map{m.x, m.y} : Map{m.z, m.w};
-      }
+      if (fl & kSide) return j == 0 ? Map{mp[k].x, mp[k].y} : Map{mp[k].z, mp[k].w};
       const double K = rec_k(q, j);
       return Map{K, K};
     };
@@ -1150,7 +1191,13 @@ __device__ typename Acc<Dt<DT>::kWide>::T resolve_chain(const void* x, const Ten
       const int ls = __builtin_ctzll(ball);
       acc = rebuild<W>(__shfl(Al, ls, 64), G);
       TN_STAT(0, 1);
+#ifdef ADFL_TN_STATS
+      const long long w0c = clock64();
+#endif
       acc = resolve_window<DT>(x, T, c, sp, S, recs, maps, (wb + ls) * kWinTiles, nt, acc, lane);
+#ifdef ADFL_TN_STATS
+      TN_STAT(6, clock64() - w0c);
+#endif
       wstart = ls + 1;
     }
   }
@@ -1222,12 +1269,11 @@ __global__ __launch_bounds__(64) void k_tn_finish(const void* __restrict__ x, co
 #ifdef ADFL_TN_STATS
   if (blockIdx.x == 0) {
     for (int w = 0; w < 8; ++w) {
-      printf("tn_stats chain %d: windows %llu tiles %llu rounds %llu cycles %llu detail %llu\n", w, g_tn_stats[w][0],
-             g_tn_stats[w][1], g_tn_stats[w][2], g_tn_stats[w][3], g_tn_stats[w][4]);
-      for (int i = 0; i < 5; ++i) g_tn_stats[w][i] = 0;
-      printf("tn_statsB chain %d: loads %llu scan %llu stores %llu total %llu\n", w, g_tn_statsB[w][0],
-             g_tn_statsB[w][1], g_tn_statsB[w][2], g_tn_statsB[w][3]);
-      for (int i = 0; i < 4; ++i) g_tn_statsB[w][i] = 0;
+      printf("tn_stats chain %d: windows %llu tiles %llu rounds %llu cycles %llu detail %llu segload %llu windesc %llu"
+             " winscans %llu exactrounds %llu segcycles %llu\n", w, g_tn_stats[w][0], g_tn_stats[w][1], g_tn_stats[w][2],
+             g_tn_stats[w][3], g_tn_stats[w][4], g_tn_stats[w][5], g_tn_stats[w][6], g_tn_stats[w][7], g_tn_stats[w][8],
+             g_tn_stats[w][9]);
+      for (int i = 0; i < 10; ++i) g_tn_stats[w][i] = 0;
     }
   }
 #endif
@@ -1276,12 +1322,13 @@ struct Scratch {
   int* wing;   // phase C2: window summaries, at the slot of the window's first tile
   double4* winmaps;
   double* chain_acc;  // phase D: each chain's exact accumulator, [tensor][kMaxChains]
+  double* wsum;       // phase B: each window's sum of S, at the slot of the window's first tile
 };
 inline int64_t align256(int64_t b) { return (b + 255) & ~(int64_t)255; }
 inline int64_t scratch_bytes(int64_t nchunks, int64_t ntensors) {
   return align256(ntensors * 4) + align256(nchunks * kSlots * 8) + align256(nchunks * kSlots * (int64_t)sizeof(Rec)) +
          align256(nchunks * kSlots * 32) + align256((nchunks + 1) * 4) + align256(nchunks * kSlots * 4) +
-         align256(nchunks * kSlots * 32) + align256(ntensors * kMaxChains * 8);
+         align256(nchunks * kSlots * 32) + align256(ntensors * kMaxChains * 8) + align256(nchunks * kSlots * 8);
 }
 inline Scratch carve(void* p, int64_t nchunks, int64_t ntensors) {
   char* b = (char*)p;
@@ -1301,6 +1348,8 @@ inline Scratch carve(void* p, int64_t nchunks, int64_t ntensors) {
   s.winmaps = (double4*)b;
   b += align256(nchunks * kSlots * 32);
   s.chain_acc = (double*)b;
+  b += align256(ntensors * kMaxChains * 8);
+  s.wsum = (double*)b;
   return s;
 }
 
@@ -1315,7 +1364,8 @@ int launch(const void* x, const adfl_slq_chunk* chunks, int64_t nchunks, int64_t
   }
   if (any_long) {
     k_tn_sums<DT><<<(unsigned)nchunks, 256, 0, st>>>(x, chunks, nchunks, threads, s.tfirst, s.S);
-    k_tn_grids<DT><<<dim3((unsigned)ntensors, 8), kGridThreads, 0, st>>>(chunks, nchunks, s.tfirst, threads, s.S, s.recs);
+    k_tn_winsums<DT><<<dim3((unsigned)ntensors, 8, 8), 256, 0, st>>>(chunks, nchunks, s.tfirst, threads, s.S, s.wsum);
+    k_tn_grids<DT><<<dim3((unsigned)ntensors, 8, 8), 256, 0, st>>>(chunks, nchunks, s.tfirst, threads, s.S, s.wsum, s.recs);
     if (hipError_t e = hipMemsetAsync(s.exact, 0, 4, st)) return (int)e;
     k_tn_maps<DT><<<(unsigned)nchunks, 256, 0, st>>>(x, chunks, nchunks, threads, s.recs, s.maps, s.exact + 1);
     k_tn_maps_exact<DT><<<(unsigned)(nchunks < 256 ? nchunks : 256), 256, 0, st>>>(x, chunks, nchunks, threads, s.recs, s.maps,
