@@ -1,14 +1,37 @@
-# rocprofv3 over the bench workload: kernel trace + stats (the bench line printed under the profiler is
-# kept next to it), then FETCH_SIZE and WRITE_SIZE in separate PMC passes, then kernel traces of the
-# C3 bucketed and stochastic config benches.
+#!/bin/bash
+# Kernel trace and HBM traffic of any workload, on the GPU box: rocprofv3 --kernel-trace --stats, then separate
+# FETCH_SIZE and WRITE_SIZE passes (counters only in their own runs), summarised per kernel and grid by
+# tools/pmc_kernels.py (with the guide's gfx950 FETCH_SIZE correction).
+#
+#   tools/gpu_prof.sh NAME [--no-pmc] [--secs S] -- python3 tools/ref_norm_prof.py --cfg c2 --reps 3
+#
+# Writes gpurun_out/prof_NAME/{trace,fetch,write}/ and pmc_traffic.json; the program runs from the repo root
+# (put it right after "--": python3 ..., never env / bash -c). Stops at the first failing step.
 set -o pipefail
-R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out
-mkdir -p $O
-cd /tmp && export TMPDIR=/tmp
-echo "== trace"; timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_trace -o trace -- python3 $R/bench.py --steps 50 --warmup 10 --no-cpu-baseline --pmc off > $O/prof_trace.log 2>&1; rc=$?; grep '"metric"' $O/prof_trace.log; [ $rc -eq 0 ] || exit $rc
-echo "== fetch"; timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/prof_fetch -o fetch -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --pmc off > $O/prof_fetch.log 2>&1; rc=$?; [ $rc -eq 0 ] || exit $rc
-echo "== write"; timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/prof_write -o write -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --pmc off > $O/prof_write.log 2>&1; rc=$?; [ $rc -eq 0 ] || exit $rc
-echo "== c3 trace"; timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c3 -o c3 -- python3 $R/tools/bench_configs.py --mode c3 --steps 50 --warmup 5 > $O/prof_c3.log 2>&1; rc=$?; grep '"metric"' $O/prof_c3.log; [ $rc -eq 0 ] || exit $rc
-echo "== stoch trace"; timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_stoch -o stoch -- python3 $R/tools/bench_configs.py --mode stoch --steps 20 --warmup 3 > $O/prof_stoch.log 2>&1; rc=$?; [ $rc -eq 0 ] || exit $rc
-find $O/prof_trace $O/prof_fetch $O/prof_write $O/prof_c3 $O/prof_stoch -name "*.csv" | head -30
+name=$1
+shift
+pmc=1
+secs=300
+while [ $# -gt 0 ] && [ "$1" != "--" ]; do
+  case $1 in
+    --no-pmc) pmc=0 ;;
+    --secs) secs=$2; shift ;;
+    *) echo "unknown option $1" >&2; exit 2 ;;
+  esac
+  shift
+done
+[ "$1" = "--" ] && shift
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/prof_$name
+mkdir -p "$O"
+export TMPDIR=/tmp
+cd "$R" || exit 1
+timeout -k 10 "$secs" rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace" -o trace -- "$@" > "$O/trace.log" 2>&1 || exit $?
+if [ $pmc = 1 ]; then
+  timeout -k 10 "$secs" rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/fetch" -o fetch -- "$@" > "$O/fetch.log" 2>&1 || exit $?
+  timeout -k 10 "$secs" rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/write" -o write -- "$@" > "$O/write.log" 2>&1 || exit $?
+  f=$(find "$O/fetch" -name "*counter_collection.csv" | head -1)
+  g=$(find "$O/write" -name "*counter_collection.csv" | head -1)
+  python3 tools/pmc_kernels.py "$f" "$g" > "$O/pmc_traffic.json" || exit $?
+fi
+find "$O" -name "*kernel_stats.csv"
