@@ -22,7 +22,6 @@ Contract kept from the reference:
 There is no CPU fallback: without a GPU and the built HIP library these methods raise.
 """
 
-import math
 import os
 import threading
 import time
@@ -32,7 +31,7 @@ from typing import Dict, List, Optional, Tuple
 import numpy as np
 import torch
 
-from .. import hostcopy, ops, sum_order
+from .. import hostcopy, ops, qerror, sum_order
 from ..model import (CompressedParameters, Parameters, QuantParameter, QuantParameters, get_parameter_info)
 from .channel import Channel, IdentityChannel
 
@@ -332,6 +331,16 @@ def _host_scales(amax_bits: np.ndarray, bits: int) -> np.ndarray:
     return (amax_bits.view(np.float32) / np.float32((1 << (bits - 1)) - 1)).astype(np.float32)
 
 
+def _qerror_sums(x_dev: torch.Tensor, d_dev: torch.Tensor, lay: ops.BucketLayout):
+    """The reference's q-error sums of a bucket against its decode (qerror.reference_sums): over the
+    tensors back to back, so a padded layout (int4 buckets: align 2) is compacted first."""
+    sizes = lay.sizes.tolist()
+    if (lay.offsets != np.concatenate([[0], np.cumsum(lay.sizes)[:-1]])).any():
+        x_dev = torch.cat([x_dev[o:o + n] for o, n in zip(lay.offsets.tolist(), sizes)])
+        d_dev = torch.cat([d_dev[o:o + n] for o, n in zip(lay.offsets.tolist(), sizes)])
+    return qerror.reference_sums(x_dev, d_dev, sizes)
+
+
 def _encode_host_dict(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _DeviceStaging, bits: int,
                       stats: Optional[list], emit, idle):
     """The all-CPU fp32 dict's encode with its outputs built in the shadow of the copies.
@@ -384,7 +393,8 @@ def _encode_host_dict(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _D
                                       scales=st.buf("scales", lay.ntensors, torch.float32),
                                       partials=st.buf("partials", lay.nchunks, torch.int32))
     if stats is not None:
-        stats.extend(ops.qerror_batched(x_dev, q_dev, s_dev, lay))
+        stats.append(_qerror_sums(x_dev, ops.decode_batched(q_dev, s_dev, lay, out=st.buf("qe_d", lay.total, torch.float32)),
+                                  lay))
     scales_host = st.buf("scales_host", lay.ntensors, torch.float32, pinned=True)
     scales_host.copy_(s_dev, non_blocking=True)
     scales_ready = torch.cuda.Event()
@@ -428,7 +438,8 @@ def _encode_dict(params: Parameters, names: List[str], bits: int, stats: Optiona
                                       scales=st.buf("scales", lay.ntensors, torch.float32),
                                       partials=st.buf("partials", lay.nchunks, torch.int32))
     if stats is not None:
-        stats.extend(ops.qerror_batched(x_dev, q_dev, s_dev, lay))
+        stats.append(_qerror_sums(x_dev, ops.decode_batched(q_dev, s_dev, lay, out=st.buf("qe_d", lay.total, torch.float32)),
+                                  lay))
     scales_host = st.buf("scales_host", lay.ntensors, torch.float32, pinned=True)
     scales_host.copy_(s_dev, non_blocking=True)
     on_cpu = [not t.is_cuda for t in tensors]
@@ -634,7 +645,8 @@ def _encode_dict_packed(params: Parameters, names: List[str], bits: int, stats: 
                                            scales=st.buf("scales", lay.ntensors, torch.float32),
                                            partials=st.buf("partials", lay.nchunks, torch.int32))
     if stats is not None:
-        stats.extend(ops.qerror_batched_int4(x_dev, p_dev, s_dev, lay))
+        stats.append(_qerror_sums(x_dev, ops.decode_batched_int4(p_dev, s_dev, lay,
+                                                                 out=st.buf("qe_d", lay.total, torch.float32)), lay))
     scales_host = st.buf("scales_host", lay.ntensors, torch.float32, pinned=True)
     scales_host.copy_(s_dev, non_blocking=True)
     torch.cuda.current_stream(dev).synchronize()
@@ -810,19 +822,18 @@ class SLQChannel(Channel):
         Returns (c_params, c_time, q_error_mse, q_error_cos): the values
         Src/ADFL/Client/worker.py:176,186-189 gets from on_client_send, an extra on_server_receive and
         parameter_relative_mse / parameter_cosine_similarity(exclude_bias=True)
-        (Src/ADFL/model.py:256-323). Here the metrics are four fp64 sums taken on the device from the
-        bucket and its payload in the same encode, with no decode and no extra transfer. They agree
-        with the reference's fp32 host reductions to within fp32 summation error (tests use 1e-5
-        relative)."""
+        (Src/ADFL/model.py:256-323), bit for bit: the decode stays on the device (no extra transfer) and
+        the fp32 sums run in torch's CPU order with this process's torch.get_num_threads() (qerror.py).
+        c_time covers the encode only, as on_client_send's does."""
         s_time = time.perf_counter()
         stats: list = []
         q_params = self._quantize_params(params, self.bits, stats)
         c_time = time.perf_counter() - s_time
         if not stats:  # nothing quantized: parameter_relative_mse returns 0.0; cosine of empty vectors raises
             raise RuntimeError("send_with_q_error: no ndim > 1 tensors to measure (torch.cat of an empty list)")
-        err, xx, xd, dd = stats
-        rel_mse = err / xx if xx > 0 else 0.0
-        cos = xd / max(math.sqrt(xx * dd), 1e-8)  # torch.nn.functional.cosine_similarity, eps = 1e-8
+        e, s, c = stats[0]
+        count = sum(int(p.numel()) for p in params.values() if p.ndim > 1)
+        rel_mse, cos = qerror.metrics(e, s, c, count)
         return q_params, c_time, rel_mse, cos
 
     def _quantize_params(self, params: Parameters, bits: int, stats: Optional[list] = None) -> QuantParameters:

@@ -8,7 +8,7 @@ SRC_ROOT = os.path.dirname(PKG_DIR)                      # ad-federatedlearning_
 REPO_ROOT = os.path.dirname(SRC_ROOT)
 CSRC = os.path.join(SRC_ROOT, "csrc", "slq_codec.hip")
 SOURCES = [CSRC, os.path.join(SRC_ROOT, "csrc", "stoch_codec.hip"), os.path.join(SRC_ROOT, "csrc", "stoch_dtype.hip"),
-           os.path.join(SRC_ROOT, "csrc", "torch_norm.hip"),
+           os.path.join(SRC_ROOT, "csrc", "torch_norm.hip"), os.path.join(SRC_ROOT, "csrc", "qerror_ref.hip"),
            os.path.join(SRC_ROOT, "csrc", "bucket_copy.hip"), os.path.join(SRC_ROOT, "csrc", "host_copy.cpp")]
 DEPENDS = SOURCES + [os.path.join(SRC_ROOT, "csrc", h) for h in ("cnat_log2_table.h", "cnat_log2_dt_table.h", "philox.h", "torch_sum_order.h", "torch_norm_walk.h")]
 INCLUDE = os.path.join(REPO_ROOT, "include")
@@ -22,7 +22,7 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp
 
 def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(LIB_DIR, exist_ok=True)
-    deps = DEPENDS + [os.path.join(INCLUDE, h) for h in ("adfl_slq.h", "adfl_stoch.h", "adfl_host.h")]
+    deps = DEPENDS + [os.path.join(INCLUDE, h) for h in ("adfl_slq.h", "adfl_stoch.h", "adfl_host.h", "adfl_qerror.h")]
     stamp = LIB_PATH + ".rounds"
     want = os.environ.get("ADFL_PHILOX_ROUNDS", "7")
     built = open(stamp).read().strip() if os.path.exists(stamp) else "7"

@@ -328,3 +328,126 @@ double oracle_torch_l2_norm_f64(const double* x, int64_t n) {
     for (int64_t i = nv; i < n; ++i) b = fma(x[i], x[i], b);
     return sqrt(b);
 }
+
+/* torch.sum(t) of a contiguous fp32 CPU tensor to a scalar, as torch 2.10 computes it (cascade_sum over a
+ * TensorIterator reduced to one output; aten/src/ATen/native/cpu/SumKernel.cpp with 8-float AVX2 vectors,
+ * TensorIteratorReduce.cpp parallel_reduce), restated and pinned against torch itself
+ * (tests/test_qerror_order.py). The reference's q-error metrics take it per tensor,
+ * torch.sum((a - b) ** 2) (Src/ADFL/model.py:266-284), and over the product vector of
+ * cosine_similarity (model.py:302-323).
+ *   level(count)  multi_row_sum's cascade over one column of `count` values: level_power lp =
+ *                 max(4, CeilLog2(count) / 4) (CeilLog2(x) = 1 for x <= 2, else floor(log2(x - 1)) + 1);
+ *                 acc0 adds values in order; after every 2^lp values acc1 += acc0, acc0 = 0, and at every
+ *                 2^(2 lp) acc2 += acc1, acc1 = 0, at every 2^(3 lp) acc3 += acc2, acc2 = 0; at the end
+ *                 ((acc0 + acc1) + acc2) + acc3.
+ *   row(L)        row_sum: four partials (values 4g + p, g < L / 4, each a level() cascade over L / 4), the
+ *                 L % 4 leftovers added to partial 0 in order, then ((p0 + p1) + p2) + p3.
+ *   inner(L)      L >= 8 (vectorized_inner_sum): lane l (0..7) is row() over the L / 8 vectors' element l;
+ *                 0 + the L % 8 trailing values in order, then + lane 0, .., lane 7. L < 8: row(L).
+ *   sum(n, T)     n < 32768 (at::internal::GRAIN_SIZE) or T == 1: 0 + inner(n). Otherwise the two-pass
+ *                 reduction: at::parallel_for's split (nt = min(T, ceil(n / 32768)) ranges of ceil(n / nt)),
+ *                 buffer[t] = 0 + inner(range t) for each range, zeros in the other T - nt slots, and the
+ *                 result 0 + inner over the T buffer values. T is torch.get_num_threads() of the caller. */
+static int level_power(int64_t count) {
+    int c = 1;
+    if (count > 2) {
+        uint64_t v = (uint64_t)count - 1;
+        c = 0;
+        while (v) { ++c; v >>= 1; }
+    }
+    return c / 4 > 4 ? c / 4 : 4;
+}
+
+static float level_sum(const float* d, int64_t count, int64_t stride) {
+    const int lp = level_power(count);
+    const int64_t step = (int64_t)1 << lp, mask = step - 1;
+    float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    int64_t i = 0;
+    while (i + step <= count) {
+        for (int64_t j = 0; j < step; ++j, ++i) acc[0] = acc[0] + d[i * stride];
+        for (int j = 1; j < 4; ++j) {
+            acc[j] = acc[j] + acc[j - 1];
+            acc[j - 1] = 0.0f;
+            if ((i & (mask << (j * lp))) != 0) break;
+        }
+    }
+    for (; i < count; ++i) acc[0] = acc[0] + d[i * stride];
+    for (int j = 1; j < 4; ++j) acc[0] = acc[0] + acc[j];
+    return acc[0];
+}
+
+static float row_sum_f(const float* d, int64_t n, int64_t stride) {
+    const int64_t g = n / 4;
+    float p[4];
+    for (int k = 0; k < 4; ++k) p[k] = level_sum(d + k * stride, g, 4 * stride);
+    for (int64_t i = 4 * g; i < n; ++i) p[0] = p[0] + d[i * stride];
+    for (int k = 1; k < 4; ++k) p[0] = p[0] + p[k];
+    return p[0];
+}
+
+static float inner_sum_f(const float* d, int64_t n) {
+    if (n < 8) return row_sum_f(d, n, 1);
+    const int64_t v = n / 8;
+    float acc = 0.0f;
+    for (int64_t i = 8 * v; i < n; ++i) acc = acc + d[i];
+    for (int l = 0; l < 8; ++l) acc = acc + row_sum_f(d + l, v, 8);
+    return acc;
+}
+
+float oracle_torch_sum_f32(const float* x, int64_t n, int32_t threads) {
+    if (n < 32768 || threads <= 1) return 0.0f + inner_sum_f(x, n);
+    int64_t nt = (n + 32767) / 32768;
+    if (nt > threads) nt = threads;
+    const int64_t cs = (n + nt - 1) / nt;
+    float* buf = (float*)calloc((size_t)threads, sizeof(float));
+    for (int64_t t = 0; t < nt; ++t) {
+        const int64_t b = t * cs;
+        if (b < n) buf[t] = 0.0f + inner_sum_f(x + b, (cs < n - b ? cs : n - b));
+    }
+    const float r = 0.0f + inner_sum_f(buf, threads);
+    free(buf);
+    return r;
+}
+
+/* The reference's q-error metrics of an update x against its decode d (Src/ADFL/Client/worker.py:186-189:
+ * parameter_relative_mse and parameter_cosine_similarity with exclude_bias=True, Src/ADFL/model.py:256-323),
+ * for the ndim > 1 tensors given back to back in x / d (sizes[t] elements each, dict order):
+ *   e[t] = torch.sum((x_t - d_t) ** 2), s[t] = torch.sum((x_t - 0) ** 2)   (fp32, the order above)
+ *   *cos = torch.sum((x / max(|x|, 1e-8)) * (d / max(|d|, 1e-8)))           (F.cosine_similarity, dim=0)
+ * with |.| the reference-order fp32 norm (oracle_torch_l2_norm) and max the NaN-propagating clamp_min.
+ * The caller forms the Python doubles: mse = sum(float(e[t])) / N etc. */
+void oracle_qerror_ref(const float* x, const float* d, const int64_t* sizes, int32_t ntensors, int32_t threads,
+                       float* e, float* s, float* cos_out) {
+    int64_t total = 0, mx = 0;
+    for (int32_t t = 0; t < ntensors; ++t) {
+        total += sizes[t];
+        if (sizes[t] > mx) mx = sizes[t];
+    }
+    float* tmp = (float*)malloc(sizeof(float) * (size_t)(total > 0 ? total : 1));
+    int64_t off = 0;
+    for (int32_t t = 0; t < ntensors; ++t) {
+        const int64_t n = sizes[t];
+        for (int64_t i = 0; i < n; ++i) {
+            const float df = x[off + i] - d[off + i];
+            tmp[i] = df * df;
+        }
+        e[t] = oracle_torch_sum_f32(tmp, n, threads);
+        for (int64_t i = 0; i < n; ++i) {
+            const float a = x[off + i] - 0.0f;
+            tmp[i] = a * a;
+        }
+        s[t] = oracle_torch_sum_f32(tmp, n, threads);
+        off += n;
+    }
+    float n1 = oracle_torch_l2_norm(x, total), n2 = oracle_torch_l2_norm(d, total);
+    const float eps = 1e-8f;
+    if (!(n1 != n1) && n1 < eps) n1 = eps;
+    if (!(n2 != n2) && n2 < eps) n2 = eps;
+    for (int64_t i = 0; i < total; ++i) {
+        const float a = x[i] / n1, b = d[i] / n2;
+        tmp[i] = a * b;
+    }
+    *cos_out = oracle_torch_sum_f32(tmp, total, threads);
+    free(tmp);
+    (void)mx;
+}

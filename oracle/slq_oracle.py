@@ -62,6 +62,8 @@ def lib():
         L.oracle_torch_sum_col.argtypes, L.oracle_torch_sum_col.restype = [P, I32, I64, I64], F
         L.oracle_torch_mean_rows.argtypes, L.oracle_torch_mean_rows.restype = [P, I32, I64, P], None
         L.oracle_torch_sum_rows.argtypes, L.oracle_torch_sum_rows.restype = [P, I32, I64, P], None
+        L.oracle_torch_sum_f32.argtypes, L.oracle_torch_sum_f32.restype = [P, I64, I32], F
+        L.oracle_qerror_ref.argtypes, L.oracle_qerror_ref.restype = [P, P, P, I32, I32, P, P, P], None
         _lib = L
     return _lib
 
@@ -238,3 +240,40 @@ def aten_encode(t, bits: int):
 def aten_decode(q):
     """Src/ADFL/Channel/quant.py:110."""
     return q.dequantize()
+
+
+def torch_sum_f32(x: np.ndarray, threads: int) -> float:
+    """torch.sum of a contiguous fp32 tensor to a scalar, in torch 2.10's CPU order with `threads` threads
+    (slq_oracle.c oracle_torch_sum_f32)."""
+    x = np.ascontiguousarray(x, dtype=np.float32).reshape(-1)
+    return float(lib().oracle_torch_sum_f32(_ptr(x), x.size, int(threads)))
+
+
+def qerror_sums(xs, ds, threads: int):
+    """Per-tensor fp32 sums e[t] = sum((x - d)^2), s[t] = sum(x^2) and the fp32 cosine sum over the
+    concatenation (slq_oracle.c oracle_qerror_ref) for the ndim > 1 tensors xs / their decodes ds."""
+    sizes = np.array([np.asarray(x).size for x in xs], dtype=np.int64)
+    x = np.ascontiguousarray(np.concatenate([np.asarray(a, np.float32).reshape(-1) for a in xs]))
+    d = np.ascontiguousarray(np.concatenate([np.asarray(a, np.float32).reshape(-1) for a in ds]))
+    e = np.zeros(len(xs), np.float32)
+    s = np.zeros(len(xs), np.float32)
+    c = np.zeros(1, np.float32)
+    lib().oracle_qerror_ref(_ptr(x), _ptr(d), _ptr(sizes), len(xs), int(threads), _ptr(e), _ptr(s), _ptr(c))
+    return e, s, float(c[0])
+
+
+def qerror_metrics(xs, ds, threads: int):
+    """(parameter_relative_mse, parameter_cosine_similarity) as the reference returns them
+    (Src/ADFL/model.py:256-323, exclude_bias=True over the ndim > 1 tensors xs, in dict order): Python-double
+    sums of the fp32 per-tensor sums, each divided by the element count, then their ratio."""
+    e, s, c = qerror_sums(xs, ds, threads)
+    n = sum(int(np.asarray(x).size) for x in xs)
+    num = 0.0
+    den = 0.0
+    for v in e.tolist():
+        num += v
+    for v in s.tolist():
+        den += v
+    num = num / n if n > 0 else 0.0
+    den = den / n if n > 0 else 0.0
+    return (num / den if den > 0 else 0.0), c

@@ -25,7 +25,7 @@ def declared_functions():
 
 
 def test_headers_present():
-    assert [os.path.basename(h) for h in HEADERS] == ["adfl_host.h", "adfl_slq.h", "adfl_stoch.h"]
+    assert [os.path.basename(h) for h in HEADERS] == ["adfl_host.h", "adfl_qerror.h", "adfl_slq.h", "adfl_stoch.h"]
 
 
 def test_header_declares_the_binding_table():

@@ -146,17 +146,18 @@ def test_stoch_receive_mean_of_reference_payloads(codec):
 
 @pytest.mark.parametrize("bits", [8, 4])
 def test_send_with_q_error_vs_reference(bits):
+    """The worker's q-error metrics (Src/ADFL/Client/worker.py:186-189) equal the reference's Python doubles
+    bit for bit on every client, NaN / inf clients included (qerror.py, csrc/qerror_ref.hip)."""
     _, m = fixture()
     ch = SLQChannel(bits)
-    checked = 0
-    for c in range(len(m["clients"])):
-        ref = m["q_error"][f"slq{bits}_c{c}"]
-        rmse, rcos = float(ref["mse"]), float(ref["cos"])
-        _, _, mse, cos = ch.send_with_q_error(client_dict(c))
-        if not (np.isfinite(rmse) and np.isfinite(rcos)):
-            assert np.isnan(mse) == np.isnan(rmse) and np.isnan(cos) == np.isnan(rcos), (c, mse, rmse, cos, rcos)
-            continue
-        assert abs(mse - rmse) <= 1e-5 * abs(rmse), (c, mse, rmse)
-        assert abs(cos - rcos) <= 1e-5, (c, cos, rcos)
-        checked += 1
-    assert checked >= 50
+    same = lambda a, b: (np.isnan(a) and np.isnan(b)) or a == b  # noqa: E731
+    old = torch.get_num_threads()
+    torch.set_num_threads(8)  # the generator's (tests/golden/make_golden_aggregate.py)
+    try:
+        for c in range(len(m["clients"])):
+            ref = m["q_error"][f"slq{bits}_c{c}"]
+            rmse, rcos = float(ref["mse"]), float(ref["cos"])
+            _, _, mse, cos = ch.send_with_q_error(client_dict(c))
+            assert same(mse, rmse) and same(cos, rcos), (c, mse, rmse, cos, rcos)
+    finally:
+        torch.set_num_threads(old)

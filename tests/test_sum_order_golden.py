@@ -10,9 +10,7 @@ against the reference executed in place (tests/golden/aggregate.npz, make_golden
   stack([received..., own]).mean(0) (Examples/ray_ad.py:183-188) with the receiver's update exact;
 * the oracle's decodes of the reference's own QSGD / RQSGD / CNAT payloads, averaged in torch's order,
   equal simple_aggregate of the reference's decodes at K = 5, 8, 16, 20;
-* an fp64 restatement of the q-error metrics (what SLQChannel.send_with_q_error computes on the device)
-  is within 1e-5 of the reference's parameter_relative_mse / parameter_cosine_similarity (executed; they
-  reduce in fp32)."""
+* the q-error metrics (torch.sum to a scalar, cosine_similarity) are pinned in tests/test_qerror_order.py."""
 
 import json
 import os
@@ -152,40 +150,6 @@ def test_stochastic_mean_of_reference_payloads(codec):
     for k in m["k_stoch"]:
         for n in SHAPES:
             assert same_f32(oracle.torch_mean_rows([dec[c][n] for c in range(k)]), a[f"{codec}__k{k}__{n}"]), (k, n)
-
-
-def qerror_fp64(x: dict, d: dict):
-    """send_with_q_error's metrics in fp64 (k_qerror_batched's four sums): relative MSE and cosine."""
-    err = xx = xd = dd = 0.0
-    for n in SHAPES:
-        xv = x[n].reshape(-1).astype(np.float64)
-        dv = d[n].reshape(-1).astype(np.float64)
-        e = (x[n].reshape(-1) - d[n].reshape(-1)).astype(np.float64)   # fp32 difference, as (a - b)
-        err += float(np.sum(e * e))
-        xx += float(np.sum(xv * xv))
-        xd += float(np.sum(xv * dv))
-        dd += float(np.sum(dv * dv))
-    return err / xx if xx > 0 else 0.0, xd / max(np.sqrt(xx * dd), 1e-8)
-
-
-@pytest.mark.parametrize("bits", [8, 4])
-def test_qerror_restatement_vs_reference(bits):
-    _, m = fixture()
-    checked = 0
-    for c in range(len(m["clients"])):
-        ref = m["q_error"][f"slq{bits}_c{c}"]
-        rmse, rcos = float(ref["mse"]), float(ref["cos"])
-        x, dec = _slq_decoded(bits, c)
-        mse, cos = qerror_fp64(x, {n: dec[n][2] for n in SHAPES})
-        if not (np.isfinite(rmse) and np.isfinite(rcos)):   # the NaN / inf clients: non-finite on both sides
-            assert np.isnan(mse) == np.isnan(rmse) and np.isnan(cos) == np.isnan(rcos), (c, mse, rmse, cos, rcos)
-            continue
-        # the reference reduces in fp32 (torch.sum per tensor, cosine_similarity on fp32 vectors): its own
-        # rounding error is what separates the two (observed <= 2e-6); the bar is 1e-5
-        assert abs(mse - rmse) <= 1e-5 * abs(rmse), (c, mse, rmse)
-        assert abs(cos - rcos) <= 1e-5, (c, cos, rcos)
-        checked += 1
-    assert checked >= 50
 
 
 def test_host_sum_rows_equals_torch_per_entry():
