@@ -219,6 +219,61 @@ def _stage_in(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _DeviceSta
 _PIPELINE = os.environ.get("ADFL_HOST_PIPELINE", "1") != "0"
 
 
+class PhaseClock:
+    """Wall milliseconds the calling thread spends in each phase of the host-to-host path (exclusive, no extra
+    synchronisation): filled while a `phase_clock()` block is active, e.g. bench.py's channel_c3_dict."""
+
+    def __init__(self):
+        self.ms: Dict[str, float] = {}
+
+
+_CLOCK: Optional[PhaseClock] = None
+
+
+class _Phase:
+    __slots__ = ("name", "t0")
+
+    def __init__(self, name: str):
+        self.name = name
+
+    def __enter__(self):
+        self.t0 = time.perf_counter()
+
+    def __exit__(self, *exc):
+        c = _CLOCK
+        if c is not None:
+            c.ms[self.name] = c.ms.get(self.name, 0.0) + (time.perf_counter() - self.t0) * 1e3
+
+
+class _NoPhase:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *exc):
+        return None
+
+
+_NO_PHASE = _NoPhase()
+
+
+def _ph(name: str):
+    return _NO_PHASE if _CLOCK is None else _Phase(name)
+
+
+class phase_clock:
+    """`with phase_clock() as c:` — c.ms holds the phase split of the channel calls made inside."""
+
+    def __enter__(self) -> PhaseClock:
+        global _CLOCK
+        self.prev = _CLOCK
+        _CLOCK = PhaseClock()
+        return _CLOCK
+
+    def __exit__(self, *exc):
+        global _CLOCK
+        _CLOCK = self.prev
+
+
 class _PendingD2H:
     """D2H of a device bucket into the reused pinned staging, enqueued range by range with an event each;
     finish() scatters every range into the per-tensor CPU storages as soon as its copy lands (the native
@@ -258,24 +313,30 @@ class _PendingD2H:
         k = 0
         try:
             for (lo, hi), ev in zip(self.ranges, self.events):
-                while k < count and offs[k] < hi:   # every tensor the range [lo, hi) touches starts below hi
-                    t = make(k)
-                    if t.is_cuda or not t.is_contiguous() or t.element_size() != es:
-                        raise ValueError("staging: outputs must be contiguous CPU tensors of the bucket's element size")
-                    if t.numel() * es >= (4 << 20):
-                        hostcopy.advise_huge([t])
-                    ptrs[k] = t.data_ptr()
-                    outs.append(t)
-                    k += 1
-                ev.synchronize()   # usually landed already: the outputs took longer than the copy
-                pending.append(hostcopy.submit_pieces(*_range_copies(ptrs, lay, base, es, lo, hi, to_bucket=False),
-                                                      stream=True, keep=self.host))
+                with _ph("out.alloc"):
+                    while k < count and offs[k] < hi:   # every tensor the range [lo, hi) touches starts below hi
+                        t = make(k)
+                        if t.is_cuda or not t.is_contiguous() or t.element_size() != es:
+                            raise ValueError("staging: outputs must be contiguous CPU tensors of the bucket's "
+                                             "element size")
+                        if t.numel() * es >= (4 << 20):
+                            hostcopy.advise_huge([t])
+                        ptrs[k] = t.data_ptr()
+                        outs.append(t)
+                        k += 1
+                with _ph("out.d2h_wait"):
+                    ev.synchronize()   # usually landed already: the outputs took longer than the copy
+                with _ph("out.scatter_submit"):
+                    pending.append(hostcopy.submit_pieces(*_range_copies(ptrs, lay, base, es, lo, hi,
+                                                                         to_bucket=False),
+                                                          stream=True, keep=self.host))
             while k < count:   # tensors past the last range (none for a bucket layout; kept for safety)
                 outs.append(make(k))
                 k += 1
         finally:
-            for pd in pending:
-                pd.wait()
+            with _ph("out.scatter_wait"):
+                for pd in pending:
+                    pd.wait()
         return outs
 
     def finish(self, outs: List[torch.Tensor]) -> None:
@@ -352,7 +413,8 @@ def _encode_host_dict(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _D
     objects). Then one encode launch, the payload D2H range by range with the native scatter behind it. The
     device's scales are checked against the host's (a mismatch rebuilds that output with the device's, which
     the payload was quantized with). Returns [(q, scale)] per tensor."""
-    _host_heap(lay)
+    with _ph("enc.heap"):
+        _host_heap(lay)
     dev = st.device
     stream = torch.cuda.current_stream(dev)
     x_dev = st.buf("x", lay.total, torch.float32)
@@ -362,11 +424,13 @@ def _encode_host_dict(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _D
     ptrs = _ptrs(tensors)
     ranges = _ranges(lay, 4)
     jobs = []
-    for lo, hi in ranges:
-        plan = _plan(lay, lo, hi)
-        b_ptr, t_ptr, nb = plan.copies(ptrs, host.data_ptr(), 4, True)
-        jobs.append(hostcopy.submit_pieces(b_ptr, t_ptr, nb, absmax_ptrs=np.uint64(a_base) + plan.ku * np.uint64(4),
-                                           keep=(host, amax)))
+    with _ph("enc.gather_submit"):
+        for lo, hi in ranges:
+            plan = _plan(lay, lo, hi)
+            b_ptr, t_ptr, nb = plan.copies(ptrs, host.data_ptr(), 4, True)
+            jobs.append(hostcopy.submit_pieces(b_ptr, t_ptr, nb,
+                                               absmax_ptrs=np.uint64(a_base) + plan.ku * np.uint64(4),
+                                               keep=(host, amax)))
     ends = lay.offsets + lay.sizes
     eaq, qint8 = torch._empty_affine_quantized, torch.qint8
     outs: List[torch.Tensor] = []
@@ -374,24 +438,29 @@ def _encode_host_dict(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _D
     made = 0
     try:
         for (lo, hi), job in zip(ranges, jobs):
-            job.wait()
-            x_dev[lo:hi].copy_(host[lo:hi], non_blocking=True)
+            with _ph("enc.gather_absmax_wait"):
+                job.wait()
+            with _ph("enc.h2d_enqueue"):
+                x_dev[lo:hi].copy_(host[lo:hi], non_blocking=True)
             done = int(np.searchsorted(ends, hi, side="right"))   # tensors whose every byte is staged
             if done > made:
-                scales[made:done] = _host_scales(amax[made:done], bits)
-                for k in range(made, done):
-                    sc = float(scales[k])
-                    q = eaq(tensors[k].shape, scale=sc, zero_point=0, dtype=qint8)
-                    outs.append(q)
-                    emit(k, q, sc)
+                with _ph("enc.outputs"):
+                    scales[made:done] = _host_scales(amax[made:done], bits)
+                    for k in range(made, done):
+                        sc = float(scales[k])
+                        q = eaq(tensors[k].shape, scale=sc, zero_point=0, dtype=qint8)
+                        outs.append(q)
+                        emit(k, q, sc)
                 made = done
-            idle()
+            with _ph("enc.passthrough"):
+                idle()
     finally:
         for j in jobs:
             j.wait()
-    q_dev, s_dev = ops.encode_batched(x_dev, lay, bits, q=st.buf("q", lay.total, torch.int8),
-                                      scales=st.buf("scales", lay.ntensors, torch.float32),
-                                      partials=st.buf("partials", lay.nchunks, torch.int32))
+    with _ph("enc.kernel_launch"):
+        q_dev, s_dev = ops.encode_batched(x_dev, lay, bits, q=st.buf("q", lay.total, torch.int8),
+                                          scales=st.buf("scales", lay.ntensors, torch.float32),
+                                          partials=st.buf("partials", lay.nchunks, torch.int32))
     if stats is not None:
         stats.append(_qerror_sums(x_dev, ops.decode_batched(q_dev, s_dev, lay, out=st.buf("qe_d", lay.total, torch.float32)),
                                   lay))
@@ -399,10 +468,13 @@ def _encode_host_dict(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _D
     scales_host.copy_(s_dev, non_blocking=True)
     scales_ready = torch.cuda.Event()
     scales_ready.record(stream)
-    pending = _PendingD2H(q_dev, lay, st, "q")
-    while idle():   # the caller's remaining objects while the kernel and the D2H run
-        pass
-    pending.finish(outs)
+    with _ph("enc.d2h_enqueue"):
+        pending = _PendingD2H(q_dev, lay, st, "q")
+    with _ph("enc.passthrough"):
+        while idle():   # the caller's remaining objects while the kernel and the D2H run
+            pass
+    with _ph("enc.d2h_wait_scatter"):
+        pending.finish(outs)
     scales_ready.synchronize()
     dev_scales = scales_host.numpy()
     bad = np.nonzero(dev_scales.view(np.uint32) != scales.view(np.uint32))[0]
@@ -498,11 +570,14 @@ def _decode_dict(items: List[Tuple[str, torch.Tensor]]) -> Dict[str, torch.Tenso
     # host payloads are gathered byte-wise from their storages, device ones by one gather launch: neither
     # needs an int8 view object per tensor
     qs = [q if all_host or all_dev else _int8_view(q) for _, q in items]
-    q_dev = _stage_in(qs, lay, st, "dq", torch.int8)
-    # q_scale() is a double; fbgemm's dequantize uses it as fp32 (quant.py:110), so round it the same way
-    s_dev = torch.tensor([q.q_scale() for _, q in items], dtype=torch.float32).to(dev, non_blocking=True)
+    with _ph("dec.gather_h2d"):
+        q_dev = _stage_in(qs, lay, st, "dq", torch.int8)
+    with _ph("dec.scales"):
+        # q_scale() is a double; fbgemm's dequantize uses it as fp32 (quant.py:110), so round it the same way
+        s_dev = torch.tensor([q.q_scale() for _, q in items], dtype=torch.float32).to(dev, non_blocking=True)
     on_cpu = [not q.is_cuda for _, q in items]
-    out_dev = ops.decode_batched(q_dev, s_dev, lay, out=st.buf("d_out", lay.total, torch.float32))
+    with _ph("dec.kernel_launch"):
+        out_dev = ops.decode_batched(q_dev, s_dev, lay, out=st.buf("d_out", lay.total, torch.float32))
     decoded = _hand_out(out_dev, lay, [q.shape for _, q in items], on_cpu, st, "d_out")
     return {name: t for (name, _), t in zip(items, decoded)}
 
@@ -585,6 +660,23 @@ def _simple_aggregate(values: List[torch.Tensor]) -> torch.Tensor:
     """One entry of simple_aggregate (Src/ADFL/model.py:221-234), as the reference computes it."""
     with torch.no_grad():
         return torch.sum(torch.stack(values, dim=0), dim=0) / len(values)
+
+
+def device_mean_order_ok() -> bool:
+    """The device mean kernels follow torch's CPU sum(dim=0) order as ATen's AVX2 kernel takes it
+    (csrc/torch_sum_order.h). If this process's torch sums in another order (sum_order.self_check fails:
+    another torch build or CPU kernel), receive_mean decodes and aggregates every entry on the host the
+    reference's way instead, so the device and host halves of one aggregate never disagree; warned once."""
+    ok = sum_order.self_check()
+    if not ok and not _ORDER_WARNED[0]:
+        _ORDER_WARNED[0] = True
+        import warnings
+        warnings.warn("adfl_amd: this torch's CPU sum order differs from the one the device mean kernels "
+                      "restate; receive_mean aggregates on the host (bit-identical, slower)", RuntimeWarning)
+    return ok
+
+
+_ORDER_WARNED = [False]
 
 
 def _aggregate_entries(names: List[str], parts: List[Parameters]) -> Dict[str, torch.Tensor]:
@@ -780,7 +872,7 @@ class SLQChannel(Channel):
         s_time = time.perf_counter()
         names = list(all_c_params[0].params.keys())
         fused = [n for n in names if all(n in c.params and self._fusable(c.params[n]) for c in all_c_params)
-                 and len({tuple(c.params[n].shape) for c in all_c_params}) == 1]
+                 and len({tuple(c.params[n].shape) for c in all_c_params}) == 1] if device_mean_order_ok() else []
         out: Parameters = {}
         if fused:
             decoded = self._mean_payloads(all_c_params, fused)

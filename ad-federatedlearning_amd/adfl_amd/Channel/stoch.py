@@ -43,7 +43,8 @@ from .. import hostcopy, ops
 from .. import stoch as sops
 from ..model import CompressedParameters, Parameters, QuantParameter, QuantParameters, get_parameter_info
 from .channel import Channel, IdentityChannel
-from .quant import _PendingD2H, _aggregate_entries, _hand_out, _serialized, _stage_in, _stage_rows, _staging
+from .quant import (_PendingD2H, _aggregate_entries, _hand_out, _serialized, _stage_in, _stage_rows, _staging,
+                    device_mean_order_ok)
 
 _CODECS = ("qsgd", "rqsgd", "cnat")
 
@@ -378,7 +379,7 @@ class _StochChannel(Channel):
         s_time = time.perf_counter()
         names = list(all_c_params[0].params.keys())
         fused = [n for n in names if all(n in c.params and self._fusable(c.params[n]) for c in all_c_params)
-                 and len({tuple(c.params[n].data.shape) for c in all_c_params}) == 1]
+                 and len({tuple(c.params[n].data.shape) for c in all_c_params}) == 1] if device_mean_order_ok() else []
         out: Parameters = {}
         if fused:
             out.update(zip(fused, _decode_mean_stoch(all_c_params, fused, self.CODEC, self.bits)))

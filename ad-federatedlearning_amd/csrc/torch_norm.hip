@@ -210,34 +210,75 @@ __device__ __forceinline__ Map lane_map_exact(const E (&v)[kLane], int g) {
   return Map{se, so - 1.0};
 }
 
+// Lane maps on grids g and g + d (d = +1 or -1) in one pass. SQ (bf16 / fp16 inputs): x^2 has at most 22
+// significant bits, so hi = x^2 / u is exact in fp32 and its fraction decides ties: fp32 / int32 arithmetic,
+// no fp64 (a square that underflows is far below 1/2: no tie, increment 0). Otherwise lane_map_exact twice.
+__device__ __forceinline__ float pow2f(int k) { return __int_as_float((k + 127) << 23); }
+__device__ __forceinline__ void sq_step(float h, int& e, int& o) {
+  const float k = (h + 12582912.0f) - 12582912.0f;  // rint, |h| < 2^22
+  const float fr = h - k;
+  const bool tie = __builtin_fabsf(fr) == 0.5f;
+  const int ki = (int)k - ((tie && fr < 0.0f) ? 1 : 0);
+  e += ki;
+  o += ki;
+  if (tie) {
+    e += e & 1;
+    o += o & 1;
+  }
+}
+template <bool W, bool SQ, typename E>
+__device__ __forceinline__ void lane_maps_pair(const E (&v)[kLane], int g, int d, Map& m0, Map& m1) {
+  if constexpr (!W && SQ) {
+    const int s = 23 - g;
+    const float sa = pow2f(s >> 1), sb = (s & 1) ? 2.0f : 1.0f, sd = d > 0 ? 0.5f : 2.0f;
+    int e0 = 0, o0 = 1, e1 = 0, o1 = 1;
+    bool big0 = false, big1 = false;
+#pragma unroll
+    for (int i = 0; i < kLane; ++i) {
+      const float xs = (float)v[i] * sa;
+      const float h0 = xs * xs * sb, h1 = h0 * sd;
+      big0 |= !(h0 < 0x1p21f);  // NaN / inf too: not covered
+      big1 |= !(h1 < 0x1p21f);
+      sq_step(big0 ? 0.0f : h0, e0, o0);
+      sq_step(big1 ? 0.0f : h1, e1, o1);
+    }
+    const double inf = __builtin_inf();
+    m0 = big0 ? Map{inf, inf} : Map{(double)e0, (double)(o0 - 1)};
+    m1 = (big1 || g + d < Acc<W>::kGmin || g + d > Acc<W>::kGmax) ? Map{inf, inf} : Map{(double)e1, (double)(o1 - 1)};
+  } else {
+    m0 = lane_map_exact<W>(v, g);
+    m1 = (g + d < Acc<W>::kGmin || g + d > Acc<W>::kGmax) ? Map{__builtin_inf(), __builtin_inf()} : lane_map_exact<W>(v, g + d);
+  }
+}
+
 // ---- dtype traits
 template <int DT> struct Dt;
 template <> struct Dt<ADFL_DTYPE_F32> {
   using S = float;
   using E = float;
   static constexpr int NC = 8, VB = 8;
-  static constexpr bool kContig = false, kWide = false;
+  static constexpr bool kContig = false, kWide = false, kSq = false;
   __device__ static E ld(const void* x, int64_t i) { return ((const float*)x)[i]; }
 };
 template <> struct Dt<ADFL_DTYPE_BF16> {
   using S = uint16_t;
   using E = float;
   static constexpr int NC = 8, VB = 16;
-  static constexpr bool kContig = false, kWide = false;
+  static constexpr bool kContig = false, kWide = false, kSq = true;
   __device__ static E ld(const void* x, int64_t i) { return __uint_as_float((uint32_t)((const uint16_t*)x)[i] << 16); }
 };
 template <> struct Dt<ADFL_DTYPE_F16> {
   using S = uint16_t;
   using E = float;
   static constexpr int NC = 1, VB = 1;
-  static constexpr bool kContig = true, kWide = false;
+  static constexpr bool kContig = true, kWide = false, kSq = true;
   __device__ static E ld(const void* x, int64_t i) { return __half2float(__ushort_as_half(((const uint16_t*)x)[i])); }
 };
 template <> struct Dt<ADFL_DTYPE_F64> {
   using S = double;
   using E = double;
   static constexpr int NC = 4, VB = 4;
-  static constexpr bool kContig = false, kWide = true;
+  static constexpr bool kContig = false, kWide = true, kSq = false;
   __device__ static E ld(const void* x, int64_t i) { return ((const double*)x)[i]; }
 };
 
@@ -799,8 +840,10 @@ __global__ __launch_bounds__(256) void k_tn_maps_exact(const void* __restrict__ 
             z[i] = (pc == 0 ? e < G.bnd : e >= G.bnd) ? w[i] : (E)0;
           }
           const int g = s_g[pc < npieces ? pc : 0];
-          acc0[pc] = compose(acc0[pc], wave_compose(lane_map_exact<W>(z, g), lane));
-          acc1[pc] = compose(acc1[pc], wave_compose(lane_map_exact<W>(z, g - 1), lane));
+          Map l0, l1;
+          lane_maps_pair<W, D::kSq>(z, g, -1, l0, l1);
+          acc0[pc] = compose(acc0[pc], wave_compose(l0, lane));
+          acc1[pc] = compose(acc1[pc], wave_compose(l1, lane));
         }
       } else {
         const int g = s_g[D::NC == 8 ? row : row / 2];
@@ -811,8 +854,10 @@ __global__ __launch_bounds__(256) void k_tn_maps_exact(const void* __restrict__ 
           const int e = (s0 + lane * kLane + i) * D::NC + c;
           if (e >= G.lim) w[i] = (E)0;
         }
-        const Map m0 = wave_compose(lane_map_exact<W>(w, g), lane);
-        const Map m1 = wave_compose(lane_map_exact<W>(w, g - 1), lane);
+        Map l0, l1;
+        lane_maps_pair<W, D::kSq>(w, g, -1, l0, l1);
+        const Map m0 = wave_compose(l0, lane);
+        const Map m1 = wave_compose(l1, lane);
         if (lane == 0) {
           s_m[wave][h][0] = m0.e;
           s_m[wave][h][1] = m0.o;
@@ -943,6 +988,31 @@ __device__ __forceinline__ typename Acc<Dt<DT>::kWide>::T resolve_segment(const 
     TN_STAT(2, 1);
     const int G = grid_of(acc);
     const double A = a_of(acc);
+    if constexpr (!W && Dt<DT>::kSq) {  // exact-square inputs: the lane maps on G and G + 1 in one pass
+      Map m0, m1;
+      lane_maps_pair<W, true>(v, G, +1, m0, m1);
+      if (lane < start) m0 = Map{0.0, 0.0};
+      const double Al = apply(wave_excl(m0, lane), A);
+      const double out = apply(m0, Al);
+      const unsigned long long ball = __ballot(lane >= start && !(out < Acc<W>::kTop));
+      if (ball == 0ull) return rebuild<W>(__shfl(out, 63, 64), G);
+      const int ls = __builtin_ctzll(ball);
+      A_t a = rebuild<W>(__shfl(Al, ls, 64), G);
+      if (lane == ls) {
+#pragma unroll
+        for (int i = 0; i < kLane; ++i) a = fma_t(v[i], v[i], a);
+      }
+      acc = __shfl(a, ls, 64);
+      start = ls + 1;
+      if (start == 64) return acc;
+      if (__builtin_isfinite(acc) && grid_of(acc) == G + 1) {  // on from lane ls + 1 with the maps on G + 1
+        const Map n1 = lane > ls ? m1 : Map{0.0, 0.0};
+        const double Al1 = apply(wave_excl(n1, lane), a_of(acc));
+        const double out1 = apply(n1, Al1);
+        if (__ballot(lane > ls && !(out1 < Acc<W>::kTop)) == 0ull) return rebuild<W>(__shfl(out1, 63, 64), G + 1);
+      }
+      continue;
+    }
     if constexpr (!W) {
       const double sc = pow2(23 - G);
       double K0 = 0.0, K1 = 0.0;
@@ -1368,7 +1438,7 @@ int launch(const void* x, const adfl_slq_chunk* chunks, int64_t nchunks, int64_t
     k_tn_grids<DT><<<dim3((unsigned)ntensors, 8, 8), 256, 0, st>>>(chunks, nchunks, s.tfirst, threads, s.S, s.wsum, s.recs);
     if (hipError_t e = hipMemsetAsync(s.exact, 0, 4, st)) return (int)e;
     k_tn_maps<DT><<<(unsigned)nchunks, 256, 0, st>>>(x, chunks, nchunks, threads, s.recs, s.maps, s.exact + 1);
-    k_tn_maps_exact<DT><<<(unsigned)(nchunks < 256 ? nchunks : 256), 256, 0, st>>>(x, chunks, nchunks, threads, s.recs, s.maps,
+    k_tn_maps_exact<DT><<<(unsigned)(nchunks < 1024 ? nchunks : 1024), 256, 0, st>>>(x, chunks, nchunks, threads, s.recs, s.maps,
                                                                                    s.exact + 1);
     k_tn_windows<DT><<<dim3((unsigned)ntensors, 8, 8), 256, 0, st>>>(chunks, nchunks, s.tfirst, threads, s.recs, s.maps, s.wing,
                                                                      s.winmaps);

@@ -636,6 +636,21 @@ def extra_pcie(dev, lib, steps: int) -> dict:
     pinned_ok = float(s.item()) == sr and torch.equal(qr.int_repr(), q_h) and torch.equal(qr.dequantize(), out_h)
     del qr, x, q, q2, out, x_h, q_h, out_h
 
+    dict_leg = channel_c3_dict(steps)
+    return {"pinned_1GiB": {"workload": "C2's 1 GiB fp32 from and to pinned host memory (10N bytes over PCIe)",
+                            "steps": steps, "ms_per_round_trip": round(wall * 1e3, 3),
+                            "GiB_per_s": round(n * 4 / GIB / wall, 2), "segments_ms": segs,
+                            "pcie_GBs": round(10 * n / (pcie_ms * 1e-3) / 1e9, 1), "parity": bool(pinned_ok)},
+            "channel_c3_dict": dict_leg}
+
+
+def channel_c3_dict(steps: int) -> dict:
+    """ADFL's own host call pattern on C3: SLQChannel(8).on_client_send then on_server_receive of a CPU
+    state dict of 256 weights (11,689,512 fp32) + 256 biases (Src/ADFL/Client/worker.py:176,
+    Src/ADFL/Server/async_sc.py:209), medians of the calls, with the calling thread's wall time per internal
+    phase (quant.phase_clock: gather + absmax, H2D enqueue, output allocation, D2H wait, scatter, ...;
+    "other" is the rest of the call)."""
+    from adfl_amd.Channel import SLQChannel, quant
     base, rem = divmod(RESNET18_PARAMS, 256)
     g = torch.Generator().manual_seed(11)
     params = {}
@@ -643,19 +658,26 @@ def extra_pcie(dev, lib, steps: int) -> dict:
         params[f"layer{i}.weight"] = torch.randn(1, base + (1 if i < rem else 0), generator=g) * 1e-3
         params[f"layer{i}.bias"] = torch.randn(64, generator=g) * 1e-3
     ch = SLQChannel(8)
-    enc_t, dec_t = [], []
+    enc_t, dec_t, enc_ph, dec_ph = [], [], [], []
     qp = dp = None
     for k in range(3 + max(steps, 10)):
         dp = None  # the previous round's results are released outside the timed calls
         qp = None
-        t1 = time.perf_counter()
-        qp, _ = ch.on_client_send(params)
-        t2 = time.perf_counter()
-        dp, _ = ch.on_server_receive(qp)
-        t3 = time.perf_counter()
+        with quant.phase_clock() as ce:
+            t1 = time.perf_counter()
+            qp, _ = ch.on_client_send(params)
+            t2 = time.perf_counter()
+        with quant.phase_clock() as cd:
+            t3 = time.perf_counter()
+            dp, _ = ch.on_server_receive(qp)
+            t4 = time.perf_counter()
         if k >= 3:
             enc_t.append(t2 - t1)
-            dec_t.append(t3 - t2)
+            dec_t.append(t4 - t3)
+            ce.ms["other"] = (t2 - t1) * 1e3 - sum(ce.ms.values())
+            cd.ms["other"] = (t4 - t3) * 1e3 - sum(cd.ms.values())
+            enc_ph.append(ce.ms)
+            dec_ph.append(cd.ms)
     dict_ok = True
     for name, t in params.items():
         if t.ndim > 1:
@@ -664,19 +686,20 @@ def extra_pcie(dev, lib, steps: int) -> dict:
                 and qp.params[name].data.q_scale() == qr.q_scale() and torch.equal(dp[name], qr.dequantize())
         else:
             dict_ok = dict_ok and torch.equal(dp[name], t)
+
+    def phases(rows):
+        keys = sorted({k for r in rows for k in r})
+        return {k: round(_median([r.get(k, 0.0) for r in rows]), 3) for k in keys}
     e_ms, d_ms = _median(enc_t) * 1e3, _median(dec_t) * 1e3
     gib_dict = sum(t.numel() for t in params.values()) * 4 / GIB
-    return {"pinned_1GiB": {"workload": "C2's 1 GiB fp32 from and to pinned host memory (10N bytes over PCIe)",
-                            "steps": steps, "ms_per_round_trip": round(wall * 1e3, 3),
-                            "GiB_per_s": round(n * 4 / GIB / wall, 2), "segments_ms": segs,
-                            "pcie_GBs": round(10 * n / (pcie_ms * 1e-3) / 1e9, 1), "parity": bool(pinned_ok)},
-            "channel_c3_dict": {"workload": "SLQChannel(8).on_client_send + on_server_receive on a CPU state dict "
-                                            "of 256 weights (11,689,512 fp32) + 256 biases, host to host",
-                                "rounds": len(enc_t), "encode_ms": round(e_ms, 3), "decode_ms": round(d_ms, 3),
-                                "round_trip_ms": round(e_ms + d_ms, 3),
-                                "GiB_per_s": round(gib_dict / ((e_ms + d_ms) * 1e-3), 2),
-                                "statistic": "median of the calls; the previous round's results are freed "
-                                             "before each timed call", "parity": bool(dict_ok)}}
+    return {"workload": "SLQChannel(8).on_client_send + on_server_receive on a CPU state dict "
+                        "of 256 weights (11,689,512 fp32) + 256 biases, host to host",
+            "rounds": len(enc_t), "encode_ms": round(e_ms, 3), "decode_ms": round(d_ms, 3),
+            "round_trip_ms": round(e_ms + d_ms, 3),
+            "GiB_per_s": round(gib_dict / ((e_ms + d_ms) * 1e-3), 2),
+            "phases_ms": {"encode": phases(enc_ph), "decode": phases(dec_ph)},
+            "statistic": "median of the calls (phases: median per phase); the previous round's results are "
+                         "freed before each timed call", "parity": bool(dict_ok)}
 
 
 def extra_stoch_c3(dev, lib, steps: int) -> dict:

@@ -116,3 +116,25 @@ def test_receive_mean_errors():
     u2 = ch.on_client_send({"w": torch.randn(4, 5)})[0]
     with pytest.raises(RuntimeError):   # torch.stack of unequal shapes, as simple_aggregate raises
         ch.receive_mean([u1, u2])
+
+
+@pytest.mark.parametrize("channel", ["SLQChannel", "QSGDChannel"])
+def test_receive_mean_falls_back_when_torch_sums_in_another_order(channel, monkeypatch):
+    """If this torch's CPU sum order is not the one the device mean kernels restate (sum_order.self_check
+    fails), receive_mean aggregates every entry on the host as the reference does — still simple_aggregate
+    of the channel's own decodes, bit for bit — and warns once (the device and host halves of
+    one aggregate must not disagree)."""
+    import importlib
+    from adfl_amd import sum_order
+    from adfl_amd.Channel import quant
+    C = importlib.import_module("adfl_amd.Channel")
+    ch = getattr(C, channel)(8)
+    updates = [ch.on_client_send(_client(r))[0] for r in range(5)]
+    decoded = [ch.on_server_receive(u)[0] for u in updates]
+    want = simple_aggregate(decoded)
+    monkeypatch.setattr(sum_order, "self_check", lambda: False)
+    monkeypatch.setattr(quant, "_ORDER_WARNED", [False])
+    with pytest.warns(RuntimeWarning, match="sum order"):
+        got, _ = ch.receive_mean(updates)
+    for n in want:
+        assert _same(got[n], want[n]), n
