@@ -31,7 +31,7 @@ from typing import Dict, List, Optional, Tuple
 import numpy as np
 import torch
 
-from .. import hostcopy, ops, qerror, sum_order
+from .. import _torchhost, hostcopy, ops, qerror, sum_order
 from ..model import (CompressedParameters, Parameters, QuantParameter, QuantParameters, get_parameter_info)
 from .channel import Channel, IdentityChannel
 
@@ -183,19 +183,21 @@ def _host_heap(lay: ops.BucketLayout) -> None:
 
 
 def _stage_in(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _DeviceStaging, key: str,
-              dtype: torch.dtype) -> torch.Tensor:
-    """The bucket on the device: one gather + one H2D for CPU tensors, one device gather otherwise."""
+              dtype: torch.dtype, host_ptrs: Optional[np.ndarray] = None) -> torch.Tensor:
+    """The bucket on the device: one gather + one H2D for CPU tensors, one device gather otherwise.
+    host_ptrs: the tensors' data pointers when the caller knows them all to be contiguous CPU tensors of the
+    bucket's element size (adfl_torchhost.qint8_meta checked them in one call)."""
     dev_buf = st.buf(key, lay.total, dtype)
-    kinds = {t.is_cuda for t in tensors}
+    kinds = {False} if host_ptrs is not None else {t.is_cuda for t in tensors}
     if kinds == {False}:
         _host_heap(lay)
         host = st.buf(key + "_host", lay.total, dtype, pinned=True)
         es = host.element_size()
-        if all(t.is_contiguous() and t.element_size() == es for t in tensors):
+        if host_ptrs is not None or all(t.is_contiguous() and t.element_size() == es for t in tensors):
             # Native parallel gather (csrc/host_copy.cpp) in element ranges, each range's H2D enqueued as
             # soon as it is staged so the copy engine overlaps the next range's host copy. Pads of an
             # aligned layout are never read.
-            ptrs = _ptrs(tensors)
+            ptrs = _ptrs(tensors) if host_ptrs is None else host_ptrs
             for lo, hi in _ranges(lay, es):
                 hostcopy.copy_pieces(*_range_copies(ptrs, lay, host.data_ptr(), es, lo, hi, to_bucket=True))
                 dev_buf[lo:hi].copy_(host[lo:hi], non_blocking=True)
@@ -292,7 +294,7 @@ class _PendingD2H:
             ev.record(stream)
             self.events.append(ev)
 
-    def finish_building(self, make, count: int) -> List[torch.Tensor]:
+    def finish_building(self, make, count: int, make_batch=None) -> List[torch.Tensor]:
         """Create the `count` outputs (make(k): a fresh contiguous CPU tensor for tensor k of the layout) in
         offset order while the D2H runs, and hand each staging range's scatter to the native pool as soon as
         its copy has landed and every output it touches exists; the pool copies while this thread goes on
@@ -300,6 +302,8 @@ class _PendingD2H:
         once every byte has landed in them. ADFL_HOST_PIPELINE=0: create all, then finish() (the A/B)."""
         lay = self.lay
         offs = lay.offsets
+        if make is None:  # batched creation only: make(k) from it when the slow path needs one
+            make = lambda k: make_batch(k, k + 1)[0][0]  # noqa: E731
         if not _PIPELINE or count != lay.ntensors or (count > 1 and (np.diff(offs) < 0).any()):
             outs = [make(k) for k in range(count)]
             hostcopy.advise_huge(outs)
@@ -314,6 +318,15 @@ class _PendingD2H:
         try:
             for (lo, hi), ev in zip(self.ranges, self.events):
                 with _ph("out.alloc"):
+                    if make_batch is not None:   # the range's new outputs in one native call (adfl_torchhost)
+                        k_end = int(np.searchsorted(offs, hi, side="left"))
+                        if k_end > k:
+                            ts, pt = make_batch(k, k_end)
+                            outs.extend(ts)
+                            ptrs[k:k_end] = pt.numpy().view(np.uint64)
+                            for j in np.nonzero(lay.sizes[k:k_end] * es >= (4 << 20))[0].tolist():
+                                hostcopy.advise_huge([ts[j]])
+                            k = k_end
                     while k < count and offs[k] < hi:   # every tensor the range [lo, hi) touches starts below hi
                         t = make(k)
                         if t.is_cuda or not t.is_contiguous() or t.element_size() != es:
@@ -339,13 +352,15 @@ class _PendingD2H:
                     pd.wait()
         return outs
 
-    def finish(self, outs: List[torch.Tensor]) -> None:
-        """outs: contiguous CPU tensors owned by the caller, tensor k receiving bucket elements at offsets[k]."""
+    def finish(self, outs: List[torch.Tensor], ptrs: Optional[np.ndarray] = None) -> None:
+        """outs: contiguous CPU tensors owned by the caller, tensor k receiving bucket elements at offsets[k].
+        ptrs: their data pointers when the caller made them (adfl_torchhost) and knows them to fit."""
         es = self.host.element_size()
-        for t in outs:
-            if t.is_cuda or not t.is_contiguous() or t.element_size() != es:
-                raise ValueError("staging: outputs must be contiguous CPU tensors of the bucket's element size")
-        ptrs = _ptrs(outs)
+        if ptrs is None:
+            for t in outs:
+                if t.is_cuda or not t.is_contiguous() or t.element_size() != es:
+                    raise ValueError("staging: outputs must be contiguous CPU tensors of the bucket's element size")
+            ptrs = _ptrs(outs)
         for (lo, hi), ev in zip(self.ranges, self.events):
             ev.synchronize()
             hostcopy.copy_pieces(*_range_copies(ptrs, self.lay, self.host.data_ptr(), es, lo, hi, to_bucket=False),
@@ -359,7 +374,7 @@ def _stage_out(dev_buf: torch.Tensor, lay: ops.BucketLayout, st: _DeviceStaging,
 
 
 def _hand_out(out_dev: torch.Tensor, lay: ops.BucketLayout, shapes: List[torch.Size], on_cpu: List[bool],
-              st: _DeviceStaging, key: str) -> List[torch.Tensor]:
+              st: _DeviceStaging, key: str, like: Optional[List[torch.Tensor]] = None) -> List[torch.Tensor]:
     """Decoded tensors as the reference returns them (quant.py:107-112): one new, owned, writable tensor
     per entry — pageable CPU tensors for CPU payloads, device tensors for device payloads — never views
     of a shared bucket (a strategy keeps single updates alive, Src/ADFL/Strategy/fed_buff.py:75,90, and
@@ -369,6 +384,9 @@ def _hand_out(out_dev: torch.Tensor, lay: ops.BucketLayout, shapes: List[torch.S
     if all(on_cpu):
         pending = _PendingD2H(out_dev, lay, st, key)
         dt = out_dev.dtype
+        if like is not None and dt == torch.float32:   # `like`: tensors of the outputs' shapes (the payloads)
+            th = _torchhost.get()
+            return pending.finish_building(None, len(shapes), make_batch=lambda a, b: th.empty_f32_like(like[a:b]))
         return pending.finish_building(lambda k: torch.empty(shapes[k], dtype=dt), len(shapes))
     if not any(on_cpu) and out_dev.device == st.device:
         # device dict: fresh owned tensors filled from the bucket by one launch (not one clone per tensor)
@@ -421,7 +439,8 @@ def _encode_host_dict(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _D
     host = st.buf("x_host", lay.total, torch.float32, pinned=True)
     amax = np.zeros(lay.ntensors, dtype=np.uint32)
     a_base = amax.ctypes.data
-    ptrs = _ptrs(tensors)
+    th = _torchhost.get()
+    ptrs = th.data_ptrs(tensors).numpy().view(np.uint64)
     ranges = _ranges(lay, 4)
     jobs = []
     with _ph("enc.gather_submit"):
@@ -432,8 +451,8 @@ def _encode_host_dict(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _D
                                                absmax_ptrs=np.uint64(a_base) + plan.ku * np.uint64(4),
                                                keep=(host, amax)))
     ends = lay.offsets + lay.sizes
-    eaq, qint8 = torch._empty_affine_quantized, torch.qint8
     outs: List[torch.Tensor] = []
+    out_ptrs = np.zeros(lay.ntensors, dtype=np.uint64)
     scales = np.zeros(lay.ntensors, dtype=np.float32)
     made = 0
     try:
@@ -446,11 +465,14 @@ def _encode_host_dict(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _D
             if done > made:
                 with _ph("enc.outputs"):
                     scales[made:done] = _host_scales(amax[made:done], bits)
-                    for k in range(made, done):
-                        sc = float(scales[k])
-                        q = eaq(tensors[k].shape, scale=sc, zero_point=0, dtype=qint8)
+                    # the range's payload tensors in one native call (adfl_torchhost): the qint8 tensors
+                    # torch.quantize_per_tensor(x, scale, 0, torch.qint8) would return, still to be filled
+                    qs, qp = th.empty_qint8_like(tensors[made:done], torch.from_numpy(scales[made:done]))
+                    out_ptrs[made:done] = qp.numpy().view(np.uint64)
+                    sl = scales[made:done].tolist()
+                    for j, q in enumerate(qs):
                         outs.append(q)
-                        emit(k, q, sc)
+                        emit(made + j, q, sl[j])
                 made = done
             with _ph("enc.passthrough"):
                 idle()
@@ -474,7 +496,7 @@ def _encode_host_dict(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _D
         while idle():   # the caller's remaining objects while the kernel and the D2H run
             pass
     with _ph("enc.d2h_wait_scatter"):
-        pending.finish(outs)
+        pending.finish(outs, out_ptrs)
     scales_ready.synchronize()
     dev_scales = scales_host.numpy()
     bad = np.nonzero(dev_scales.view(np.uint32) != scales.view(np.uint32))[0]
@@ -559,26 +581,31 @@ def _decode_dict(items: List[Tuple[str, torch.Tensor]]) -> Dict[str, torch.Tenso
     """Decode qint8 tensors (per-tensor affine, zero point 0) in one bucketed pass."""
     st = _staging()
     dev = st.device
-    qint8, pta = torch.qint8, torch.per_tensor_affine
-    for name, q in items:
-        if q.dtype != qint8 or q.qscheme() != pta or q.q_zero_point() != 0:
-            raise ValueError(f"SLQChannel: '{name}' is not a per-tensor qint8 payload with zero point 0")
-    lay = st.layout(tuple([q.numel() for _, q in items]))
+    qlist = [q for _, q in items]
+    with _ph("dec.meta"):
+        # every payload's quantizer, size, place and data pointer in one native call (adfl_torchhost)
+        ok, all_host, numel, scales, ptrs = _torchhost.get().qint8_meta(qlist)
+    if not ok:
+        qint8, pta = torch.qint8, torch.per_tensor_affine
+        for name, q in items:
+            if not q.is_quantized or q.dtype != qint8 or q.qscheme() != pta or q.q_zero_point() != 0:
+                raise ValueError(f"SLQChannel: '{name}' is not a per-tensor qint8 payload with zero point 0")
+    lay = st.layout(tuple(numel.tolist()))
     # CPU qint8 payloads are gathered byte-wise straight from their storage; device ones through int8 views
-    all_host = all(not q.is_cuda and q.is_contiguous() for _, q in items)
-    all_dev = all(q.is_cuda and q.device == dev and q.is_contiguous() for _, q in items)
+    all_dev = not all_host and all(q.is_cuda and q.device == dev and q.is_contiguous() for q in qlist)
     # host payloads are gathered byte-wise from their storages, device ones by one gather launch: neither
     # needs an int8 view object per tensor
-    qs = [q if all_host or all_dev else _int8_view(q) for _, q in items]
+    qs = qlist if all_host or all_dev else [_int8_view(q) for q in qlist]
     with _ph("dec.gather_h2d"):
-        q_dev = _stage_in(qs, lay, st, "dq", torch.int8)
+        q_dev = _stage_in(qs, lay, st, "dq", torch.int8, host_ptrs=ptrs.numpy().view(np.uint64) if all_host else None)
     with _ph("dec.scales"):
-        # q_scale() is a double; fbgemm's dequantize uses it as fp32 (quant.py:110), so round it the same way
-        s_dev = torch.tensor([q.q_scale() for _, q in items], dtype=torch.float32).to(dev, non_blocking=True)
-    on_cpu = [not q.is_cuda for _, q in items]
+        # q_scale() is a double; fbgemm's dequantize uses it as fp32 (quant.py:110): qint8_meta rounded it so
+        s_dev = scales.to(dev, non_blocking=True)
+    on_cpu = [True] * len(qlist) if all_host else [not q.is_cuda for q in qlist]
     with _ph("dec.kernel_launch"):
         out_dev = ops.decode_batched(q_dev, s_dev, lay, out=st.buf("d_out", lay.total, torch.float32))
-    decoded = _hand_out(out_dev, lay, [q.shape for _, q in items], on_cpu, st, "d_out")
+    decoded = _hand_out(out_dev, lay, [q.shape for q in qlist] if not all_host else [None] * len(qlist), on_cpu, st,
+                        "d_out", like=qlist if all_host else None)
     return {name: t for (name, _), t in zip(items, decoded)}
 
 
@@ -811,17 +838,21 @@ class SLQChannel(Channel):
     def _receive(self, c_params: CompressedParameters) -> Tuple[Parameters, float]:
         assert isinstance(c_params, QuantParameters)
         s_time = time.perf_counter()
-        quant = [(name, p.data) for name, p in c_params.params.items() if p.data.ndim > 1 and p.data.is_quantized]
-        decoded = _decode_dict(quant) if quant else {}
-        params = {}
-        for name, p in c_params.params.items():
-            if name in decoded:
-                params[name] = decoded[name]
-            elif p.data.ndim > 1:
-                params[name] = p.data.data.dequantize()  # non-quantized payload: what quant.py:110 does
-            else:
-                params[name] = p.data.data  # passthrough (quant.py:111-112)
-        return params, time.perf_counter() - s_time
+        names = list(c_params.params.keys())
+        datas = [p.data for p in c_params.params.values()]
+        th = _torchhost.get()
+        kinds = th.payload_kinds(datas).numpy()   # _dequantize_tensor's cases for every entry in one call
+        qi = np.nonzero(kinds == 1)[0].tolist()
+        decoded = _decode_dict([(names[i], datas[i]) for i in qi]) if qi else {}
+        vals: List[Optional[torch.Tensor]] = [None] * len(names)
+        for i in qi:
+            vals[i] = decoded[names[i]]
+        pi = np.nonzero(kinds == 0)[0].tolist()
+        for i, t in zip(pi, th.variable_data([datas[i] for i in pi])):
+            vals[i] = t  # passthrough: q_param.data.data (quant.py:111-112)
+        for i in np.nonzero(kinds == 2)[0].tolist():
+            vals[i] = datas[i].data.dequantize()  # non-quantized ndim > 1 payload: what quant.py:110 does
+        return dict(zip(names, vals)), time.perf_counter() - s_time
 
     def receive_add_(self, c_params: CompressedParameters, targets: List[Parameters]) -> float:
         """``on_client_receive(c_params)`` followed by ``add_parameters_inpace(t, decoded, 1, 1, False)`` for

@@ -241,8 +241,10 @@ def _decode_stoch(items: List[Tuple[str, QuantParameter]], codec: str, bits: int
     """Decode (levels, signs, norm[, min]) payloads of ndim > 1 tensors in one bucketed pass."""
     st = _staging()
     lay, out_dev = _decode_stoch_bucket(st, items, codec, bits)
-    on_cpu = [not p.data.is_cuda for _, p in items]
-    decoded = _hand_out(out_dev, lay, [p.data.shape for _, p in items], on_cpu, st, "d_out")
+    datas = [p.data for _, p in items]
+    on_cpu = [not d.is_cuda for d in datas]
+    # CPU payloads: the fp32 outputs (shaped like the level planes) made in one native call per range
+    decoded = _hand_out(out_dev, lay, [d.shape for d in datas], on_cpu, st, "d_out", like=datas if all(on_cpu) else None)
     return {name: t for (name, _), t in zip(items, decoded)}
 
 

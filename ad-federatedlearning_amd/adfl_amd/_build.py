@@ -42,5 +42,34 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return LIB_PATH
 
 
+TORCH_HOST_SRC = os.path.join(SRC_ROOT, "csrc", "torch_host.cpp")
+TORCH_HOST_PATH = os.path.join(LIB_DIR, "adfl_torchhost.so")
+
+
+def build_torch_host(force: bool = False, verbose: bool = False) -> str:
+    """The channels' host-side torch plumbing (csrc/torch_host.cpp): a CPython extension over ATen, built with
+    g++ against this image's torch (headers, libc10 / libtorch, its C++11 ABI), in-tree like the codec."""
+    import sysconfig
+
+    import torch
+    from torch.utils import cpp_extension as ce
+    os.makedirs(LIB_DIR, exist_ok=True)
+    if (not force and os.path.exists(TORCH_HOST_PATH)
+            and os.path.getmtime(TORCH_HOST_PATH) >= os.path.getmtime(TORCH_HOST_SRC)):
+        return TORCH_HOST_PATH
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    incs = [f"-I{d}" for d in ce.include_paths()] + [f"-I{sysconfig.get_paths()['include']}"]
+    libdir = ce.library_paths()[0]
+    cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-shared", "-fPIC", "-w",
+           f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_EXTENSION_NAME=adfl_torchhost", "-DTORCH_API_INCLUDE_EXTENSION_H",
+           *incs, TORCH_HOST_SRC, "-o", TORCH_HOST_PATH, f"-L{libdir}", f"-Wl,-rpath,{libdir}",
+           "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    return TORCH_HOST_PATH
+
+
 if __name__ == "__main__":
     print(build(force=True, verbose=True))
+    print(build_torch_host(force=True, verbose=True))

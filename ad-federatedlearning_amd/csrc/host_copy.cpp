@@ -8,6 +8,8 @@
 #include <sched.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstdlib>
 #include <condition_variable>
 #include <cstdint>
@@ -38,8 +40,8 @@ struct Job {
   int (*wait_fn)(void*) = nullptr;
   void* wait_arg = nullptr;
   uint32_t* const* absmax = nullptr;  // ADFL_HOST_COPY_ABSMAX: piece k's max |fp32 bits| max'ed into *absmax[k]
-  int next = 0;  // next unclaimed part (under the pool mutex)
-  int done = 0;  // finished parts (under the pool mutex)
+  int next = 0;               // next unclaimed part (under the pool mutex)
+  std::atomic<int> done{0};   // finished parts (incremented under the pool mutex; a waiter may spin on it)
   int status = 0;
   // owned storage of an asynchronous job
   std::vector<uint32_t*> own_absmax;
@@ -194,13 +196,24 @@ class Pool {
     {
       std::lock_guard<std::mutex> lk(mu_);
       queue_.push_back(job);
+      queued_.fetch_add(1, std::memory_order_relaxed);
     }
     cv_.notify_all();
   }
 
   int wait(Job* job) {
-    std::unique_lock<std::mutex> lk(mu_);
-    done_cv_.wait(lk, [&] { return job->done == job->parts; });
+    // spin first: a channel call's copies finish within microseconds of each other, and a thread woken from
+    // a condition variable (and a deep C-state) costs tens of microseconds each time
+    const auto t0 = std::chrono::steady_clock::now();
+    while (job->done.load(std::memory_order_acquire) != job->parts) {
+      if (std::chrono::steady_clock::now() - t0 > spin_) {
+        std::unique_lock<std::mutex> lk(mu_);
+        done_cv_.wait(lk, [&] { return job->done.load(std::memory_order_acquire) == job->parts; });
+        break;
+      }
+      _mm_pause();
+    }
+    std::lock_guard<std::mutex> lk(mu_);  // the status, written before the last part counted
     return job->status;
   }
 
@@ -221,7 +234,14 @@ class Pool {
     return n;
   }
 
-  Pool() {
+  // ADFL_HOST_SPIN_US (default 200): how long an idle worker, or a waiting caller, spins before sleeping
+  static std::chrono::microseconds spin_time() {
+    long us = 200;
+    if (const char* e = std::getenv("ADFL_HOST_SPIN_US")) us = std::max(0L, std::atol(e));
+    return std::chrono::microseconds(us);
+  }
+
+  Pool() : spin_(spin_time()) {
     const int n = pool_threads() - 1;
     for (int i = 0; i < n; ++i) workers_.emplace_back([this] { loop(); });
     for (auto& t : workers_) {
@@ -243,6 +263,7 @@ class Pool {
     for (auto it = queue_.begin(); it != queue_.end(); ++it)
       if (*it == job) {
         queue_.erase(it);
+        queued_.fetch_sub(1, std::memory_order_relaxed);
         return;
       }
   }
@@ -250,11 +271,15 @@ class Pool {
   void finish(Job* job, int status) {
     std::lock_guard<std::mutex> lk(mu_);
     if (status != 0 && job->status == 0) job->status = status;
-    if (++job->done == job->parts) done_cv_.notify_all();
+    const int parts = job->parts;  // read before the count: a spinning waiter may free the job right after it
+    if (job->done.fetch_add(1, std::memory_order_acq_rel) + 1 == parts) done_cv_.notify_all();
   }
 
   void loop() {
     for (;;) {
+      const auto t0 = std::chrono::steady_clock::now();
+      while (queued_.load(std::memory_order_relaxed) == 0 && std::chrono::steady_clock::now() - t0 < spin_)
+        _mm_pause();
       Job* job;
       int p;
       {
@@ -262,7 +287,10 @@ class Pool {
         cv_.wait(lk, [&] { return !queue_.empty(); });
         job = queue_.front();
         p = job->next++;
-        if (job->next == job->parts) queue_.pop_front();
+        if (job->next == job->parts) {
+          queue_.pop_front();
+          queued_.fetch_sub(1, std::memory_order_relaxed);
+        }
       }
       finish(job, run_part(*job, p));
     }
@@ -273,6 +301,8 @@ class Pool {
   std::mutex mu_;
   std::condition_variable cv_, done_cv_;
   std::deque<Job*> queue_;
+  std::atomic<int> queued_{0};  // jobs in queue_ (idle workers spin on it before sleeping)
+  const std::chrono::microseconds spin_;
 };
 
 int64_t build_prefix(const int64_t* nbytes, void* const* dsts, const void* const* srcs, int64_t n,
@@ -358,8 +388,8 @@ int64_t adfl_host_copy_submit_absmax(void* const* dsts, const void* const* srcs,
   // the workers only (the caller returns at once); at least one part, so the wait callback always runs
   job->parts = pool.workers() > 0 ? parts_for(std::max<int64_t>(total, 1), nthreads, pool.workers()) : 1;
   if (pool.workers() == 0) {  // no worker threads on this host: run it here
-    job->done = job->parts;
     job->status = run_part(*job, 0);
+    job->done.store(job->parts, std::memory_order_release);
   } else {
     pool.push(job);
   }

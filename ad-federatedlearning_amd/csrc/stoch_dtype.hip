@@ -180,8 +180,14 @@ __device__ __forceinline__ uint32_t encode_elem(typename T::C x, typename T::C u
     if (__builtin_isinf(v)) return (uint32_t)max_e & 0xffu;
     int lo, hi;
     cnat_bounds<T>(v, lo, hi, tb);
-    // the reference's (2^c - |x|) / 2^f, each op rounded to the dtype (2^16 is inf in fp16: prob NaN, ceil)
-    const C prob = T::rn(T::rn(T::rn(pow2i<C>(hi)) - xa) / T::rn(pow2i<C>(lo)));
+    // the reference's (2^c - |x|) / 2^f, each op rounded to the dtype (2^16 is inf in fp16: prob NaN, ceil).
+    // f >= log2(eps) (v >= eps), so 2^f is a normal value of the dtype and the quotient of the rounded
+    // numerator (0, or at least ulp(2^c) >= 2^(f - mantissa bits)) by it is exact in C: an exponent shift
+    // (v_ldexp) gives the quotient the division would, without the ~10-instruction correctly rounded divide.
+    const C num = T::rn(T::rn(pow2i<C>(hi)) - xa);
+    C prob;
+    if constexpr (sizeof(C) == 4) prob = T::rn(__builtin_ldexpf(num, -lo));
+    else prob = __builtin_ldexp(num, -lo);
     const int r = u < prob ? lo : hi;
     return (uint32_t)min(max(r, min_e), max_e) & 0xffu;
   }

@@ -1,0 +1,107 @@
+// torch_host.cpp — the host-resident channel path's per-tensor torch plumbing, one call per batch
+// (adfl_amd/Channel/quant.py). ADFL hands the channel CPU state dicts of ~256 tensors (Src/ADFL/model.py:195-197)
+// and expects 256 owned tensors back from every on_client_send / on_server_receive (quant.py:74-112): their
+// creation, and reading each payload's quantizer, cost ~2.5 us per tensor per Python call — about 0.6 ms per
+// direction on C3, as much as the PCIe copies they overlap. Here each batch is one call into ATen:
+//   empty_f32_like(like)            fresh contiguous fp32 CPU tensors shaped like `like` (the decode's outputs)
+//   empty_qint8_like(like, scales)  per-tensor affine qint8 CPU tensors, zero point 0, scale[k] (the payloads,
+//                                   as torch.quantize_per_tensor(x, scale, 0, torch.qint8) shapes them)
+//   qint8_meta(q)                   for payload tensors: whether every one is a per-tensor affine qint8 tensor
+//                                   with zero point 0, whether all are contiguous CPU tensors, their element
+//                                   counts, fp32 scales (fbgemm uses q_scale() as fp32, quant.py:110) and
+//                                   data pointers
+//   data_ptrs(ts)                   the tensors' data pointers
+//   payload_kinds(ts)               per payload 0: ndim <= 1 (passed through), 1: ndim > 1 and quantized (decoded),
+//                                   2: ndim > 1 otherwise — _receive's three cases (quant.py:107-112)
+//   variable_data(ts)               t.data for each (what _receive hands back for a passthrough entry)
+// Every returned pointer table is an int64 CPU tensor (the native copy pool's piece lists).
+#include <torch/extension.h>
+
+#include <cstdint>
+#include <tuple>
+#include <vector>
+
+namespace {
+
+std::tuple<std::vector<at::Tensor>, at::Tensor> empty_f32_like(const std::vector<at::Tensor>& like) {
+  std::vector<at::Tensor> out;
+  out.reserve(like.size());
+  at::Tensor ptrs = at::empty({(int64_t)like.size()}, at::kLong);
+  int64_t* p = ptrs.data_ptr<int64_t>();
+  const auto opts = at::TensorOptions().dtype(at::kFloat);
+  for (size_t k = 0; k < like.size(); ++k) {
+    out.push_back(at::empty(like[k].sizes(), opts));
+    p[k] = (int64_t)(intptr_t)out.back().data_ptr();
+  }
+  return {std::move(out), ptrs};
+}
+
+std::tuple<std::vector<at::Tensor>, at::Tensor> empty_qint8_like(const std::vector<at::Tensor>& like,
+                                                                 const at::Tensor& scales) {
+  TORCH_CHECK(scales.scalar_type() == at::kFloat && scales.is_contiguous() && !scales.is_cuda() &&
+                  scales.numel() == (int64_t)like.size(),
+              "empty_qint8_like: one fp32 CPU scale per tensor");
+  const float* s = scales.data_ptr<float>();
+  std::vector<at::Tensor> out;
+  out.reserve(like.size());
+  at::Tensor ptrs = at::empty({(int64_t)like.size()}, at::kLong);
+  int64_t* p = ptrs.data_ptr<int64_t>();
+  const auto opts = at::TensorOptions().dtype(at::kQInt8);
+  for (size_t k = 0; k < like.size(); ++k) {
+    out.push_back(at::_empty_affine_quantized(like[k].sizes(), opts, (double)s[k], 0));
+    p[k] = (int64_t)(intptr_t)out.back().data_ptr();
+  }
+  return {std::move(out), ptrs};
+}
+
+std::tuple<bool, bool, at::Tensor, at::Tensor, at::Tensor> qint8_meta(const std::vector<at::Tensor>& q) {
+  const int64_t n = (int64_t)q.size();
+  at::Tensor numel = at::empty({n}, at::kLong), scales = at::empty({n}, at::kFloat), ptrs = at::empty({n}, at::kLong);
+  int64_t* ne = numel.data_ptr<int64_t>();
+  float* sc = scales.data_ptr<float>();
+  int64_t* pt = ptrs.data_ptr<int64_t>();
+  bool ok = true, host = true;
+  for (int64_t k = 0; k < n; ++k) {
+    const at::Tensor& t = q[k];
+    const bool quant = t.is_quantized() && t.scalar_type() == at::kQInt8 && t.qscheme() == at::kPerTensorAffine &&
+                       t.q_zero_point() == 0;
+    ok = ok && quant;
+    host = host && !t.is_cuda() && t.is_contiguous();
+    ne[k] = t.numel();
+    sc[k] = quant ? (float)t.q_scale() : 0.0f;
+    pt[k] = (int64_t)(intptr_t)t.data_ptr();
+  }
+  return {ok, host, numel, scales, ptrs};
+}
+
+at::Tensor data_ptrs(const std::vector<at::Tensor>& ts) {
+  at::Tensor ptrs = at::empty({(int64_t)ts.size()}, at::kLong);
+  int64_t* p = ptrs.data_ptr<int64_t>();
+  for (size_t k = 0; k < ts.size(); ++k) p[k] = (int64_t)(intptr_t)ts[k].data_ptr();
+  return ptrs;
+}
+
+at::Tensor payload_kinds(const std::vector<at::Tensor>& ts) {
+  at::Tensor k = at::empty({(int64_t)ts.size()}, at::kByte);
+  uint8_t* p = k.data_ptr<uint8_t>();
+  for (size_t i = 0; i < ts.size(); ++i) p[i] = ts[i].dim() <= 1 ? 0 : (ts[i].is_quantized() ? 1 : 2);
+  return k;
+}
+
+std::vector<at::Tensor> variable_data(const std::vector<at::Tensor>& ts) {
+  std::vector<at::Tensor> out;
+  out.reserve(ts.size());
+  for (const auto& t : ts) out.push_back(t.variable_data());
+  return out;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("empty_f32_like", &empty_f32_like);
+  m.def("empty_qint8_like", &empty_qint8_like);
+  m.def("qint8_meta", &qint8_meta);
+  m.def("data_ptrs", &data_ptrs);
+  m.def("payload_kinds", &payload_kinds);
+  m.def("variable_data", &variable_data);
+}

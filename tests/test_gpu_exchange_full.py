@@ -5,6 +5,7 @@ device per rank, so the rows travel over gloo through pinned host memory as in t
 
 * C5: K = 2 clients x 2^30 fp32 (4 GiB) each, SLQ bits 4, int4-packed, chunks = 8 (quantize of chunk c
       overlapped with the all-gather of chunk c-1);
+* C5 at its stated client count: K = 8 x 2^30 int4-packed, chunks = 8 (the mean checked at sampled positions);
 * C4: K = 8 clients x 2^28 fp32 (1 GiB) each, SLQ bits 8.
 
 Client r's update is randn(n) * 1e-3 from a device generator seeded r. Checks, on every rank:
@@ -36,7 +37,28 @@ def _sha(a) -> str:
     return hashlib.sha256(memoryview(np.ascontiguousarray(a)).cast("B")).hexdigest()
 
 
-def _worker(rank, world, port, numel, bits, packed, chunks, q):
+def _sampled_mean_check(out, rows, scales, xh, rank, packed, m=1 << 16):
+    """The mean at m random positions (the same for every rank) against the oracle over just those columns.
+    numel and m are multiples of 32, so every column sums in the same (SEQ) order whatever its index
+    (csrc/torch_sum_order.h), and the oracle over the sampled columns is the oracle at those positions."""
+    import slq_oracle as oracle
+    numel = xh.size
+    assert numel % 32 == 0 and m % 32 == 0
+    idx = np.sort(np.random.default_rng(12345).choice(numel, size=m, replace=False))
+    qs = []
+    for r in range(len(rows)):
+        if packed:
+            b = rows[r][idx // 2].astype(np.int16)
+            qv = np.where(idx % 2 == 0, (b >> 4) & 0xF, b & 0xF) - 8
+            qs.append(qv.astype(np.int8))
+        else:
+            qs.append(rows[r][idx].view(np.int8))
+    want = oracle.dequantize_mean_self(qs, scales, m, rank, np.ascontiguousarray(xh[idx]), False)
+    got = out[idx]
+    return bool(np.array_equal(got.view(np.uint32), want.view(np.uint32)))
+
+
+def _worker(rank, world, port, numel, bits, packed, chunks, q, sampled=False):
     try:
         sys.path.insert(0, os.path.join(REPO, "ad-federatedlearning_amd"))
         sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -93,8 +115,12 @@ def _worker(rank, world, port, numel, bits, packed, chunks, q):
         del payload
 
         # 3. the mean = oracle.dequantize_mean_self over the (verified) oracle rows, own update exact
-        want = oracle.dequantize_mean_self(rows, scales, numel, rank, xh, packed)
-        got_sha, want_sha = _sha(out.cpu().numpy()), _sha(want)
+        if sampled:   # K = 8 x 2^30: the oracle at 2^16 sampled positions (same order as the full vector)
+            ok = _sampled_mean_check(out.cpu().numpy(), rows, scales, xh, rank, packed)
+            got_sha, want_sha = ("sampled" if ok else "sampled-mismatch"), "sampled"
+        else:
+            want = oracle.dequantize_mean_self(rows, scales, numel, rank, xh, packed)
+            got_sha, want_sha = _sha(out.cpu().numpy()), _sha(want)
         q.put((rank, {"own_rows_equal_oracle": own_ok, "received_rows_equal_oracle": rows_ok,
                       "mean_sha256": got_sha, "oracle_mean_sha256": want_sha,
                       "exchange_s": round(t_exchange, 3), "total_s": round(time.perf_counter() - t0, 1)}))
@@ -104,13 +130,14 @@ def _worker(rank, world, port, numel, bits, packed, chunks, q):
         q.put((rank, f"error {e!r}\n{traceback.format_exc()}"))
 
 
-def _run(world, numel, bits, packed, chunks, limit_s):
+def _run(world, numel, bits, packed, chunks, limit_s, sampled=False):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, numel, bits, packed, chunks, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, numel, bits, packed, chunks, q, sampled))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -146,6 +173,14 @@ def _run(world, numel, bits, packed, chunks, limit_s):
 @pytest.mark.timeout(300)
 def test_c5_two_clients_4gib_int4_packed_chunks8():
     _run(world=2, numel=1 << 30, bits=4, packed=True, chunks=8, limit_s=280)
+
+
+@pytest.mark.timeout(560)
+def test_c5_eight_clients_4gib_int4_packed_chunks8():
+    """BASELINE configs[4] at its stated client count (Examples/ray_ad.py:183-188): 8 clients x 2^30 fp32,
+    int4-packed in 8 chunks. Rows checked in full (own = oracle encode, received = senders' SHA-256); the
+    8-row mean against the oracle at 2^16 sampled positions on every rank."""
+    _run(world=8, numel=1 << 30, bits=4, packed=True, chunks=8, limit_s=540, sampled=True)
 
 
 @pytest.mark.timeout(300)
