@@ -31,7 +31,8 @@ from typing import Dict, List, Optional, Tuple
 import numpy as np
 import torch
 
-from .. import _torchhost, hostcopy, ops, qerror, sum_order
+from .. import _lib, _torchhost, hostcopy, ops, qerror, sum_order
+from .._lib import check
 from ..model import (CompressedParameters, Parameters, QuantParameter, QuantParameters, get_parameter_info)
 from .channel import Channel, IdentityChannel
 
@@ -47,6 +48,14 @@ class _DeviceStaging:
         self.lock = threading.RLock()
         self._bufs: Dict[str, torch.Tensor] = {}
         self.layouts: "OrderedDict[Tuple[int, ...], ops.BucketLayout]" = OrderedDict()
+        self._d2h: Optional[torch.cuda.Stream] = None
+
+    def d2h_stream(self) -> torch.cuda.Stream:
+        """The range-pipelined host paths' copy-back stream: a range's D2H runs here, behind an event on the
+        compute stream, so it overlaps the next range's H2D (one stream would serialise them)."""
+        if self._d2h is None:
+            self._d2h = torch.cuda.Stream(self.device)
+        return self._d2h
 
     def buf(self, key: str, numel: int, dtype: torch.dtype, pinned: bool = False) -> torch.Tensor:
         t = self._bufs.get(key)
@@ -169,6 +178,34 @@ def _range_copies(ptrs: np.ndarray, lay: ops.BucketLayout, base: int, es: int, l
     p = _plan(lay, lo, hi)
     out = p.copies(ptrs, base, es, to_bucket)
     return out + (p.k,) if with_tensors else out
+
+
+ctypes_chunk_bytes = 24  # sizeof(adfl_slq_chunk)
+_CHUNK_DT = np.dtype([("start", "<i8"), ("len", "<i4"), ("tensor", "<i4"), ("first_chunk", "<i4"),
+                      ("nchunks", "<i4")])
+
+
+class _ChunkMeta:
+    """A layout's chunk table as arrays (cached on the layout): every chunk's [start, end) and, per tensor, its
+    first chunk and one past its last — what the range-pipelined host paths launch chunk ranges with."""
+
+    __slots__ = ("start", "end", "first", "cend")
+
+    def __init__(self, lay: ops.BucketLayout):
+        c = np.frombuffer(lay.chunks, dtype=_CHUNK_DT)
+        self.start = c["start"].astype(np.int64)
+        self.end = self.start + c["len"]
+        t_first = np.zeros(lay.ntensors, dtype=np.int64)
+        t_first[c["tensor"][c["first_chunk"] == np.arange(len(c))]] = np.nonzero(c["first_chunk"] == np.arange(len(c)))[0]
+        self.first = t_first
+        self.cend = t_first + c["nchunks"][t_first]
+
+
+def _chunk_meta(lay: ops.BucketLayout) -> _ChunkMeta:
+    m = lay.__dict__.get("_chunk_meta")
+    if m is None:
+        m = lay.__dict__["_chunk_meta"] = _ChunkMeta(lay)
+    return m
 
 
 def _ptrs(tensors: List[torch.Tensor]) -> np.ndarray:
@@ -422,21 +459,35 @@ def _qerror_sums(x_dev: torch.Tensor, d_dev: torch.Tensor, lay: ops.BucketLayout
 
 def _encode_host_dict(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _DeviceStaging, bits: int,
                       stats: Optional[list], emit, idle):
-    """The all-CPU fp32 dict's encode with its outputs built in the shadow of the copies.
+    """The all-CPU fp32 dict's encode, pipelined range by range across the host, the link and the GPU.
 
     The gather into the pinned bucket is queued on the native pool range by range and reduces max|x| per
     tensor as it copies (adfl_host_copy_submit_absmax), so a tensor's scale is known on the host as soon as
-    its last byte is staged. While the copy engine moves range r, this thread creates the qint8 outputs of the
-    tensors completed so far (emit(k, q, scale) per tensor) and runs `idle()` (the caller's other payload
-    objects). Then one encode launch, the payload D2H range by range with the native scatter behind it. The
-    device's scales are checked against the host's (a mismatch rebuilds that output with the device's, which
-    the payload was quantized with). Returns [(q, scale)] per tensor."""
+    its last byte is staged. For each staging range, as its gather lands: its H2D is enqueued; the tensors it
+    completes are quantized at once (adfl_slq_quantize_batched_range over their chunks, from the host's max|x|
+    bits as partials: the same scales the two-pass encode computes), their payload bytes go back D2H behind
+    an event, their qint8 outputs are created (one native call) and emit(k, q, scale) builds each payload
+    object, and the scatter into those outputs is queued on the pool behind the event — so the D2H and
+    scatter of range r overlap the H2D of range r + 1. `idle()` (the caller's other payload objects) runs in
+    between. The device's scales are checked against the host's at the end. Returns [(q, scale)] per
+    tensor."""
     with _ph("enc.heap"):
         _host_heap(lay)
     dev = st.device
     stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+    lib = _lib.load()
     x_dev = st.buf("x", lay.total, torch.float32)
     host = st.buf("x_host", lay.total, torch.float32, pinned=True)
+    q_dev = st.buf("q", lay.total, torch.int8)
+    q_host = st.buf("q_host", lay.total, torch.int8, pinned=True)
+    s_dev = st.buf("scales", lay.ntensors, torch.float32)
+    part_dev = st.buf("partials", lay.nchunks, torch.int32)
+    part_host = st.buf("partials_host", lay.nchunks, torch.int32, pinned=True)
+    part_np = part_host.numpy().view(np.uint32)
+    chunks_ptr = lay.device_chunks(dev).data_ptr()
+    d2h = st.d2h_stream()
+    cm = _chunk_meta(lay)
     amax = np.zeros(lay.ntensors, dtype=np.uint32)
     a_base = amax.ctypes.data
     th = _torchhost.get()
@@ -454,6 +505,7 @@ def _encode_host_dict(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _D
     outs: List[torch.Tensor] = []
     out_ptrs = np.zeros(lay.ntensors, dtype=np.uint64)
     scales = np.zeros(lay.ntensors, dtype=np.float32)
+    scatters = []
     made = 0
     try:
         for (lo, hi), job in zip(ranges, jobs):
@@ -463,6 +515,20 @@ def _encode_host_dict(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _D
                 x_dev[lo:hi].copy_(host[lo:hi], non_blocking=True)
             done = int(np.searchsorted(ends, hi, side="right"))   # tensors whose every byte is staged
             if done > made:
+                with _ph("enc.kernel_launch"):
+                    c0, c1 = int(cm.first[made]), int(cm.cend[done - 1])
+                    part_np[c0:c1] = 0
+                    part_np[cm.first[made:done]] = amax[made:done]
+                    part_dev[c0:c1].copy_(part_host[c0:c1], non_blocking=True)
+                    check(lib.adfl_slq_quantize_batched_range(x_dev.data_ptr(), chunks_ptr, c0, c1 - c0, bits,
+                                                              part_dev.data_ptr(), q_dev.data_ptr(),
+                                                              s_dev.data_ptr(), sh))
+                    e0, e1 = int(lay.offsets[made]), int(ends[done - 1])
+                    d2h.wait_stream(stream)
+                    with torch.cuda.stream(d2h):
+                        q_host[e0:e1].copy_(q_dev[e0:e1], non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(d2h)
                 with _ph("enc.outputs"):
                     scales[made:done] = _host_scales(amax[made:done], bits)
                     # the range's payload tensors in one native call (adfl_torchhost): the qint8 tensors
@@ -473,16 +539,19 @@ def _encode_host_dict(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _D
                     for j, q in enumerate(qs):
                         outs.append(q)
                         emit(made + j, q, sl[j])
+                with _ph("enc.scatter_submit"):
+                    scatters.append(hostcopy.submit_pieces(
+                        *_range_copies(out_ptrs, lay, q_host.data_ptr(), 1, e0, e1, to_bucket=False),
+                        stream=True, event=ev, keep=q_host))
                 made = done
             with _ph("enc.passthrough"):
                 idle()
     finally:
         for j in jobs:
             j.wait()
-    with _ph("enc.kernel_launch"):
-        q_dev, s_dev = ops.encode_batched(x_dev, lay, bits, q=st.buf("q", lay.total, torch.int8),
-                                          scales=st.buf("scales", lay.ntensors, torch.float32),
-                                          partials=st.buf("partials", lay.nchunks, torch.int32))
+        with _ph("enc.scatter_wait"):
+            for j in scatters:
+                j.wait()
     if stats is not None:
         stats.append(_qerror_sums(x_dev, ops.decode_batched(q_dev, s_dev, lay, out=st.buf("qe_d", lay.total, torch.float32)),
                                   lay))
@@ -490,13 +559,9 @@ def _encode_host_dict(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _D
     scales_host.copy_(s_dev, non_blocking=True)
     scales_ready = torch.cuda.Event()
     scales_ready.record(stream)
-    with _ph("enc.d2h_enqueue"):
-        pending = _PendingD2H(q_dev, lay, st, "q")
     with _ph("enc.passthrough"):
-        while idle():   # the caller's remaining objects while the kernel and the D2H run
+        while idle():   # the caller's remaining objects
             pass
-    with _ph("enc.d2h_wait_scatter"):
-        pending.finish(outs, out_ptrs)
     scales_ready.synchronize()
     dev_scales = scales_host.numpy()
     bad = np.nonzero(dev_scales.view(np.uint32) != scales.view(np.uint32))[0]
@@ -511,7 +576,7 @@ def _encode_host_dict(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _D
 
 @_serialized
 def _encode_dict(params: Parameters, names: List[str], bits: int, stats: Optional[list] = None,
-                 emit=None, idle=None):
+                 emit=None, idle=None, meta=None):
     """Encode the ndim>1 tensors `names` of `params` in one bucketed pass.
 
     Returns {name: (qint8 tensor on the input's device, python float scale)}. With `stats` (a list), the
@@ -522,8 +587,10 @@ def _encode_dict(params: Parameters, names: List[str], bits: int, stats: Optiona
     st = _staging()
     dev = st.device
     tensors = [params[n] for n in names]
-    lay = st.layout(tuple(int(t.numel()) for t in tensors))
-    if _PIPELINE and all(not t.is_cuda and t.is_contiguous() and t.dtype == torch.float32 for t in tensors):
+    # meta: (sizes, all contiguous CPU) from _quantize_params' native scan (every tensor already fp32)
+    lay = st.layout(meta[0] if meta is not None else tuple(int(t.numel()) for t in tensors))
+    all_host = meta[1] if meta is not None else all(not t.is_cuda and t.is_contiguous() for t in tensors)
+    if _PIPELINE and all_host and (meta is not None or all(t.dtype == torch.float32 for t in tensors)):
         res = _encode_host_dict(tensors, lay, st, bits, stats, emit or (lambda k, q, sc: None),
                                 idle or (lambda: False))
         return {name: r for name, r in zip(names, res)}
@@ -591,6 +658,9 @@ def _decode_dict(items: List[Tuple[str, torch.Tensor]]) -> Dict[str, torch.Tenso
             if not q.is_quantized or q.dtype != qint8 or q.qscheme() != pta or q.q_zero_point() != 0:
                 raise ValueError(f"SLQChannel: '{name}' is not a per-tensor qint8 payload with zero point 0")
     lay = st.layout(tuple(numel.tolist()))
+    if all_host and _PIPELINE:
+        decoded = _decode_host_dict(qlist, lay, st, ptrs.numpy().view(np.uint64), scales)
+        return {name: t for (name, _), t in zip(items, decoded)}
     # CPU qint8 payloads are gathered byte-wise straight from their storage; device ones through int8 views
     all_dev = not all_host and all(q.is_cuda and q.device == dev and q.is_contiguous() for q in qlist)
     # host payloads are gathered byte-wise from their storages, device ones by one gather launch: neither
@@ -607,6 +677,80 @@ def _decode_dict(items: List[Tuple[str, torch.Tensor]]) -> Dict[str, torch.Tenso
     decoded = _hand_out(out_dev, lay, [q.shape for q in qlist] if not all_host else [None] * len(qlist), on_cpu, st,
                         "d_out", like=qlist if all_host else None)
     return {name: t for (name, _), t in zip(items, decoded)}
+
+
+def _decode_host_dict(qlist: List[torch.Tensor], lay: ops.BucketLayout, st: _DeviceStaging, ptrs: np.ndarray,
+                      scales: torch.Tensor) -> List[torch.Tensor]:
+    """CPU qint8 payloads -> owned CPU fp32 tensors, pipelined range by range: the byte gather of every range
+    is queued on the native pool at once; as range r lands, its H2D is enqueued, the chunks it completes are
+    decoded (adfl_slq_dequantize_batched on that chunk range), their floats go back D2H behind an event, the
+    outputs of the tensors they reach are created (one native call) and the scatter is queued on the pool
+    behind the event — so the D2H of range r overlaps the H2D of range r + 1 and the scatters overlap the
+    D2H. Bit-identical to the one-launch decode (each chunk is decoded by the same kernel)."""
+    with _ph("dec.heap"):
+        _host_heap(lay)
+    dev = st.device
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+    lib = _lib.load()
+    q_dev = st.buf("dq", lay.total, torch.int8)
+    q_host = st.buf("dq_host", lay.total, torch.int8, pinned=True)
+    out_dev = st.buf("d_out", lay.total, torch.float32)
+    out_host = st.buf("d_out_host", lay.total, torch.float32, pinned=True)
+    chunks_ptr = lay.device_chunks(dev).data_ptr()
+    d2h = st.d2h_stream()
+    cm = _chunk_meta(lay)
+    th = _torchhost.get()
+    ranges = _ranges(lay, 4)
+    with _ph("dec.gather_submit"):
+        jobs = [hostcopy.submit_pieces(*_range_copies(ptrs, lay, q_host.data_ptr(), 1, lo, hi, to_bucket=True),
+                                       keep=q_host) for lo, hi in ranges]
+    with _ph("dec.scales"):
+        s_dev = scales.to(dev, non_blocking=True)
+    offs = lay.offsets
+    outs: List[torch.Tensor] = []
+    out_ptrs = np.zeros(lay.ntensors, dtype=np.uint64)
+    scatters = []
+    c_made = 0
+    t_made = 0
+    try:
+        for (lo, hi), job in zip(ranges, jobs):
+            with _ph("dec.gather_wait"):
+                job.wait()
+            with _ph("dec.kernel_launch"):
+                q_dev[lo:hi].copy_(q_host[lo:hi], non_blocking=True)
+                c_end = int(np.searchsorted(cm.end, hi, side="right"))   # chunks whose every byte is staged
+                if c_end <= c_made:
+                    continue
+                check(lib.adfl_slq_dequantize_batched(q_dev.data_ptr(), chunks_ptr + c_made * ctypes_chunk_bytes,
+                                                      c_end - c_made, s_dev.data_ptr(), out_dev.data_ptr(), sh))
+                e0, e1 = int(cm.start[c_made]), int(cm.end[c_end - 1])
+                d2h.wait_stream(stream)
+                with torch.cuda.stream(d2h):
+                    out_host[e0:e1].copy_(out_dev[e0:e1], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(d2h)
+                c_made = c_end
+            with _ph("out.alloc"):
+                t_end = int(np.searchsorted(offs, e1, side="left"))    # tensors starting below e1
+                if t_end > t_made:
+                    ts, pt = th.empty_f32_like(qlist[t_made:t_end])
+                    outs.extend(ts)
+                    out_ptrs[t_made:t_end] = pt.numpy().view(np.uint64)
+                    for j in np.nonzero(lay.sizes[t_made:t_end] * 4 >= (4 << 20))[0].tolist():
+                        hostcopy.advise_huge([ts[j]])
+                    t_made = t_end
+            with _ph("out.scatter_submit"):
+                scatters.append(hostcopy.submit_pieces(
+                    *_range_copies(out_ptrs, lay, out_host.data_ptr(), 4, e0, e1, to_bucket=False),
+                    stream=True, event=ev, keep=out_host))
+    finally:
+        for j in jobs:
+            j.wait()
+        with _ph("out.scatter_wait"):
+            for j in scatters:
+                j.wait()
+    return outs
 
 
 @_serialized
@@ -961,22 +1105,30 @@ class SLQChannel(Channel):
 
     def _quantize_params(self, params: Parameters, bits: int, stats: Optional[list] = None) -> QuantParameters:
         """Biases and running metrics (ndim <= 1) are not quantized (quant.py:74-94)."""
-        names = [name for name, p in params.items() if p.ndim > 1]
-        for name in names:
-            ops.require_quantizable(params[name])
+        items = list(params.items())
+        # every entry's ndim / numel / dtype / placement in one native call (adfl_torchhost.tensor_meta)
+        ndim, numel, f32, host = (a.numpy() for a in _torchhost.get().tensor_meta([p for _, p in items]))
+        qi = np.nonzero(ndim > 1)[0]
+        names = [items[i][0] for i in qi.tolist()]
+        bad = qi[(numel[qi] == 0) | ~f32[qi]]
+        if bad.size:
+            ops.require_quantizable(items[int(bad[0])][1])   # raises the reference's error for that tensor
+        sizes = numel[qi].tolist()
+        meta = (tuple(sizes), bool(host[qi].all()))
         signs = torch.zeros(1, dtype=torch.uint8)  # the unused field (quant.py:91), one object per call
         qp = QuantParameter
         made: Dict[str, QuantParameter] = {}
         size = [0]
         # positional: QuantParameter(data, bits, scale, signs, shape, dtype, q_dtype) (model.py:21-31)
 
+        f32t, qint8 = torch.float32, torch.qint8
+
         def emit(k, q, scale):   # a quantized entry, built as soon as its output exists
             n = names[k]
-            p = params[n]
             if n not in made:
-                size[0] += q.numel()          # a qint8 payload: one byte per element
-            made[n] = qp(q, bits, scale, signs, p.shape, p.dtype, q.dtype)
-        rest = iter([(n, p) for n, p in params.items() if p.ndim <= 1])
+                size[0] += sizes[k]           # a qint8 payload: one byte per element
+            made[n] = qp(q, bits, scale, signs, q.shape, f32t, qint8)
+        rest = iter([items[i] for i in np.nonzero(ndim <= 1)[0].tolist()])
 
         def idle(batch=32):      # passthrough entries (quant.py:80-81), a batch per copy range
             for _ in range(batch):
@@ -987,7 +1139,7 @@ class SLQChannel(Channel):
                 made[e[0]] = qp(t, bits, 1, signs, t.shape, t.dtype, t.dtype)
                 size[0] += t.nbytes
             return True
-        encoded = _encode_dict(params, names, bits, stats, emit=emit, idle=idle) if names else {}
+        encoded = _encode_dict(params, names, bits, stats, emit=emit, idle=idle, meta=meta) if names else {}
         for k, n in enumerate(names):
             if n not in made:    # device dicts and the other staging paths: built here
                 emit(k, *encoded[n])

@@ -50,6 +50,7 @@ SIGNATURES = {
     "adfl_slq_build_encode_work": (I64, [P, I64, P, I64]),
     "adfl_slq_encode_batched_work": (INT, [P, P, I64, P, I64, INT, P, P, P, P]),
     "adfl_slq_dequantize_batched": (INT, [P, P, I64, P, P, P]),
+    "adfl_slq_quantize_batched_range": (INT, [P, P, I64, I64, INT, P, P, P, P]),
     "adfl_slq_qerror_batched": (INT, [P, P, P, I64, P, P, P]),
     "adfl_slq_qerror_batched_int4": (INT, [P, P, P, I64, P, P, P]),
     "adfl_slq_encode_batched_int4": (INT, [P, P, I64, INT, P, P, P, P]),

@@ -65,8 +65,10 @@ class Pending:
     def wait(self) -> None:
         if self.ticket:
             t, self.ticket = self.ticket, 0
-            self._keep = None
-            check(_host_lib().adfl_host_copy_wait(t))
+            try:
+                check(_host_lib().adfl_host_copy_wait(t))
+            finally:
+                self._keep = None   # only now: the workers may still read the buffers / wait on the event
 
     def __del__(self):   # a job is always waited for: its buffers must outlive the copy
         try:

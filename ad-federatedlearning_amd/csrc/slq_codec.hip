@@ -637,12 +637,14 @@ __global__ __launch_bounds__(kBlock) void k_absmax_batched(const float* __restri
 }
 
 // Pass 2: the chunk's loads are issued before the partial reduction, whose latency they hide.
+// chunk_base: the first chunk of the launch (adfl_slq_quantize_batched_range; 0 for the whole table).
 __global__ __launch_bounds__(kBlock) void k_quantize_batched(const float* __restrict__ x,
                                                              const adfl_slq_chunk* __restrict__ chunks,
                                                              float qmax, const uint32_t* __restrict__ partials,
-                                                             int8_t* __restrict__ q, float* __restrict__ scales) {
+                                                             int8_t* __restrict__ q, float* __restrict__ scales,
+                                                             int64_t chunk_base = 0) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kWaves][kTile / 4];
-  const int64_t ci = blockIdx.x;
+  const int64_t ci = chunk_base + blockIdx.x;
   const adfl_slq_chunk c = chunks[ci];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   ChunkRegs r;
@@ -1247,7 +1249,19 @@ int adfl_slq_encode_batched(const float* d_x, const adfl_slq_chunk* d_chunks, in
   hipLaunchKernelGGL(k_absmax_batched, dim3((unsigned)nchunks), dim3(kBlock), 0, st, d_x, d_chunks, d_partials);
   if (int s = launch_status()) return s;
   hipLaunchKernelGGL(k_quantize_batched, dim3((unsigned)nchunks), dim3(kBlock), 0, st, d_x, d_chunks, qmax_f(bits),
-                     (const uint32_t*)d_partials, d_q, d_scales);
+                     (const uint32_t*)d_partials, d_q, d_scales, (int64_t)0);
+  return launch_status();
+}
+
+int adfl_slq_quantize_batched_range(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t chunk_begin,
+                                    int64_t count, int bits, const uint32_t* d_partials, int8_t* d_q,
+                                    float* d_scales, void* stream) {
+  if (!d_x || !d_chunks || !d_q || !d_scales || !d_partials || chunk_begin < 0 || count < 1 || count > INT32_MAX)
+    return ADFL_E_ARG;
+  if (int s = check_bits(bits)) return s;
+  if (!aligned16(d_x) || !aligned16(d_q)) return ADFL_E_ALIGN;
+  hipLaunchKernelGGL(k_quantize_batched, dim3((unsigned)count), dim3(kBlock), 0, (hipStream_t)stream, d_x, d_chunks,
+                     qmax_f(bits), d_partials, d_q, d_scales, chunk_begin);
   return launch_status();
 }
 

@@ -14,9 +14,12 @@
 //   payload_kinds(ts)               per payload 0: ndim <= 1 (passed through), 1: ndim > 1 and quantized (decoded),
 //                                   2: ndim > 1 otherwise — _receive's three cases (quant.py:107-112)
 //   variable_data(ts)               t.data for each (what _receive hands back for a passthrough entry)
+//   tensor_meta(ts)                 per tensor: ndim, numel, whether fp32, whether a contiguous CPU tensor — what
+//                                   _quantize_params and the staging choose by, for a whole state dict at once
 // Every returned pointer table is an int64 CPU tensor (the native copy pool's piece lists).
 #include <torch/extension.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <tuple>
 #include <vector>
@@ -95,6 +98,24 @@ std::vector<at::Tensor> variable_data(const std::vector<at::Tensor>& ts) {
   return out;
 }
 
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> tensor_meta(const std::vector<at::Tensor>& ts) {
+  const int64_t n = (int64_t)ts.size();
+  at::Tensor ndim = at::empty({n}, at::kByte), numel = at::empty({n}, at::kLong), f32 = at::empty({n}, at::kBool),
+             host = at::empty({n}, at::kBool);
+  uint8_t* nd = ndim.data_ptr<uint8_t>();
+  int64_t* ne = numel.data_ptr<int64_t>();
+  bool* f = f32.data_ptr<bool>();
+  bool* h = host.data_ptr<bool>();
+  for (int64_t i = 0; i < n; ++i) {
+    const at::Tensor& t = ts[i];
+    nd[i] = (uint8_t)std::min<int64_t>(t.dim(), 255);
+    ne[i] = t.numel();
+    f[i] = t.scalar_type() == at::kFloat;
+    h[i] = !t.is_cuda() && t.is_contiguous();
+  }
+  return {ndim, numel, f32, host};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -104,4 +125,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("data_ptrs", &data_ptrs);
   m.def("payload_kinds", &payload_kinds);
   m.def("variable_data", &variable_data);
+  m.def("tensor_meta", &tensor_meta);
 }

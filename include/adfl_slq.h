@@ -114,6 +114,17 @@ int adfl_slq_encode_batched_work(const float* d_x, const adfl_slq_chunk* d_chunk
                                  uint32_t* d_partials, void* stream);
 int adfl_slq_dequantize_batched(const int8_t* d_q, const adfl_slq_chunk* d_chunks, int64_t nchunks,
                                 const float* d_scales, float* d_out, void* stream);
+/* The quantize pass of adfl_slq_encode_batched over chunks [chunk_begin, chunk_begin + count) of the FULL
+ * chunk table d_chunks, from absmax partials the caller supplies: d_partials[c] for every chunk c of the
+ * tensors involved, the per-chunk max|x| bits or the whole tensor's at its first chunk and 0 at the others
+ * (the scale is fp32(max / (2^(bits-1)-1)) of their max, written by each tensor's first chunk). A host that
+ * reduced every tensor's max|x| while staging it (SLQChannel's fused gather, quant.py:100) quantizes the
+ * tensors one staging range completes while the next range is still being copied; same payload and scales
+ * as adfl_slq_encode_batched. A dequantize of a chunk range is adfl_slq_dequantize_batched on d_chunks +
+ * chunk_begin. */
+int adfl_slq_quantize_batched_range(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t chunk_begin,
+                                    int64_t count, int bits, const uint32_t* d_partials, int8_t* d_q,
+                                    float* d_scales, void* stream);
 
 /* Quantization error of a bucket against its own payload without materialising the decode — the
  * metrics Src/ADFL/Client/worker.py:186-189 computes with parameter_relative_mse /

@@ -64,3 +64,26 @@ def test_many_jobs_behind_one_event_keep_order():
     want = src_dev.cpu()
     for o in outs:
         assert torch.equal(o, want)
+
+
+def test_job_keeps_its_event_and_buffers_alive():
+    """The job, not the caller, keeps the event (and the buffers it names) alive until every part has run: a
+    caller that drops its own references right after submitting must not leave the workers waiting on a
+    destroyed event (the range-pipelined host paths record a fresh event per range)."""
+    import gc
+    n = 1 << 21
+    src_dev = torch.randn(n, device=DEV)
+    pinned = torch.zeros(n).pin_memory()
+    dst = torch.zeros(n)
+    torch.cuda.synchronize()
+    torch.cuda._sleep(20_000_000)
+    pinned.copy_(src_dev, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(DEV))
+    job = hostcopy.submit_pieces([dst.data_ptr()], [pinned.data_ptr()], [4 * n], event=ev, keep=pinned)
+    want = None
+    del ev, pinned
+    gc.collect()
+    job.wait()
+    want = src_dev.cpu()
+    assert torch.equal(dst, want)
