@@ -21,13 +21,13 @@ DEV = torch.device("cuda", 0)
 
 @pytest.mark.parametrize("pieces", [1, 7])
 def test_copy_waits_for_the_event(pieces):
-    n = 1 << 22
+    n = 1 << 26                                 # a 256 MiB D2H: milliseconds on the link, so it is still running
     pinned = torch.full((n,), -1.0).pin_memory()
     dst = torch.zeros(n)
     src_dev = torch.arange(n, dtype=torch.float32, device=DEV)
     stream = torch.cuda.current_stream(DEV)
     torch.cuda.synchronize()
-    torch.cuda._sleep(50_000_000)               # tens of ms of GPU time before the D2H
+    torch.cuda._sleep(50_000_000)
     pinned.copy_(src_dev, non_blocking=True)
     ev = torch.cuda.Event()
     ev.record(stream)
