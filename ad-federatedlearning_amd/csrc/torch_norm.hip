@@ -26,19 +26,20 @@
 // a non-finite value, or a step of 2^24 ulps or more is not covered: the reference arithmetic (fma) runs it.
 //
 // Phases (long tensors: more than kShortMax elements), one launch each, every block independent:
-//   A  k_tn_stage<.., false>: per 8192-element chunk and chain, the fp64 sum S of x^2 (one read of x);
-//   B  k_tn_grids: per chain, the exclusive fp64 prefix of S over its tiles predicts the binade of the
-//      fp32 / fp64 accumulator at each tile's start: g_hi = binade of P (1 + 2^-8); the chain trails the
-//      exact prefix (fp32 chains of randn at 2^25 steps by about 7 %), so g_hi and g_hi - 1 are kept;
-//   C  k_tn_stage<.., true>: per chunk and chain, the maps (Ke, Ko) of its steps under g_hi and g_hi - 1
-//      (second read of x): staged chain-major through LDS so a lane holds 16 consecutive steps of a chain,
-//      lane maps composed in order across the wave;
-//   D  k_tn_resolve: one block per tensor, one wave per chain: the chain's tiles 64 at a time — pick each
-//      tile's map for the exact accumulator's binade, exclusive scan of the maps, and the first tile that
-//      is not covered (a crossing, a miss of the predictor) is resolved in detail: its steps in segments
-//      of 1024, lane maps under the current binade, scanned, the first uncovered lane runs its 16 steps
-//      with fma, and so on. Then the lane sum, tail, sqrt and rounding to the dtype.
-// Short tensors go straight to D with every tile resolved in detail.
+//   A  k_tn_sums: per 8192-element chunk and chain (fp16: piece), the fp64 sum S of x^2 (one read of x);
+//   B  k_tn_winsums + k_tn_grids: per window of 512 tiles the sum of S, then per tile the exclusive prefix P
+//      (earlier windows + a wave scan) predicts the binade of the accumulator at the tile's start:
+//      g = binade(P (1 + 2^-8)) — a prediction only (a miss leaves the tile uncovered, resolved in D);
+//   C  k_tn_maps: per tile, its integer totals on g and g - 1, order-free (k = rint(hi), rint(2 hi)); a
+//      chunk whose squares may hide a tie is listed for k_tn_maps_exact, which stages it chain-major through
+//      LDS and composes each lane's 16 steps as (Ke, Ko) maps in order (second read of x);
+//   C2 k_tn_windows: per window, the composition of its tiles' maps for the two binades it can start in;
+//   D  k_tn_chains: one wave per chain: windows 64 at a time on the exact accumulator's binade, the first one
+//      not covered tile by tile, the first tile not covered in segments of 1024 steps (lane sums or maps on
+//      G and G + 1, scanned; the lane that crosses runs its steps with fma); then k_tn_finish: the lane sum
+//      (fp16: piece sums in order), the tail, sqrt and the rounding to the dtype.
+// fp32 tensors up to kShortMax elements take the in-order walker (torch_norm_walk.h); other short tensors go
+// straight to D with every tile resolved in detail. DESIGN.md §10.
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 #include <hip/hip_fp16.h>
