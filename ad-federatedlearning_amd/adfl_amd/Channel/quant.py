@@ -22,6 +22,7 @@ Contract kept from the reference:
 There is no CPU fallback: without a GPU and the built HIP library these methods raise.
 """
 
+import ctypes
 import os
 import threading
 import time
@@ -49,6 +50,7 @@ class _DeviceStaging:
         self._bufs: Dict[str, torch.Tensor] = {}
         self.layouts: "OrderedDict[Tuple[int, ...], ops.BucketLayout]" = OrderedDict()
         self._d2h: Optional[torch.cuda.Stream] = None
+        self._events: List[int] = []
 
     def d2h_stream(self) -> torch.cuda.Stream:
         """The range-pipelined host paths' copy-back stream: a range's D2H runs here, behind an event on the
@@ -56,6 +58,18 @@ class _DeviceStaging:
         if self._d2h is None:
             self._d2h = torch.cuda.Stream(self.device)
         return self._d2h
+
+    def events(self, n: int) -> List[int]:
+        """n hipEvent_t handles (timing-free, on this device) for the range-pipelined host paths: a range's
+        kernel-done and copied-back events (adfl_stage_*_range). Kept for the staging's life: every call waits
+        for all its ranges' scatters before it returns, so the next call may record them again."""
+        if len(self._events) < n:
+            more = n - len(self._events)
+            arr = (ctypes.c_void_p * more)()
+            with torch.cuda.device(self.device):
+                check(_lib.load().adfl_stage_events_create(more, arr))
+            self._events.extend(int(a) for a in arr)
+        return self._events
 
     def buf(self, key: str, numel: int, dtype: torch.dtype, pinned: bool = False) -> torch.Tensor:
         t = self._bufs.get(key)
@@ -493,6 +507,10 @@ def _encode_host_dict(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _D
     th = _torchhost.get()
     ptrs = th.data_ptrs(tensors).numpy().view(np.uint64)
     ranges = _ranges(lay, 4)
+    evs = st.events(2 * len(ranges))
+    d2h_h = d2h.cuda_stream
+    hx, dx, qd, qh = host.data_ptr(), x_dev.data_ptr(), q_dev.data_ptr(), q_host.data_ptr()
+    pd, ph, sd = part_dev.data_ptr(), part_host.data_ptr(), s_dev.data_ptr()
     jobs = []
     with _ph("enc.gather_submit"):
         for lo, hi in ranges:
@@ -507,43 +525,50 @@ def _encode_host_dict(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _D
     scales = np.zeros(lay.ntensors, dtype=np.float32)
     scatters = []
     made = 0
+    staged: List[Tuple[int, int, int, int, int]] = []   # ranges on the device whose outputs are not built yet
+    r = 0
     try:
-        for (lo, hi), job in zip(ranges, jobs):
-            with _ph("enc.gather_absmax_wait"):
-                job.wait()
-            with _ph("enc.h2d_enqueue"):
-                x_dev[lo:hi].copy_(host[lo:hi], non_blocking=True)
-            done = int(np.searchsorted(ends, hi, side="right"))   # tensors whose every byte is staged
-            if done > made:
+        while r < len(ranges) or staged:
+            # every range whose gather has landed goes to the device at once (the link, not this thread, then
+            # paces the H2D); the thread waits on a gather only when it has no outputs left to build
+            while r < len(ranges) and (not staged or jobs[r].done()):
+                lo, hi = ranges[r]
+                with _ph("enc.gather_absmax_wait"):
+                    jobs[r].wait()
+                done = int(np.searchsorted(ends, hi, side="right"))   # tensors whose every byte is staged
                 with _ph("enc.kernel_launch"):
-                    c0, c1 = int(cm.first[made]), int(cm.cend[done - 1])
-                    part_np[c0:c1] = 0
-                    part_np[cm.first[made:done]] = amax[made:done]
-                    part_dev[c0:c1].copy_(part_host[c0:c1], non_blocking=True)
-                    check(lib.adfl_slq_quantize_batched_range(x_dev.data_ptr(), chunks_ptr, c0, c1 - c0, bits,
-                                                              part_dev.data_ptr(), q_dev.data_ptr(),
-                                                              s_dev.data_ptr(), sh))
-                    e0, e1 = int(lay.offsets[made]), int(ends[done - 1])
-                    d2h.wait_stream(stream)
-                    with torch.cuda.stream(d2h):
-                        q_host[e0:e1].copy_(q_dev[e0:e1], non_blocking=True)
-                    ev = torch.cuda.Event()
-                    ev.record(d2h)
-                with _ph("enc.outputs"):
-                    scales[made:done] = _host_scales(amax[made:done], bits)
-                    # the range's payload tensors in one native call (adfl_torchhost): the qint8 tensors
-                    # torch.quantize_per_tensor(x, scale, 0, torch.qint8) would return, still to be filled
-                    qs, qp = th.empty_qint8_like(tensors[made:done], torch.from_numpy(scales[made:done]))
-                    out_ptrs[made:done] = qp.numpy().view(np.uint64)
-                    sl = scales[made:done].tolist()
-                    for j, q in enumerate(qs):
-                        outs.append(q)
-                        emit(made + j, q, sl[j])
-                with _ph("enc.scatter_submit"):
-                    scatters.append(hostcopy.submit_pieces(
-                        *_range_copies(out_ptrs, lay, q_host.data_ptr(), 1, e0, e1, to_bucket=False),
-                        stream=True, event=ev, keep=q_host))
-                made = done
+                    # one native call: the range's H2D; the quantize of the tensors it completes from the host's
+                    # max|x| bits; their payload bytes back D2H on the side stream behind an event
+                    # (host_stage.hip)
+                    c0 = c1 = e0 = e1 = 0
+                    if done > made:
+                        c0, c1 = int(cm.first[made]), int(cm.cend[done - 1])
+                        part_np[c0:c1] = 0
+                        part_np[cm.first[made:done]] = amax[made:done]
+                        e0, e1 = int(lay.offsets[made]), int(ends[done - 1])
+                    check(lib.adfl_stage_encode_range(hx, dx, lo, hi, ph, pd, chunks_ptr, c0, c1 - c0, bits, qd, sd,
+                                                      qh, e0, e1, sh, d2h_h, evs[2 * r], evs[2 * r + 1]))
+                if done > made:
+                    staged.append((made, done, e0, e1, evs[2 * r + 1]))
+                    made = done
+                r += 1
+            if not staged:
+                continue
+            t0, t1, e0, e1, ev = staged.pop(0)
+            with _ph("enc.outputs"):
+                scales[t0:t1] = _host_scales(amax[t0:t1], bits)
+                # the range's payload tensors in one native call (adfl_torchhost): the qint8 tensors
+                # torch.quantize_per_tensor(x, scale, 0, torch.qint8) would return, still to be filled
+                qs, qp = th.empty_qint8_like(tensors[t0:t1], torch.from_numpy(scales[t0:t1]))
+                out_ptrs[t0:t1] = qp.numpy().view(np.uint64)
+                sl = scales[t0:t1].tolist()
+                for j, q in enumerate(qs):
+                    outs.append(q)
+                    emit(t0 + j, q, sl[j])
+            with _ph("enc.scatter_submit"):
+                scatters.append(hostcopy.submit_pieces(
+                    *_range_copies(out_ptrs, lay, q_host.data_ptr(), 1, e0, e1, to_bucket=False),
+                    stream=True, event=ev, keep=q_host))
             with _ph("enc.passthrough"):
                 idle()
     finally:
@@ -644,8 +669,9 @@ def _int8_view(q: torch.Tensor) -> torch.Tensor:
 
 
 @_serialized
-def _decode_dict(items: List[Tuple[str, torch.Tensor]]) -> Dict[str, torch.Tensor]:
-    """Decode qint8 tensors (per-tensor affine, zero point 0) in one bucketed pass."""
+def _decode_dict(items: List[Tuple[str, torch.Tensor]], idle=None) -> Dict[str, torch.Tensor]:
+    """Decode qint8 tensors (per-tensor affine, zero point 0) in one bucketed pass. idle(): the caller's
+    other entries, run by the pipelined host path while its last copies are in flight (else not at all)."""
     st = _staging()
     dev = st.device
     qlist = [q for _, q in items]
@@ -659,7 +685,7 @@ def _decode_dict(items: List[Tuple[str, torch.Tensor]]) -> Dict[str, torch.Tenso
                 raise ValueError(f"SLQChannel: '{name}' is not a per-tensor qint8 payload with zero point 0")
     lay = st.layout(tuple(numel.tolist()))
     if all_host and _PIPELINE:
-        decoded = _decode_host_dict(qlist, lay, st, ptrs.numpy().view(np.uint64), scales)
+        decoded = _decode_host_dict(qlist, lay, st, ptrs.numpy().view(np.uint64), scales, idle)
         return {name: t for (name, _), t in zip(items, decoded)}
     # CPU qint8 payloads are gathered byte-wise straight from their storage; device ones through int8 views
     all_dev = not all_host and all(q.is_cuda and q.device == dev and q.is_contiguous() for q in qlist)
@@ -680,7 +706,7 @@ def _decode_dict(items: List[Tuple[str, torch.Tensor]]) -> Dict[str, torch.Tenso
 
 
 def _decode_host_dict(qlist: List[torch.Tensor], lay: ops.BucketLayout, st: _DeviceStaging, ptrs: np.ndarray,
-                      scales: torch.Tensor) -> List[torch.Tensor]:
+                      scales: torch.Tensor, idle=None) -> List[torch.Tensor]:
     """CPU qint8 payloads -> owned CPU fp32 tensors, pipelined range by range: the byte gather of every range
     is queued on the native pool at once; as range r lands, its H2D is enqueued, the chunks it completes are
     decoded (adfl_slq_dequantize_batched on that chunk range), their floats go back D2H behind an event, the
@@ -702,6 +728,9 @@ def _decode_host_dict(qlist: List[torch.Tensor], lay: ops.BucketLayout, st: _Dev
     cm = _chunk_meta(lay)
     th = _torchhost.get()
     ranges = _ranges(lay, 4)
+    evs = st.events(2 * len(ranges))
+    d2h_h = d2h.cuda_stream
+    qh, qd, od, oh = q_host.data_ptr(), q_dev.data_ptr(), out_dev.data_ptr(), out_host.data_ptr()
     with _ph("dec.gather_submit"):
         jobs = [hostcopy.submit_pieces(*_range_copies(ptrs, lay, q_host.data_ptr(), 1, lo, hi, to_bucket=True),
                                        keep=q_host) for lo, hi in ranges]
@@ -714,22 +743,22 @@ def _decode_host_dict(qlist: List[torch.Tensor], lay: ops.BucketLayout, st: _Dev
     c_made = 0
     t_made = 0
     try:
-        for (lo, hi), job in zip(ranges, jobs):
+        sd = s_dev.data_ptr()
+        for r, ((lo, hi), job) in enumerate(zip(ranges, jobs)):
             with _ph("dec.gather_wait"):
                 job.wait()
             with _ph("dec.kernel_launch"):
-                q_dev[lo:hi].copy_(q_host[lo:hi], non_blocking=True)
+                # one native call: the range's H2D; the decode of the chunks it completes; their floats back
+                # D2H on the side stream behind an event (host_stage.hip)
                 c_end = int(np.searchsorted(cm.end, hi, side="right"))   # chunks whose every byte is staged
                 if c_end <= c_made:
+                    check(lib.adfl_stage_decode_range(qh, qd, lo, hi, chunks_ptr, 0, 0, sd, od, oh, 0, 0, sh, d2h_h,
+                                                      evs[2 * r], evs[2 * r + 1]))
                     continue
-                check(lib.adfl_slq_dequantize_batched(q_dev.data_ptr(), chunks_ptr + c_made * ctypes_chunk_bytes,
-                                                      c_end - c_made, s_dev.data_ptr(), out_dev.data_ptr(), sh))
                 e0, e1 = int(cm.start[c_made]), int(cm.end[c_end - 1])
-                d2h.wait_stream(stream)
-                with torch.cuda.stream(d2h):
-                    out_host[e0:e1].copy_(out_dev[e0:e1], non_blocking=True)
-                ev = torch.cuda.Event()
-                ev.record(d2h)
+                check(lib.adfl_stage_decode_range(qh, qd, lo, hi, chunks_ptr, c_made, c_end - c_made, sd, od, oh, e0,
+                                                  e1, sh, d2h_h, evs[2 * r], evs[2 * r + 1]))
+                ev = evs[2 * r + 1]
                 c_made = c_end
             with _ph("out.alloc"):
                 t_end = int(np.searchsorted(offs, e1, side="left"))    # tensors starting below e1
@@ -744,6 +773,9 @@ def _decode_host_dict(qlist: List[torch.Tensor], lay: ops.BucketLayout, st: _Dev
                 scatters.append(hostcopy.submit_pieces(
                     *_range_copies(out_ptrs, lay, out_host.data_ptr(), 4, e0, e1, to_bucket=False),
                     stream=True, event=ev, keep=out_host))
+        if idle is not None:
+            with _ph("dec.passthrough"):
+                idle()
     finally:
         for j in jobs:
             j.wait()
@@ -987,15 +1019,23 @@ class SLQChannel(Channel):
         th = _torchhost.get()
         kinds = th.payload_kinds(datas).numpy()   # _dequantize_tensor's cases for every entry in one call
         qi = np.nonzero(kinds == 1)[0].tolist()
-        decoded = _decode_dict([(names[i], datas[i]) for i in qi]) if qi else {}
         vals: List[Optional[torch.Tensor]] = [None] * len(names)
+        rest_done = []
+
+        def rest():   # every entry but the decoded ones; the host decode runs it while its copies land
+            if rest_done:
+                return
+            rest_done.append(True)
+            pi = np.nonzero(kinds == 0)[0].tolist()
+            for i, t in zip(pi, th.variable_data([datas[i] for i in pi])):
+                vals[i] = t  # passthrough: q_param.data.data (quant.py:111-112)
+            for i in np.nonzero(kinds == 2)[0].tolist():
+                vals[i] = datas[i].data.dequantize()  # non-quantized ndim > 1 payload: what quant.py:110 does
+
+        decoded = _decode_dict([(names[i], datas[i]) for i in qi], idle=rest) if qi else {}
         for i in qi:
             vals[i] = decoded[names[i]]
-        pi = np.nonzero(kinds == 0)[0].tolist()
-        for i, t in zip(pi, th.variable_data([datas[i] for i in pi])):
-            vals[i] = t  # passthrough: q_param.data.data (quant.py:111-112)
-        for i in np.nonzero(kinds == 2)[0].tolist():
-            vals[i] = datas[i].data.dequantize()  # non-quantized ndim > 1 payload: what quant.py:110 does
+        rest()
         return dict(zip(names, vals)), time.perf_counter() - s_time
 
     def receive_add_(self, c_params: CompressedParameters, targets: List[Parameters]) -> float:

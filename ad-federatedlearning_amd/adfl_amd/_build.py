@@ -9,7 +9,8 @@ REPO_ROOT = os.path.dirname(SRC_ROOT)
 CSRC = os.path.join(SRC_ROOT, "csrc", "slq_codec.hip")
 SOURCES = [CSRC, os.path.join(SRC_ROOT, "csrc", "stoch_codec.hip"), os.path.join(SRC_ROOT, "csrc", "stoch_dtype.hip"),
            os.path.join(SRC_ROOT, "csrc", "torch_norm.hip"), os.path.join(SRC_ROOT, "csrc", "qerror_ref.hip"),
-           os.path.join(SRC_ROOT, "csrc", "bucket_copy.hip"), os.path.join(SRC_ROOT, "csrc", "host_copy.cpp")]
+           os.path.join(SRC_ROOT, "csrc", "bucket_copy.hip"), os.path.join(SRC_ROOT, "csrc", "host_stage.hip"),
+           os.path.join(SRC_ROOT, "csrc", "host_copy.cpp")]
 DEPENDS = SOURCES + [os.path.join(SRC_ROOT, "csrc", h) for h in ("cnat_log2_table.h", "cnat_log2_dt_table.h", "philox.h", "torch_sum_order.h", "torch_norm_walk.h")]
 INCLUDE = os.path.join(REPO_ROOT, "include")
 LIB_DIR = os.path.join(PKG_DIR, "lib")

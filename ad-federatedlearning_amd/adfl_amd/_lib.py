@@ -101,10 +101,15 @@ SIGNATURES = {
     "adfl_host_threads": (I32, []),
     "adfl_host_copy_submit": (I64, [P, P, P, I64, I32, I32, P, P]),
     "adfl_host_copy_wait": (INT, [I64]),
+    "adfl_host_copy_done": (INT, [I64]),
     "adfl_host_bind": (INT, [P, I32]),
     "adfl_philox_rounds": (INT, []),
     "adfl_host_copy_submit_absmax": (I64, [P, P, P, I64, I32, I32, P, P, P]),
     "adfl_event_synchronize": (INT, [P]),
+    "adfl_stage_events_create": (INT, [I32, P]),
+    "adfl_stage_events_destroy": (INT, [P, I32]),
+    "adfl_stage_encode_range": (INT, [P, P, I64, I64, P, P, P, I64, I64, INT, P, P, P, I64, I64, P, P, P, P]),
+    "adfl_stage_decode_range": (INT, [P, P, I64, I64, P, I64, I64, P, P, P, I64, I64, P, P, P, P]),
 }
 
 NORM_L2, NORM_LINF, NORM_L2_TORCH = 0, 1, 2  # ADFL_NORM_*

@@ -26,7 +26,8 @@ def _host_lib():
         if path:
             lib = ctypes.CDLL(path)
             for name in ("adfl_host_copy", "adfl_host_copy_ex", "adfl_host_threads", "adfl_host_copy_submit",
-                         "adfl_host_copy_wait", "adfl_host_copy_submit_absmax", "adfl_host_bind"):
+                         "adfl_host_copy_wait", "adfl_host_copy_done", "adfl_host_copy_submit_absmax",
+                         "adfl_host_bind"):
                 fn = getattr(lib, name)
                 fn.restype, fn.argtypes = _lib.SIGNATURES[name]
             _host = lib
@@ -70,6 +71,15 @@ class Pending:
             finally:
                 self._keep = None   # only now: the workers may still read the buffers / wait on the event
 
+    def done(self) -> bool:
+        """True once every byte is copied (wait() then returns at once); never blocks."""
+        if not self.ticket:
+            return True
+        r = _host_lib().adfl_host_copy_done(self.ticket)
+        if r < 0:
+            check(int(r))
+        return r == 1
+
     def __del__(self):   # a job is always waited for: its buffers must outlive the copy
         try:
             self.wait()
@@ -89,11 +99,11 @@ def _event_wait_fn() -> int:
 
 
 def submit_pieces(dst_ptrs: Sequence[int], src_ptrs: Sequence[int], nbytes: Sequence[int], *, stream: bool = False,
-                  event: "torch.cuda.Event | None" = None, keep=None, threads: int = 0,
+                  event: "torch.cuda.Event | int | None" = None, keep=None, threads: int = 0,
                   absmax_ptrs: "np.ndarray | None" = None) -> Pending:
-    """copy_pieces on the pool's workers, asynchronously; with `event` (a recorded torch.cuda.Event) every
-    part first waits for it (hipEventSynchronize), so the copy starts the moment the D2H that fills its
-    source lands. `keep`: objects the copy reads or writes, held until wait(). `absmax_ptrs` (uint64 per
+    """copy_pieces on the pool's workers, asynchronously; with `event` (a recorded torch.cuda.Event, or the
+    hipEvent_t handle of one the staging owns, adfl_stage_events_create) every part first waits for it
+    (hipEventSynchronize), so the copy starts the moment the D2H that fills its source lands. `keep`: objects the copy reads or writes, held until wait(). `absmax_ptrs` (uint64 per
     piece, 0 = none): fp32 pieces whose max |bits| is max'ed into the uint32 at that address
     (adfl_host_copy_submit_absmax)."""
     d = np.ascontiguousarray(dst_ptrs, dtype=np.uint64)
@@ -101,7 +111,7 @@ def submit_pieces(dst_ptrs: Sequence[int], src_ptrs: Sequence[int], nbytes: Sequ
     b = np.ascontiguousarray(nbytes, dtype=np.int64)
     if not (len(d) == len(s) == len(b)):
         raise ValueError("submit_pieces: pointer and size lists differ in length")
-    fn, arg = (None, None) if event is None else (_event_wait_fn(), event.cuda_event)
+    fn, arg = (None, None) if event is None else (_event_wait_fn(), event if isinstance(event, int) else event.cuda_event)
     if absmax_ptrs is not None:
         a = np.ascontiguousarray(absmax_ptrs, dtype=np.uint64)
         if len(a) != len(b):

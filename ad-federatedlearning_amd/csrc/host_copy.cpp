@@ -401,6 +401,12 @@ int adfl_host_bind(const int32_t* cpus, int32_t n) {
   return Pool::get().bind(cpus, n) == 0 ? ADFL_OK : ADFL_E_ARG;
 }
 
+int adfl_host_copy_done(int64_t ticket) {
+  if (ticket <= 0) return ADFL_E_ARG;
+  const Job* job = reinterpret_cast<const Job*>(ticket);
+  return job->done.load(std::memory_order_acquire) == job->parts ? 1 : 0;
+}
+
 int adfl_host_copy_wait(int64_t ticket) {
   if (ticket <= 0) return ADFL_E_ARG;
   Job* job = reinterpret_cast<Job*>(ticket);

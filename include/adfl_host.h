@@ -13,6 +13,8 @@
 
 #include <stdint.h>
 
+#include "adfl_slq.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -40,6 +42,9 @@ int adfl_host_copy_ex(void* const* dsts, const void* const* srcs, const int64_t*
 int64_t adfl_host_copy_submit(void* const* dsts, const void* const* srcs, const int64_t* nbytes, int64_t n,
                               int32_t nthreads, int32_t flags, int (*wait_fn)(void*), void* wait_arg);
 int adfl_host_copy_wait(int64_t ticket);
+/* 1 if every part of the job has finished (adfl_host_copy_wait would return at once), 0 if not, ADFL_E_ARG for
+ * a bad ticket. Never blocks and does not consume the ticket. */
+int adfl_host_copy_done(int64_t ticket);
 
 /* adfl_host_copy_submit that also reduces what it copies: piece k is fp32 (nbytes[k] and srcs[k] multiples of
  * 4) and, when absmax_bits[k] is not null, max over its elements of (bits & 0x7fffffff) is max'ed atomically
@@ -59,6 +64,36 @@ int adfl_host_bind(const int32_t* cpus, int32_t n);
 
 /* hipEventSynchronize(event) as an int-returning callback for adfl_host_copy_submit (0 = complete). */
 int adfl_event_synchronize(void* event);
+
+/* ---------------------------------------------------------------------------------------------
+ * Device steps of one staging range of the host-resident channel path (csrc/host_stage.hip): what the
+ * pipelined SLQChannel encode / decode of a CPU state dict (Src/ADFL/Channel/quant.py:74-112 on the dict
+ * Src/ADFL/model.py:195-197 hands over) enqueues as each range of the pinned bucket lands, in one call.
+ * Every step is asynchronous; h_* are PINNED host buffers, d_* device buffers, element offsets throughout.
+ *   stream:      H2D of elements [lo, hi) (hi == lo: none); if count > 0, then the kernel over chunks
+ *                [chunk_begin, chunk_begin + count) of the FULL chunk table d_chunks, then ev_compute
+ *   d2h_stream:  waits for ev_compute, D2H of output elements [e0, e1), records ev_copied — the event the
+ *                host pool's scatter of those elements waits on (adfl_host_copy_submit + adfl_event_synchronize)
+ * Returns 0, ADFL_E_ARG, or a positive hipError_t. count == 0 enqueues the H2D alone.
+ * ------------------------------------------------------------------------------------------- */
+/* n timing-free HIP events on the current device into events[0..n) (the staging keeps them for its life). */
+int adfl_stage_events_create(int32_t n, void** events);
+int adfl_stage_events_destroy(void* const* events, int32_t n);
+
+/* Encode: x range H2D; then h_partials[chunk_begin .. +count) H2D to d_partials (each tensor's max|x| bits
+ * at its first chunk, 0 at the others: adfl_slq_quantize_batched_range), that quantize into d_q / d_scales,
+ * and payload bytes [e0, e1) back into h_q. */
+int adfl_stage_encode_range(const float* h_x, float* d_x, int64_t lo, int64_t hi, const uint32_t* h_partials,
+                            uint32_t* d_partials, const adfl_slq_chunk* d_chunks, int64_t chunk_begin, int64_t count,
+                            int bits, int8_t* d_q, float* d_scales, int8_t* h_q, int64_t e0, int64_t e1, void* stream,
+                            void* d2h_stream, void* ev_compute, void* ev_copied);
+
+/* Decode: payload range H2D; then adfl_slq_dequantize_batched over the chunk range into d_out, and floats
+ * [e0, e1) back into h_out. */
+int adfl_stage_decode_range(const int8_t* h_q, int8_t* d_q, int64_t lo, int64_t hi, const adfl_slq_chunk* d_chunks,
+                            int64_t chunk_begin, int64_t count, const float* d_scales, float* d_out, float* h_out,
+                            int64_t e0, int64_t e1, void* stream, void* d2h_stream, void* ev_compute,
+                            void* ev_copied);
 
 /* Threads the pool would use for nthreads <= 0 (for logging and tests): the CPUs in this process's affinity
  * mask, at most 8, or ADFL_HOST_THREADS when set. */

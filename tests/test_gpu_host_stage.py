@@ -1,0 +1,156 @@
+"""GPU: the native staging-range calls of the host-resident channel path (include/adfl_host.h,
+adfl_stage_encode_range / adfl_stage_decode_range, csrc/host_stage.hip).
+
+A compact ragged bucket is pushed through the calls range by range exactly as the pipelined SLQChannel paths
+drive them (tensors quantized once their last byte is staged, from the host's max|x| bits; chunks decoded once
+staged; ranges that complete nothing enqueue the H2D alone), and the payload, scales and floats that come back
+through pinned memory must equal the one-launch device encode / decode bit for bit (ops.encode_batched /
+decode_batched, themselves pinned to the reference by the channel and golden suites).
+"""
+
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from adfl_amd import _lib, ops  # noqa: E402
+from adfl_amd.Channel import quant  # noqa: E402
+
+DEV = torch.device("cuda", 0)
+E_ARG = -1
+
+
+def _layout(sizes):
+    return ops.BucketLayout(sizes, align=1)
+
+
+def _host_amax_bits(x: np.ndarray, lay) -> np.ndarray:
+    bits = x.view(np.uint32) & np.uint32(0x7FFFFFFF)
+    return np.array([bits[o:o + n].max() for o, n in zip(lay.offsets, lay.sizes)], dtype=np.uint32)
+
+
+def _cuts(total, nranges):
+    c = np.linspace(0, total, nranges + 1).astype(np.int64)
+    return list(zip(c[:-1].tolist(), c[1:].tolist()))
+
+
+@pytest.mark.parametrize("sizes,nranges", [
+    ([1], 1),
+    ([3, 8192, 8193, 5, 70000, 1, 16385], 4),
+    ([100_000] * 3 + [17] * 9 + [250_000], 8),
+    ([8192 * 7 + 3, 2, 40_000, 123_457], 16),   # more ranges than some tensors: ranges that complete nothing
+])
+def test_encode_ranges_match_one_launch(sizes, nranges):
+    lib = _lib.load()
+    lay = _layout(sizes)
+    g = torch.Generator().manual_seed(len(sizes) * 7 + nranges)
+    x = (torch.randn(lay.total, generator=g) * 1e-3)
+    x[::997] *= 40.0
+    x_host = x.pin_memory()
+    x_dev = torch.empty(lay.total, device=DEV)
+    q_dev = torch.empty(lay.total, dtype=torch.int8, device=DEV)
+    q_host = torch.full((lay.total,), 77, dtype=torch.int8).pin_memory()
+    s_dev = torch.full((lay.ntensors,), -1.0, device=DEV)
+    part_dev = torch.empty(lay.nchunks, dtype=torch.int32, device=DEV)
+    part_host = torch.zeros(lay.nchunks, dtype=torch.int32).pin_memory()
+    part_np = part_host.numpy().view(np.uint32)
+    chunks = lay.device_chunks(DEV)
+    cm = quant._chunk_meta(lay)
+    amax = _host_amax_bits(x.numpy(), lay)
+    ends = lay.offsets + lay.sizes
+    evs = (ctypes.c_void_p * (2 * nranges))()
+    assert lib.adfl_stage_events_create(2 * nranges, evs) == 0
+    side = torch.cuda.Stream(DEV)
+    sh = torch.cuda.current_stream(DEV).cuda_stream
+    made = 0
+    try:
+        for r, (lo, hi) in enumerate(_cuts(lay.total, nranges)):
+            done = int(np.searchsorted(ends, hi, side="right"))
+            c0 = c1 = e0 = e1 = 0
+            if done > made:
+                c0, c1 = int(cm.first[made]), int(cm.cend[done - 1])
+                part_np[c0:c1] = 0
+                part_np[cm.first[made:done]] = amax[made:done]
+                e0, e1 = int(lay.offsets[made]), int(ends[done - 1])
+            rc = lib.adfl_stage_encode_range(x_host.data_ptr(), x_dev.data_ptr(), lo, hi, part_host.data_ptr(),
+                                             part_dev.data_ptr(), chunks.data_ptr(), c0, c1 - c0, 8,
+                                             q_dev.data_ptr(), s_dev.data_ptr(), q_host.data_ptr(), e0, e1, sh,
+                                             side.cuda_stream, evs[2 * r], evs[2 * r + 1])
+            assert rc == 0
+            made = done
+        assert made == lay.ntensors
+        torch.cuda.synchronize()
+        q_ref, s_ref = ops.encode_batched(x.to(DEV), lay, 8)
+        assert torch.equal(x_dev.cpu(), x)
+        assert torch.equal(q_host, q_ref.cpu())
+        assert torch.equal(s_dev.cpu().view(torch.int32), s_ref.cpu().view(torch.int32))
+    finally:
+        torch.cuda.synchronize()
+        lib.adfl_stage_events_destroy(evs, 2 * nranges)
+
+
+@pytest.mark.parametrize("sizes,nranges", [
+    ([1], 1),
+    ([3, 8192, 8193, 5, 70000, 1, 16385], 4),
+    ([100_000] * 3 + [17] * 9 + [250_000], 8),
+    ([8192 * 7 + 3, 2, 40_000, 123_457], 32),
+])
+def test_decode_ranges_match_one_launch(sizes, nranges):
+    lib = _lib.load()
+    lay = _layout(sizes)
+    g = torch.Generator().manual_seed(len(sizes) * 11 + nranges)
+    q = torch.randint(-128, 128, (lay.total,), generator=g, dtype=torch.int8)
+    scales = torch.rand(lay.ntensors, generator=g) * 1e-4
+    q_host = q.pin_memory()
+    q_dev = torch.empty(lay.total, dtype=torch.int8, device=DEV)
+    out_dev = torch.empty(lay.total, device=DEV)
+    out_host = torch.full((lay.total,), float("nan")).pin_memory()
+    s_dev = scales.to(DEV)
+    chunks = lay.device_chunks(DEV)
+    cm = quant._chunk_meta(lay)
+    evs = (ctypes.c_void_p * (2 * nranges))()
+    assert lib.adfl_stage_events_create(2 * nranges, evs) == 0
+    side = torch.cuda.Stream(DEV)
+    sh = torch.cuda.current_stream(DEV).cuda_stream
+    c_made = 0
+    try:
+        for r, (lo, hi) in enumerate(_cuts(lay.total, nranges)):
+            c_end = int(np.searchsorted(cm.end, hi, side="right"))
+            if c_end <= c_made:
+                rc = lib.adfl_stage_decode_range(q_host.data_ptr(), q_dev.data_ptr(), lo, hi, chunks.data_ptr(), 0, 0,
+                                                 s_dev.data_ptr(), out_dev.data_ptr(), out_host.data_ptr(), 0, 0, sh,
+                                                 side.cuda_stream, evs[2 * r], evs[2 * r + 1])
+            else:
+                e0, e1 = int(cm.start[c_made]), int(cm.end[c_end - 1])
+                rc = lib.adfl_stage_decode_range(q_host.data_ptr(), q_dev.data_ptr(), lo, hi, chunks.data_ptr(),
+                                                 c_made, c_end - c_made, s_dev.data_ptr(), out_dev.data_ptr(),
+                                                 out_host.data_ptr(), e0, e1, sh, side.cuda_stream, evs[2 * r],
+                                                 evs[2 * r + 1])
+                c_made = c_end
+            assert rc == 0
+        assert c_made == lay.nchunks
+        torch.cuda.synchronize()
+        ref = ops.decode_batched(q.to(DEV), s_dev, lay).cpu()
+        assert torch.equal(out_host.view(torch.int32), ref.view(torch.int32))
+    finally:
+        torch.cuda.synchronize()
+        lib.adfl_stage_events_destroy(evs, 2 * nranges)
+
+
+def test_stage_argument_errors():
+    lib = _lib.load()
+    buf = torch.empty(64, device=DEV)
+    hb = torch.empty(64).pin_memory()
+    p = buf.data_ptr()
+    h = hb.data_ptr()
+    # a negative count, a reversed range, a kernel range with no events: refused, nothing enqueued
+    assert lib.adfl_stage_encode_range(h, p, 0, 64, h, p, p, 0, -1, 8, p, p, h, 0, 64, None, None, None, None) == E_ARG
+    assert lib.adfl_stage_encode_range(h, p, 10, 5, h, p, p, 0, 0, 8, p, p, h, 0, 0, None, None, None, None) == E_ARG
+    assert lib.adfl_stage_encode_range(h, p, 0, 64, h, p, p, 0, 1, 8, p, p, h, 0, 64, None, None, None, None) == E_ARG
+    assert lib.adfl_stage_decode_range(h, p, 0, 64, p, 0, 1, p, p, h, 0, 64, None, None, None, None) == E_ARG
+    assert lib.adfl_stage_decode_range(None, p, 0, 64, p, 0, 0, p, p, h, 0, 0, None, None, None, None) == E_ARG
+    assert lib.adfl_stage_events_create(-1, None) == E_ARG
+    torch.cuda.synchronize()

@@ -26,8 +26,10 @@ def test_copy_waits_for_the_event(pieces):
     dst = torch.zeros(n)
     src_dev = torch.arange(n, dtype=torch.float32, device=DEV)
     stream = torch.cuda.current_stream(DEV)
+    scratch = torch.empty(n).pin_memory()
     torch.cuda.synchronize()
-    torch.cuda._sleep(50_000_000)
+    for _ in range(8):                          # ~40 ms of D2H queued in front of the one the copy waits for
+        scratch.copy_(src_dev, non_blocking=True)
     pinned.copy_(src_dev, non_blocking=True)
     ev = torch.cuda.Event()
     ev.record(stream)
@@ -39,7 +41,7 @@ def test_copy_waits_for_the_event(pieces):
     t0 = time.perf_counter()
     job = hostcopy.submit_pieces(d, s, b, event=ev, keep=(pinned, dst))
     submit_s = time.perf_counter() - t0
-    assert not ev.query()                       # the D2H is still behind the sleep: the copy must wait
+    assert not ev.query()                       # the D2H is still behind the others: the copy must wait
     job.wait()
     assert ev.query()
     assert torch.equal(dst, src_dev.cpu()), "copied before the event completed"

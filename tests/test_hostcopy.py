@@ -2,6 +2,7 @@
 equal numpy's, from one and from several Python threads at once."""
 
 import threading
+import time
 
 import numpy as np
 import pytest
@@ -121,8 +122,24 @@ def test_async_submit_and_wait():
         assert torch.equal(s, d)
     lib = _lib.load()
     assert lib.adfl_host_copy_wait(0) == -1
+    assert lib.adfl_host_copy_done(0) == -1
     with pytest.raises(ValueError):
         hostcopy.submit_pieces([1, 2], [3], [4])
+
+
+def test_async_done_polls_without_consuming():
+    """Pending.done() (adfl_host_copy_done): never blocks, turns True once the copy has finished, and leaves
+    the ticket to wait() (the encode enqueues every landed range before building outputs)."""
+    s = torch.randn(4_000_000)
+    d = torch.zeros_like(s)
+    job = hostcopy.submit_pieces([d.data_ptr()], [s.data_ptr()], [s.numel() * 4], keep=(s, d))
+    deadline = time.monotonic() + 30
+    while not job.done():
+        assert time.monotonic() < deadline
+        time.sleep(1e-4)
+    assert job.ticket != 0   # done() did not consume it
+    job.wait()
+    assert job.done() and torch.equal(s, d)
 
 
 def test_async_gather_reduces_absmax_bits():

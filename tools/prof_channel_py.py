@@ -18,9 +18,11 @@ pr = cProfile.Profile(); pr.enable()
 for _ in range(10):
     qp, _ = ch.on_client_send(params)
 pr.disable()
-pstats.Stats(pr).sort_stats("tottime").print_stats(15)
+pstats.Stats(pr).sort_stats("tottime").print_stats(25)
+pstats.Stats(pr).sort_stats("cumulative").print_stats(30)
 pr = cProfile.Profile(); pr.enable()
 for _ in range(10):
     ch.on_server_receive(qp)
 pr.disable()
-pstats.Stats(pr).sort_stats("tottime").print_stats(15)
+pstats.Stats(pr).sort_stats("tottime").print_stats(25)
+pstats.Stats(pr).sort_stats("cumulative").print_stats(30)
