@@ -475,16 +475,18 @@ def _encode_host_dict(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _D
                       stats: Optional[list], emit, idle):
     """The all-CPU fp32 dict's encode, pipelined range by range across the host, the link and the GPU.
 
-    The gather into the pinned bucket is queued on the native pool range by range and reduces max|x| per
-    tensor as it copies (adfl_host_copy_submit_absmax), so a tensor's scale is known on the host as soon as
-    its last byte is staged. For each staging range, as its gather lands: its H2D is enqueued; the tensors it
-    completes are quantized at once (adfl_slq_quantize_batched_range over their chunks, from the host's max|x|
-    bits as partials: the same scales the two-pass encode computes), their payload bytes go back D2H behind
-    an event, their qint8 outputs are created (one native call) and emit(k, q, scale) builds each payload
-    object, and the scatter into those outputs is queued on the pool behind the event — so the D2H and
-    scatter of range r overlap the H2D of range r + 1. `idle()` (the caller's other payload objects) runs in
-    between. The device's scales are checked against the host's at the end. Returns [(q, scale)] per
-    tensor."""
+    The gather into the pinned bucket is queued on the native pool range by range. As each range lands (the
+    thread enqueues every landed range before it builds outputs), one native call (adfl_stage_encode_range)
+    enqueues its H2D and, for the tensors whose every byte is now staged, the device's absmax and quantize
+    over their chunks (adfl_slq_absmax_batched_range + adfl_slq_quantize_batched_range: the two-pass encode's
+    kernels, so the same payload and scales), then their payload bytes' D2H on a side stream behind an event.
+    The D2H and scatter of range r overlap the H2D of range r + 1.
+    The outputs are built while the copies run: the gather also reduces max|x| per tensor as it copies
+    (adfl_host_copy_submit_absmax), so the host knows each scale in time to create the qint8 outputs (one
+    native call per range) and emit(k, q, scale) each payload object, and the scatter into them is queued on
+    the pool behind the range's event. `idle()` (the caller's other payload objects) runs in between. The
+    payload bytes and scales are the device's: its scales are compared with the host's at the end and any
+    output whose host scale differed is rebuilt with the device's. Returns [(q, scale)] per tensor."""
     with _ph("enc.heap"):
         _host_heap(lay)
     dev = st.device
@@ -497,8 +499,6 @@ def _encode_host_dict(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _D
     q_host = st.buf("q_host", lay.total, torch.int8, pinned=True)
     s_dev = st.buf("scales", lay.ntensors, torch.float32)
     part_dev = st.buf("partials", lay.nchunks, torch.int32)
-    part_host = st.buf("partials_host", lay.nchunks, torch.int32, pinned=True)
-    part_np = part_host.numpy().view(np.uint32)
     chunks_ptr = lay.device_chunks(dev).data_ptr()
     d2h = st.d2h_stream()
     cm = _chunk_meta(lay)
@@ -510,7 +510,7 @@ def _encode_host_dict(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _D
     evs = st.events(2 * len(ranges))
     d2h_h = d2h.cuda_stream
     hx, dx, qd, qh = host.data_ptr(), x_dev.data_ptr(), q_dev.data_ptr(), q_host.data_ptr()
-    pd, ph, sd = part_dev.data_ptr(), part_host.data_ptr(), s_dev.data_ptr()
+    pd, sd = part_dev.data_ptr(), s_dev.data_ptr()
     jobs = []
     with _ph("enc.gather_submit"):
         for lo, hi in ranges:
@@ -537,17 +537,14 @@ def _encode_host_dict(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _D
                     jobs[r].wait()
                 done = int(np.searchsorted(ends, hi, side="right"))   # tensors whose every byte is staged
                 with _ph("enc.kernel_launch"):
-                    # one native call: the range's H2D; the quantize of the tensors it completes from the host's
-                    # max|x| bits; their payload bytes back D2H on the side stream behind an event
-                    # (host_stage.hip)
+                    # one native call: the range's H2D; the device's absmax and quantize of the tensors it
+                    # completes; their payload bytes back D2H on the side stream behind an event (host_stage.hip)
                     c0 = c1 = e0 = e1 = 0
                     if done > made:
                         c0, c1 = int(cm.first[made]), int(cm.cend[done - 1])
-                        part_np[c0:c1] = 0
-                        part_np[cm.first[made:done]] = amax[made:done]
                         e0, e1 = int(lay.offsets[made]), int(ends[done - 1])
-                    check(lib.adfl_stage_encode_range(hx, dx, lo, hi, ph, pd, chunks_ptr, c0, c1 - c0, bits, qd, sd,
-                                                      qh, e0, e1, sh, d2h_h, evs[2 * r], evs[2 * r + 1]))
+                    check(lib.adfl_stage_encode_range(hx, dx, lo, hi, pd, chunks_ptr, c0, c1 - c0, bits, qd, sd, qh,
+                                                      e0, e1, sh, d2h_h, evs[2 * r], evs[2 * r + 1]))
                 if done > made:
                     staged.append((made, done, e0, e1, evs[2 * r + 1]))
                     made = done
@@ -591,7 +588,8 @@ def _encode_host_dict(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _D
     dev_scales = scales_host.numpy()
     bad = np.nonzero(dev_scales.view(np.uint32) != scales.view(np.uint32))[0]
     res = [(q, float(sc)) for q, sc in zip(outs, scales)]
-    for k in bad.tolist():   # never seen: both reduce the same bits and divide correctly rounded
+    for k in bad.tolist():   # never seen (both reduce the same magnitude bits and divide correctly rounded):
+        # the device's scale is the one the payload was quantized with
         sc = float(dev_scales[k])
         q = torch._make_per_tensor_quantized_tensor(_int8_view(outs[k]), sc, 0)
         res[k] = (q, sc)

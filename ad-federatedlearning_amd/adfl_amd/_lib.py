@@ -51,6 +51,7 @@ SIGNATURES = {
     "adfl_slq_encode_batched_work": (INT, [P, P, I64, P, I64, INT, P, P, P, P]),
     "adfl_slq_dequantize_batched": (INT, [P, P, I64, P, P, P]),
     "adfl_slq_quantize_batched_range": (INT, [P, P, I64, I64, INT, P, P, P, P]),
+    "adfl_slq_absmax_batched_range": (INT, [P, P, I64, I64, P, P]),
     "adfl_slq_qerror_batched": (INT, [P, P, P, I64, P, P, P]),
     "adfl_slq_qerror_batched_int4": (INT, [P, P, P, I64, P, P, P]),
     "adfl_slq_encode_batched_int4": (INT, [P, P, I64, INT, P, P, P, P]),
@@ -108,7 +109,7 @@ SIGNATURES = {
     "adfl_event_synchronize": (INT, [P]),
     "adfl_stage_events_create": (INT, [I32, P]),
     "adfl_stage_events_destroy": (INT, [P, I32]),
-    "adfl_stage_encode_range": (INT, [P, P, I64, I64, P, P, P, I64, I64, INT, P, P, P, I64, I64, P, P, P, P]),
+    "adfl_stage_encode_range": (INT, [P, P, I64, I64, P, P, I64, I64, INT, P, P, P, I64, I64, P, P, P, P]),
     "adfl_stage_decode_range": (INT, [P, P, I64, I64, P, I64, I64, P, P, P, I64, I64, P, P, P, P]),
 }
 

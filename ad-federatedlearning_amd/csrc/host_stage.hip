@@ -11,8 +11,8 @@
 // they are the HIP calls alone.
 //
 // Order per range, every step asynchronous:
-//   stream:      H2D [lo, hi) of the input; if count > 0: (encode) H2D of the chunk range's absmax partials,
-//                the kernel over chunks [chunk_begin, chunk_begin + count), record ev_compute
+//   stream:      H2D [lo, hi) of the input; if count > 0: (encode) the absmax and quantize kernels, (decode) the
+//                dequantize kernel, over chunks [chunk_begin, chunk_begin + count), record ev_compute
 //   d2h_stream:  wait ev_compute, D2H [e0, e1) of the output, record ev_copied (the host pool's scatter of
 //                that range waits on it through adfl_event_synchronize)
 
@@ -66,13 +66,13 @@ int adfl_stage_events_destroy(void* const* events, int32_t n) {
   return first;
 }
 
-int adfl_stage_encode_range(const float* h_x, float* d_x, int64_t lo, int64_t hi, const uint32_t* h_partials,
-                            uint32_t* d_partials, const adfl_slq_chunk* d_chunks, int64_t chunk_begin, int64_t count,
-                            int bits, int8_t* d_q, float* d_scales, int8_t* h_q, int64_t e0, int64_t e1, void* stream,
-                            void* d2h_stream, void* ev_compute, void* ev_copied) {
+int adfl_stage_encode_range(const float* h_x, float* d_x, int64_t lo, int64_t hi, uint32_t* d_partials,
+                            const adfl_slq_chunk* d_chunks, int64_t chunk_begin, int64_t count, int bits, int8_t* d_q,
+                            float* d_scales, int8_t* h_q, int64_t e0, int64_t e1, void* stream, void* d2h_stream,
+                            void* ev_compute, void* ev_copied) {
   if (!h_x || !d_x || lo < 0 || hi < lo || count < 0) return ADFL_E_ARG;
-  if (count > 0 && (!h_partials || !d_partials || !d_chunks || !d_q || !d_scales || !h_q || chunk_begin < 0 ||
-                    e0 < 0 || e1 <= e0 || !d2h_stream || !ev_compute || !ev_copied))
+  if (count > 0 && (!d_partials || !d_chunks || !d_q || !d_scales || !h_q || chunk_begin < 0 || e0 < 0 || e1 <= e0 ||
+                    !d2h_stream || !ev_compute || !ev_copied))
     return ADFL_E_ARG;
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (hi > lo) {
@@ -80,9 +80,9 @@ int adfl_stage_encode_range(const float* h_x, float* d_x, int64_t lo, int64_t hi
       return s;
   }
   if (count == 0) return 0;
-  if (int s = hip_status(hipMemcpyAsync(d_partials + chunk_begin, h_partials + chunk_begin, (size_t)count * 4,
-                                        hipMemcpyHostToDevice, st)))
-    return s;
+  // the device's own max|x| over the completed tensors' chunks (just landed, so read from the caches), then
+  // their quantize: the scales and payload never depend on anything the host reduced
+  if (int s = adfl_slq_absmax_batched_range(d_x, d_chunks, chunk_begin, count, d_partials, stream)) return s;
   if (int s = adfl_slq_quantize_batched_range(d_x, d_chunks, chunk_begin, count, bits, d_partials, d_q, d_scales,
                                               stream))
     return s;

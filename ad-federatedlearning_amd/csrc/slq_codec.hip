@@ -611,10 +611,13 @@ __device__ __forceinline__ void chunk_store(const adfl_slq_chunk& c, const Chunk
 // Pass 1: one partial per chunk, all of the chunk's loads in flight. Non-temporal: in the C3 config
 // bench, allocating loads (x left in the Infinity Cache for pass 2) measured the same (A/B in
 // profiles/r01/c3_absmax_policy.txt), and NT leaves the cache to the payload.
+// chunk_base: the first chunk of the launch (adfl_slq_absmax_batched_range; 0 for the whole table).
 __global__ __launch_bounds__(kBlock) void k_absmax_batched(const float* __restrict__ x,
                                                            const adfl_slq_chunk* __restrict__ chunks,
-                                                           uint32_t* __restrict__ partials) {
-  const adfl_slq_chunk c = chunks[blockIdx.x];
+                                                           uint32_t* __restrict__ partials,
+                                                           int64_t chunk_base = 0) {
+  const int64_t ci = chunk_base + blockIdx.x;
+  const adfl_slq_chunk c = chunks[ci];
   const float* xc = x + c.start;
   const int head = chunk_head(c.start, c.len, 4);
   const float4* x4 = reinterpret_cast<const float4*>(xc + head);
@@ -633,7 +636,7 @@ __global__ __launch_bounds__(kBlock) void k_absmax_batched(const float* __restri
 #pragma unroll
   for (int k = 0; k < U; ++k) m = max(m, abs_bits4(v[k]));
   m = block_max(m);
-  if (threadIdx.x == 0) partials[blockIdx.x] = m;
+  if (threadIdx.x == 0) partials[ci] = m;
 }
 
 // Pass 2: the chunk's loads are issued before the partial reduction, whose latency they hide.
@@ -1262,6 +1265,15 @@ int adfl_slq_quantize_batched_range(const float* d_x, const adfl_slq_chunk* d_ch
   if (!aligned16(d_x) || !aligned16(d_q)) return ADFL_E_ALIGN;
   hipLaunchKernelGGL(k_quantize_batched, dim3((unsigned)count), dim3(kBlock), 0, (hipStream_t)stream, d_x, d_chunks,
                      qmax_f(bits), d_partials, d_q, d_scales, chunk_begin);
+  return launch_status();
+}
+
+int adfl_slq_absmax_batched_range(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t chunk_begin, int64_t count,
+                                  uint32_t* d_partials, void* stream) {
+  if (!d_x || !d_chunks || !d_partials || chunk_begin < 0 || count < 1 || count > INT32_MAX) return ADFL_E_ARG;
+  if (!aligned16(d_x)) return ADFL_E_ALIGN;
+  hipLaunchKernelGGL(k_absmax_batched, dim3((unsigned)count), dim3(kBlock), 0, (hipStream_t)stream, d_x, d_chunks,
+                     d_partials, chunk_begin);
   return launch_status();
 }
 

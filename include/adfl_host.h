@@ -80,13 +80,13 @@ int adfl_event_synchronize(void* event);
 int adfl_stage_events_create(int32_t n, void** events);
 int adfl_stage_events_destroy(void* const* events, int32_t n);
 
-/* Encode: x range H2D; then h_partials[chunk_begin .. +count) H2D to d_partials (each tensor's max|x| bits
- * at its first chunk, 0 at the others: adfl_slq_quantize_batched_range), that quantize into d_q / d_scales,
- * and payload bytes [e0, e1) back into h_q. */
-int adfl_stage_encode_range(const float* h_x, float* d_x, int64_t lo, int64_t hi, const uint32_t* h_partials,
-                            uint32_t* d_partials, const adfl_slq_chunk* d_chunks, int64_t chunk_begin, int64_t count,
-                            int bits, int8_t* d_q, float* d_scales, int8_t* h_q, int64_t e0, int64_t e1, void* stream,
-                            void* d2h_stream, void* ev_compute, void* ev_copied);
+/* Encode: x range H2D; then, over the chunk range (whole tensors, every byte of them staged),
+ * adfl_slq_absmax_batched_range into d_partials (one uint32 per chunk of the table) and
+ * adfl_slq_quantize_batched_range into d_q / d_scales, and payload bytes [e0, e1) back into h_q. */
+int adfl_stage_encode_range(const float* h_x, float* d_x, int64_t lo, int64_t hi, uint32_t* d_partials,
+                            const adfl_slq_chunk* d_chunks, int64_t chunk_begin, int64_t count, int bits, int8_t* d_q,
+                            float* d_scales, int8_t* h_q, int64_t e0, int64_t e1, void* stream, void* d2h_stream,
+                            void* ev_compute, void* ev_copied);
 
 /* Decode: payload range H2D; then adfl_slq_dequantize_batched over the chunk range into d_out, and floats
  * [e0, e1) back into h_out. */

@@ -125,6 +125,11 @@ int adfl_slq_dequantize_batched(const int8_t* d_q, const adfl_slq_chunk* d_chunk
 int adfl_slq_quantize_batched_range(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t chunk_begin,
                                     int64_t count, int bits, const uint32_t* d_partials, int8_t* d_q,
                                     float* d_scales, void* stream);
+/* The absmax pass of adfl_slq_encode_batched over chunks [chunk_begin, chunk_begin + count) of the FULL chunk
+ * table: d_partials[c] = the max|x| bits of chunk c (torch.max(torch.abs(t)), quant.py:100, NaN winning) for
+ * every c in the range, the partials adfl_slq_quantize_batched_range then reduces per tensor. */
+int adfl_slq_absmax_batched_range(const float* d_x, const adfl_slq_chunk* d_chunks, int64_t chunk_begin, int64_t count,
+                                  uint32_t* d_partials, void* stream);
 
 /* Quantization error of a bucket against its own payload without materialising the decode — the
  * metrics Src/ADFL/Client/worker.py:186-189 computes with parameter_relative_mse /

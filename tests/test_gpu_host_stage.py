@@ -2,7 +2,7 @@
 adfl_stage_encode_range / adfl_stage_decode_range, csrc/host_stage.hip).
 
 A compact ragged bucket is pushed through the calls range by range exactly as the pipelined SLQChannel paths
-drive them (tensors quantized once their last byte is staged, from the host's max|x| bits; chunks decoded once
+drive them (tensors reduced and quantized on the device once their last byte is staged; chunks decoded once
 staged; ranges that complete nothing enqueue the H2D alone), and the payload, scales and floats that come back
 through pinned memory must equal the one-launch device encode / decode bit for bit (ops.encode_batched /
 decode_batched, themselves pinned to the reference by the channel and golden suites).
@@ -27,11 +27,6 @@ def _layout(sizes):
     return ops.BucketLayout(sizes, align=1)
 
 
-def _host_amax_bits(x: np.ndarray, lay) -> np.ndarray:
-    bits = x.view(np.uint32) & np.uint32(0x7FFFFFFF)
-    return np.array([bits[o:o + n].max() for o, n in zip(lay.offsets, lay.sizes)], dtype=np.uint32)
-
-
 def _cuts(total, nranges):
     c = np.linspace(0, total, nranges + 1).astype(np.int64)
     return list(zip(c[:-1].tolist(), c[1:].tolist()))
@@ -54,12 +49,9 @@ def test_encode_ranges_match_one_launch(sizes, nranges):
     q_dev = torch.empty(lay.total, dtype=torch.int8, device=DEV)
     q_host = torch.full((lay.total,), 77, dtype=torch.int8).pin_memory()
     s_dev = torch.full((lay.ntensors,), -1.0, device=DEV)
-    part_dev = torch.empty(lay.nchunks, dtype=torch.int32, device=DEV)
-    part_host = torch.zeros(lay.nchunks, dtype=torch.int32).pin_memory()
-    part_np = part_host.numpy().view(np.uint32)
+    part_dev = torch.full((lay.nchunks,), -1, dtype=torch.int32, device=DEV)
     chunks = lay.device_chunks(DEV)
     cm = quant._chunk_meta(lay)
-    amax = _host_amax_bits(x.numpy(), lay)
     ends = lay.offsets + lay.sizes
     evs = (ctypes.c_void_p * (2 * nranges))()
     assert lib.adfl_stage_events_create(2 * nranges, evs) == 0
@@ -72,11 +64,9 @@ def test_encode_ranges_match_one_launch(sizes, nranges):
             c0 = c1 = e0 = e1 = 0
             if done > made:
                 c0, c1 = int(cm.first[made]), int(cm.cend[done - 1])
-                part_np[c0:c1] = 0
-                part_np[cm.first[made:done]] = amax[made:done]
                 e0, e1 = int(lay.offsets[made]), int(ends[done - 1])
-            rc = lib.adfl_stage_encode_range(x_host.data_ptr(), x_dev.data_ptr(), lo, hi, part_host.data_ptr(),
-                                             part_dev.data_ptr(), chunks.data_ptr(), c0, c1 - c0, 8,
+            rc = lib.adfl_stage_encode_range(x_host.data_ptr(), x_dev.data_ptr(), lo, hi, part_dev.data_ptr(),
+                                             chunks.data_ptr(), c0, c1 - c0, 8,
                                              q_dev.data_ptr(), s_dev.data_ptr(), q_host.data_ptr(), e0, e1, sh,
                                              side.cuda_stream, evs[2 * r], evs[2 * r + 1])
             assert rc == 0
@@ -87,6 +77,10 @@ def test_encode_ranges_match_one_launch(sizes, nranges):
         assert torch.equal(x_dev.cpu(), x)
         assert torch.equal(q_host, q_ref.cpu())
         assert torch.equal(s_dev.cpu().view(torch.int32), s_ref.cpu().view(torch.int32))
+        # the device reduced every chunk itself: its partials are each chunk's max|x| bits
+        bits = x.numpy().view(np.uint32) & np.uint32(0x7FFFFFFF)
+        want = np.array([bits[a:b].max() for a, b in zip(cm.start, cm.end)], dtype=np.uint32)
+        assert np.array_equal(part_dev.cpu().numpy().view(np.uint32), want)
     finally:
         torch.cuda.synchronize()
         lib.adfl_stage_events_destroy(evs, 2 * nranges)
@@ -147,10 +141,32 @@ def test_stage_argument_errors():
     p = buf.data_ptr()
     h = hb.data_ptr()
     # a negative count, a reversed range, a kernel range with no events: refused, nothing enqueued
-    assert lib.adfl_stage_encode_range(h, p, 0, 64, h, p, p, 0, -1, 8, p, p, h, 0, 64, None, None, None, None) == E_ARG
-    assert lib.adfl_stage_encode_range(h, p, 10, 5, h, p, p, 0, 0, 8, p, p, h, 0, 0, None, None, None, None) == E_ARG
-    assert lib.adfl_stage_encode_range(h, p, 0, 64, h, p, p, 0, 1, 8, p, p, h, 0, 64, None, None, None, None) == E_ARG
+    assert lib.adfl_stage_encode_range(h, p, 0, 64, p, p, 0, -1, 8, p, p, h, 0, 64, None, None, None, None) == E_ARG
+    assert lib.adfl_stage_encode_range(h, p, 10, 5, p, p, 0, 0, 8, p, p, h, 0, 0, None, None, None, None) == E_ARG
+    assert lib.adfl_stage_encode_range(h, p, 0, 64, p, p, 0, 1, 8, p, p, h, 0, 64, None, None, None, None) == E_ARG
+    assert lib.adfl_slq_absmax_batched_range(p, p, 0, 0, p, None) == E_ARG
     assert lib.adfl_stage_decode_range(h, p, 0, 64, p, 0, 1, p, p, h, 0, 64, None, None, None, None) == E_ARG
     assert lib.adfl_stage_decode_range(None, p, 0, 64, p, 0, 0, p, p, h, 0, 0, None, None, None, None) == E_ARG
     assert lib.adfl_stage_events_create(-1, None) == E_ARG
     torch.cuda.synchronize()
+
+
+def test_channel_payload_and_scales_are_the_devices(monkeypatch):
+    """The host's max|x| (reduced during the gather) only lets the channel build the qint8 outputs early: the
+    payload and the scale of every entry are the device's. With the host's scales deliberately off by one ulp
+    the channel must still return exactly what it returns normally."""
+    from adfl_amd.Channel import SLQChannel
+    g = torch.Generator().manual_seed(3)
+    params = {f"l{i}.weight": torch.randn(17, 300 + 97 * i, generator=g) * 1e-3 for i in range(12)}
+    params.update({f"l{i}.bias": torch.randn(17, generator=g) for i in range(12)})
+    ch = SLQChannel(8)
+    want, _ = ch.on_client_send(params)
+    real = quant._host_scales
+    monkeypatch.setattr(quant, "_host_scales", lambda a, b: np.nextafter(real(a, b), np.float32(np.inf)))
+    got, _ = ch.on_client_send(params)
+    for n, p in want.params.items():
+        q = got.params[n]
+        assert q.scale == p.scale
+        if p.data.is_quantized:
+            assert q.data.q_scale() == p.data.q_scale()
+            assert torch.equal(q.data.int_repr(), p.data.int_repr())
