@@ -37,14 +37,17 @@ import os
 import time
 from typing import Dict, List, Tuple
 
+import numpy as np
 import torch
 
-from .. import hostcopy, ops
+from .. import _lib, _torchhost, hostcopy, ops
 from .. import stoch as sops
+from .._lib import check
 from ..model import CompressedParameters, Parameters, QuantParameter, QuantParameters, get_parameter_info
 from .channel import Channel, IdentityChannel
-from .quant import (_PendingD2H, _aggregate_entries, _hand_out, _serialized, _stage_in, _stage_rows, _staging,
-                    device_mean_order_ok)
+from . import quant as _quant
+from .quant import (_PendingD2H, _aggregate_entries, _chunk_meta, _hand_out, _host_heap, _ph, _range_copies,
+                    _ranges, _serialized, _stage_in, _stage_rows, _staging, device_mean_order_ok)
 
 _CODECS = ("qsgd", "rqsgd", "cnat")
 
@@ -100,8 +103,11 @@ def _encode_stoch(params: Parameters, names: List[str], codec: str, bits: int, u
     st = _staging()
     dev = st.device
     tensors = [params[n] for n in names]
-    lay = st.layout(tuple(int(t.numel()) for t in tensors))
-    x_dev = _stage_in(tensors, lay, st, "x", torch.float32)
+    # every tensor's size, and whether all are contiguous CPU fp32 storages (their pointers), in one native call
+    th = _torchhost.get()
+    host_ok, numel, hptrs = th.host_bytes(tensors, 4)
+    lay = st.layout(tuple(numel.tolist()))
+    x_dev = _stage_in(tensors, lay, st, "x", torch.float32, host_ptrs=hptrs.numpy().view(np.uint64) if host_ok else None)
     if seed is None:
         seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
     ws = st.buf("stoch_ws", lay.nchunks * 16, torch.uint8)
@@ -126,10 +132,25 @@ def _encode_stoch(params: Parameters, names: List[str], codec: str, bits: int, u
     nm_host[:lay.ntensors].copy_(norms, non_blocking=True)
     if mins is not None:
         nm_host[lay.ntensors:].copy_(mins, non_blocking=True)
+    if host_ok:
+        # as SLQ's encode: both planes' D2H enqueued right behind the norms, the owned outputs of both planes
+        # created by one native call each while they run, each range scattered as it lands
+        norms_ready = torch.cuda.Event()
+        norms_ready.record(torch.cuda.current_stream(dev))
+        pend_lv = _PendingD2H(lv.view(torch.uint8), lay, st, "s_levels")
+        pend_sg = _PendingD2H(sg, lay, st, "s_signs")
+        lv_parts, lv_p = th.empty_like_dtype(tensors, 1 if lv.dtype == torch.int8 else 0)
+        sg_parts, sg_p = th.empty_like_dtype(tensors, 1)
+        big = np.nonzero(lay.sizes >= (4 << 20))[0].tolist()
+        if big:
+            hostcopy.advise_huge([lv_parts[i] for i in big] + [sg_parts[i] for i in big])
+        pend_lv.finish(lv_parts, lv_p.numpy().view(np.uint64))
+        pend_sg.finish(sg_parts, sg_p.numpy().view(np.uint64))
+        norms_ready.synchronize()
+        return _payloads(names, lv_parts, sg_parts, nm_host.tolist(), lay.ntensors, codec)
     on_cpu = [not t.is_cuda for t in tensors]
     if all(on_cpu):
-        # as SLQ's encode: both planes' D2H enqueued right behind the norms, the owned outputs allocated
-        # while they run, each range scattered as it lands
+        # non-contiguous CPU tensors: the same, one output at a time
         norms_ready = torch.cuda.Event()
         norms_ready.record(torch.cuda.current_stream(dev))
         pend_lv = _PendingD2H(lv.view(torch.uint8), lay, st, "s_levels")
@@ -240,12 +261,102 @@ def _payloads(names, datas, signs, nm, ntensors: int, codec: str, dtype: torch.d
 def _decode_stoch(items: List[Tuple[str, QuantParameter]], codec: str, bits: int) -> Dict[str, torch.Tensor]:
     """Decode (levels, signs, norm[, min]) payloads of ndim > 1 tensors in one bucketed pass."""
     st = _staging()
+    if _quant._PIPELINE:
+        th = _torchhost.get()
+        datas = [p.data for _, p in items]
+        signs = [p.signs for _, p in items]
+        ok_l, numel, lptrs = th.host_bytes(datas, 1)
+        ok_s, numel_s, sptrs = th.host_bytes(signs, 1)
+        if ok_l and ok_s and torch.equal(numel, numel_s):   # CPU payloads: range-pipelined (_decode_stoch_host)
+            decoded = _decode_stoch_host(st, items, datas, numel, lptrs.numpy().view(np.uint64),
+                                         sptrs.numpy().view(np.uint64), codec, bits)
+            return {name: t for (name, _), t in zip(items, decoded)}
     lay, out_dev = _decode_stoch_bucket(st, items, codec, bits)
     datas = [p.data for _, p in items]
     on_cpu = [not d.is_cuda for d in datas]
     # CPU payloads: the fp32 outputs (shaped like the level planes) made in one native call per range
     decoded = _hand_out(out_dev, lay, [d.shape for d in datas], on_cpu, st, "d_out", like=datas if all(on_cpu) else None)
     return {name: t for (name, _), t in zip(items, decoded)}
+
+
+_CODEC_ID = {"qsgd": 0, "rqsgd": 1, "cnat": 2}   # ADFL_CODEC_* (include/adfl_stoch.h)
+
+
+def _decode_stoch_host(st, items, datas, numel: torch.Tensor, lptrs: np.ndarray, sptrs: np.ndarray, codec: str,
+                       bits: int) -> List[torch.Tensor]:
+    """CPU level / sign planes -> owned CPU fp32 tensors, pipelined range by range as SLQ's host decode
+    (quant._decode_host_dict): both planes' byte gathers queued on the native pool at once; as range r lands,
+    one native call (adfl_stage_stoch_decode_range) enqueues its two H2Ds, the codec's dequantize of the chunks
+    it completes and their floats' D2H on the side stream behind an event; the outputs those chunks reach are
+    created (one native call) and their scatter queued on the pool behind the event. Bit-identical to the
+    one-launch decode (each chunk is decoded by the same kernel)."""
+    lay = st.layout(tuple(numel.tolist()))
+    _host_heap(lay)
+    dev = st.device
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    lib = _lib.load()
+    lv_dev = st.buf("d_levels", lay.total, torch.uint8)
+    sg_dev = st.buf("d_signs", lay.total, torch.int8)
+    lv_host = st.buf("d_levels_host", lay.total, torch.uint8, pinned=True)
+    sg_host = st.buf("d_signs_host", lay.total, torch.int8, pinned=True)
+    out_dev = st.buf("d_out", lay.total, torch.float32)
+    out_host = st.buf("d_out_host", lay.total, torch.float32, pinned=True)
+    ntens = len(items)
+    sc = torch.tensor([float(p.scale) for _, p in items] + ([float(p.scale_2) for _, p in items]
+                                                            if codec == "rqsgd" else []), dtype=torch.float32)
+    s_dev = sc.to(dev, non_blocking=True)
+    nd = s_dev.data_ptr()
+    md = nd + 4 * ntens if codec == "rqsgd" else 0
+    chunks_ptr = lay.device_chunks(dev).data_ptr()
+    d2h_h = st.d2h_stream().cuda_stream
+    cm = _chunk_meta(lay)
+    th = _torchhost.get()
+    ranges = _ranges(lay, 4)
+    evs = st.events(2 * len(ranges))
+    lh, ld, gh, gd = lv_host.data_ptr(), lv_dev.data_ptr(), sg_host.data_ptr(), sg_dev.data_ptr()
+    od, oh = out_dev.data_ptr(), out_host.data_ptr()
+    cid = _CODEC_ID[codec]
+    jobs = []
+    for lo, hi in ranges:
+        a = _range_copies(lptrs, lay, lh, 1, lo, hi, to_bucket=True)
+        b = _range_copies(sptrs, lay, gh, 1, lo, hi, to_bucket=True)
+        jobs.append(hostcopy.submit_pieces(*(np.concatenate([x, y]) for x, y in zip(a, b)),
+                                           keep=(lv_host, sg_host)))
+    offs = lay.offsets
+    outs: List[torch.Tensor] = []
+    out_ptrs = np.zeros(lay.ntensors, dtype=np.uint64)
+    scatters = []
+    c_made = t_made = 0
+    try:
+        for r, ((lo, hi), job) in enumerate(zip(ranges, jobs)):
+            job.wait()
+            c_end = int(np.searchsorted(cm.end, hi, side="right"))   # chunks whose every byte is staged
+            if c_end <= c_made:
+                check(lib.adfl_stage_stoch_decode_range(cid, bits, lh, ld, gh, gd, lo, hi, chunks_ptr, 0, 0, nd, md, od,
+                                                        oh, 0, 0, sh, d2h_h, evs[2 * r], evs[2 * r + 1]))
+                continue
+            e0, e1 = int(cm.start[c_made]), int(cm.end[c_end - 1])
+            check(lib.adfl_stage_stoch_decode_range(cid, bits, lh, ld, gh, gd, lo, hi, chunks_ptr, c_made,
+                                                    c_end - c_made, nd, md, od, oh, e0, e1, sh, d2h_h, evs[2 * r],
+                                                    evs[2 * r + 1]))
+            c_made = c_end
+            t_end = int(np.searchsorted(offs, e1, side="left"))    # tensors starting below e1
+            if t_end > t_made:
+                ts, pt = th.empty_f32_like(datas[t_made:t_end])
+                outs.extend(ts)
+                out_ptrs[t_made:t_end] = pt.numpy().view(np.uint64)
+                for j in np.nonzero(lay.sizes[t_made:t_end] * 4 >= (4 << 20))[0].tolist():
+                    hostcopy.advise_huge([ts[j]])
+                t_made = t_end
+            scatters.append(hostcopy.submit_pieces(
+                *_range_copies(out_ptrs, lay, oh, 4, e0, e1, to_bucket=False),
+                stream=True, event=evs[2 * r + 1], keep=out_host))
+    finally:
+        for j in jobs:
+            j.wait()
+        for j in scatters:
+            j.wait()
+    return outs
 
 
 @_serialized
@@ -351,17 +462,23 @@ class _StochChannel(Channel):
     def _receive(self, c_params: CompressedParameters) -> Tuple[Parameters, float]:
         assert isinstance(c_params, QuantParameters)
         s_time = time.perf_counter()
-        items = [(name, p) for name, p in c_params.params.items() if p.data.ndim > 1 and p.data.numel() > 0]
-        decoded = _decode_stoch(items, self.CODEC, self.bits) if items else {}
-        params = {}
-        for name, p in c_params.params.items():
-            if name in decoded:
-                params[name] = decoded[name]
-            elif p.data.ndim > 1:  # empty tensor: the reference's scale == 0 branch
-                params[name] = torch.zeros_like(p.data, dtype=torch.float32)
-            else:
-                params[name] = p.data.data  # passthrough
-        return params, time.perf_counter() - s_time
+        names = list(c_params.params.keys())
+        ps = list(c_params.params.values())
+        datas = [p.data for p in ps]
+        th = _torchhost.get()
+        ndim, numel, _, _ = (a.numpy() for a in th.tensor_meta(datas))   # every entry in one native call
+        coded = (ndim > 1) & (numel > 0)
+        ci = np.nonzero(coded)[0].tolist()
+        decoded = _decode_stoch([(names[i], ps[i]) for i in ci], self.CODEC, self.bits) if ci else {}
+        vals = [None] * len(names)
+        for i in ci:
+            vals[i] = decoded[names[i]]
+        for i in np.nonzero(~coded & (ndim > 1))[0].tolist():   # empty tensor: the reference's scale == 0 branch
+            vals[i] = torch.zeros_like(datas[i], dtype=torch.float32)
+        pi = np.nonzero(ndim <= 1)[0].tolist()
+        for i, t in zip(pi, th.variable_data([datas[i] for i in pi])):
+            vals[i] = t  # passthrough: q_param.data.data
+        return dict(zip(names, vals)), time.perf_counter() - s_time
 
     def receive_mean(self, all_c_params: List[CompressedParameters]) -> Tuple[Parameters, float]:
         """``simple_aggregate([self.on_server_receive(c)[0] for c in all_c_params])`` — a synchronous server
@@ -433,20 +550,25 @@ class _StochChannel(Channel):
 
     def _quantize_params(self, params: Parameters, bits: int, uniforms=None, seed=None) -> QuantParameters:
         """Biases and running metrics (ndim <= 1) are not quantized."""
-        names = [name for name, p in params.items() if p.ndim > 1 and p.numel() > 0]
-        for name in names:
-            _require_codable(name, params[name], self.__class__.__name__)
+        items = list(params.items())
+        # every entry's ndim / numel / dtype in one native call (adfl_torchhost.tensor_meta)
+        ndim, numel, is_f32, _ = (a.numpy() for a in _torchhost.get().tensor_meta([t for _, t in items]))
+        coded = (ndim > 1) & (numel > 0)
+        names = [items[i][0] for i in np.nonzero(coded)[0].tolist()]
+        f32 = [items[i][0] for i in np.nonzero(coded & is_f32)[0].tolist()]
+        for i in np.nonzero(coded & ~is_f32)[0].tolist():
+            _require_codable(items[i][0], items[i][1], self.__class__.__name__)
         if uniforms is not None and {params[n].dtype for n in names} - {uniforms.dtype}:
             raise ValueError(f"{self.__class__.__name__}: injected uniforms ({uniforms.dtype}) cover one dtype bucket; "
                              f"this dict also holds {sorted(str(d) for d in {params[n].dtype for n in names})}")
-        f32 = [n for n in names if params[n].dtype == torch.float32]
         tn = reference_norm()
         encoded = (_encode_stoch(params, f32, self.CODEC, bits, uniforms if uniforms is None or
                                  uniforms.dtype == torch.float32 else None, seed, tn) if f32 else {})
-        for dtype in sops.DT_DTYPES:   # fp16 / bf16 / fp64: one bucket per dtype, in that dtype's arithmetic
-            group = [n for n in names if params[n].dtype == dtype]
-            if group:
-                encoded.update(_encode_stoch_dt(params, group, self.CODEC, bits, uniforms, seed, tn))
+        if len(f32) < len(names):
+            for dtype in sops.DT_DTYPES:   # fp16 / bf16 / fp64: one bucket per dtype, in that dtype's arithmetic
+                group = [n for n in names if params[n].dtype == dtype]
+                if group:
+                    encoded.update(_encode_stoch_dt(params, group, self.CODEC, bits, uniforms, seed, tn))
         q_params = QuantParameters({}, 0)
         pass_signs = torch.zeros(1, dtype=torch.uint8)  # passthrough entries' unused signs, one per call
         for name, param in params.items():

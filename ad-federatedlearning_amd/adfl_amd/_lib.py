@@ -111,6 +111,8 @@ SIGNATURES = {
     "adfl_stage_events_destroy": (INT, [P, I32]),
     "adfl_stage_encode_range": (INT, [P, P, I64, I64, P, P, I64, I64, INT, P, P, P, I64, I64, P, P, P, P]),
     "adfl_stage_decode_range": (INT, [P, P, I64, I64, P, I64, I64, P, P, P, I64, I64, P, P, P, P]),
+    "adfl_stage_stoch_decode_range": (INT, [I32, INT, P, P, P, P, I64, I64, P, I64, I64, P, P, P, P, I64, I64, P, P,
+                                            P, P]),
 }
 
 NORM_L2, NORM_LINF, NORM_L2_TORCH = 0, 1, 2  # ADFL_NORM_*

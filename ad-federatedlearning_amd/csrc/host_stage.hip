@@ -2,7 +2,8 @@
 // (include/adfl_host.h, adfl_stage_encode_range / adfl_stage_decode_range), as one call.
 //
 // SLQChannel's host-to-host encode and decode (Src/ADFL/Channel/quant.py:74-112 on the CPU state dict the
-// client hands over, Src/ADFL/model.py:195-197) are pipelined over staging ranges of the pinned bucket
+// client hands over, Src/ADFL/model.py:195-197), and the QSGD / RQSGD / CNAT decode (quant.py:243-252,
+// 385-398,537-545), are pipelined over staging ranges of the pinned bucket
 // (adfl_amd/Channel/quant.py, _encode_host_dict / _decode_host_dict): as range r lands in pinned memory, its
 // H2D is enqueued, the tensors or chunks it completes are (de)quantized, and their output goes back D2H on a
 // second stream behind an event, while the host pool scatters the previous range. A trace of the C3 dict
@@ -11,8 +12,9 @@
 // they are the HIP calls alone.
 //
 // Order per range, every step asynchronous:
-//   stream:      H2D [lo, hi) of the input; if count > 0: (encode) the absmax and quantize kernels, (decode) the
-//                dequantize kernel, over chunks [chunk_begin, chunk_begin + count), record ev_compute
+//   stream:      H2D [lo, hi) of the input (both byte planes for the stochastic decode); if count > 0: (encode)
+//                the absmax and quantize kernels, (decode) the codec's dequantize kernel, over chunks
+//                [chunk_begin, chunk_begin + count), record ev_compute
 //   d2h_stream:  wait ev_compute, D2H [e0, e1) of the output, record ev_copied (the host pool's scatter of
 //                that range waits on it through adfl_event_synchronize)
 
@@ -22,6 +24,7 @@
 
 #include "adfl_host.h"
 #include "adfl_slq.h"
+#include "adfl_stoch.h"
 
 namespace {
 
@@ -105,6 +108,38 @@ int adfl_stage_decode_range(const int8_t* h_q, int8_t* d_q, int64_t lo, int64_t 
   }
   if (count == 0) return 0;
   if (int s = adfl_slq_dequantize_batched(d_q, d_chunks + chunk_begin, count, d_scales, d_out, stream)) return s;
+  return copy_back(d_out, h_out, e0, e1, 4, st, static_cast<hipStream_t>(d2h_stream),
+                   static_cast<hipEvent_t>(ev_compute), static_cast<hipEvent_t>(ev_copied));
+}
+
+int adfl_stage_stoch_decode_range(int32_t codec, int bits, const uint8_t* h_levels, uint8_t* d_levels,
+                                  const int8_t* h_signs, int8_t* d_signs, int64_t lo, int64_t hi,
+                                  const adfl_slq_chunk* d_chunks, int64_t chunk_begin, int64_t count,
+                                  const float* d_norms, const float* d_mins, float* d_out, float* h_out, int64_t e0,
+                                  int64_t e1, void* stream, void* d2h_stream, void* ev_compute, void* ev_copied) {
+  if (!h_levels || !d_levels || !h_signs || !d_signs || lo < 0 || hi < lo || count < 0) return ADFL_E_ARG;
+  if (codec != ADFL_CODEC_QSGD && codec != ADFL_CODEC_RQSGD && codec != ADFL_CODEC_CNAT) return ADFL_E_ARG;
+  if (count > 0 && (!d_chunks || !d_norms || !d_out || !h_out || chunk_begin < 0 || e0 < 0 || e1 <= e0 ||
+                    !d2h_stream || !ev_compute || !ev_copied || (codec == ADFL_CODEC_RQSGD && !d_mins)))
+    return ADFL_E_ARG;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (hi > lo) {
+    if (int s = hip_status(hipMemcpyAsync(d_levels + lo, h_levels + lo, (size_t)(hi - lo), hipMemcpyHostToDevice, st)))
+      return s;
+    if (int s = hip_status(hipMemcpyAsync(d_signs + lo, h_signs + lo, (size_t)(hi - lo), hipMemcpyHostToDevice, st)))
+      return s;
+  }
+  if (count == 0) return 0;
+  const adfl_slq_chunk* c = d_chunks + chunk_begin;
+  int s = 0;
+  if (codec == ADFL_CODEC_QSGD)
+    s = adfl_qsgd_dequantize_batched(d_levels, d_signs, c, count, bits, d_norms, d_out, stream);
+  else if (codec == ADFL_CODEC_RQSGD)
+    s = adfl_rqsgd_dequantize_batched(d_levels, d_signs, c, count, bits, d_norms, d_mins, d_out, stream);
+  else
+    s = adfl_cnat_dequantize_batched(reinterpret_cast<const int8_t*>(d_levels), d_signs, c, count, d_norms, d_out,
+                                     stream);
+  if (s) return s;
   return copy_back(d_out, h_out, e0, e1, 4, st, static_cast<hipStream_t>(d2h_stream),
                    static_cast<hipEvent_t>(ev_compute), static_cast<hipEvent_t>(ev_copied));
 }

@@ -16,6 +16,10 @@
 //   variable_data(ts)               t.data for each (what _receive hands back for a passthrough entry)
 //   tensor_meta(ts)                 per tensor: ndim, numel, whether fp32, whether a contiguous CPU tensor — what
 //                                   _quantize_params and the staging choose by, for a whole state dict at once
+//   host_bytes(ts, elem)            whether every tensor is a contiguous CPU tensor of elem-byte elements, their
+//                                   element counts and data pointers (the stochastic channels' planes and inputs)
+//   empty_like_dtype(like, code)    fresh contiguous CPU tensors shaped like `like`, uint8 / int8 / fp32 (code
+//                                   0 / 1 / 2): the stochastic encode's level and sign planes
 // Every returned pointer table is an int64 CPU tensor (the native copy pool's piece lists).
 #include <torch/extension.h>
 
@@ -116,6 +120,36 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> tensor_meta(const std
   return {ndim, numel, f32, host};
 }
 
+std::tuple<bool, at::Tensor, at::Tensor> host_bytes(const std::vector<at::Tensor>& ts, int64_t elem) {
+  const int64_t n = (int64_t)ts.size();
+  at::Tensor numel = at::empty({n}, at::kLong), ptrs = at::empty({n}, at::kLong);
+  int64_t* ne = numel.data_ptr<int64_t>();
+  int64_t* pt = ptrs.data_ptr<int64_t>();
+  bool ok = true;
+  for (int64_t k = 0; k < n; ++k) {
+    const at::Tensor& t = ts[k];
+    ok = ok && !t.is_cuda() && t.is_contiguous() && (int64_t)t.element_size() == elem;
+    ne[k] = t.numel();
+    pt[k] = (int64_t)(intptr_t)t.data_ptr();
+  }
+  return {ok, numel, ptrs};
+}
+
+std::tuple<std::vector<at::Tensor>, at::Tensor> empty_like_dtype(const std::vector<at::Tensor>& like, int64_t code) {
+  TORCH_CHECK(code >= 0 && code <= 2, "empty_like_dtype: code 0 (uint8), 1 (int8) or 2 (float32)");
+  const at::ScalarType st = code == 0 ? at::kByte : (code == 1 ? at::kChar : at::kFloat);
+  std::vector<at::Tensor> out;
+  out.reserve(like.size());
+  at::Tensor ptrs = at::empty({(int64_t)like.size()}, at::kLong);
+  int64_t* p = ptrs.data_ptr<int64_t>();
+  const auto opts = at::TensorOptions().dtype(st);
+  for (size_t k = 0; k < like.size(); ++k) {
+    out.push_back(at::empty(like[k].sizes(), opts));
+    p[k] = (int64_t)(intptr_t)out.back().data_ptr();
+  }
+  return {std::move(out), ptrs};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -126,4 +160,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("payload_kinds", &payload_kinds);
   m.def("variable_data", &variable_data);
   m.def("tensor_meta", &tensor_meta);
+  m.def("host_bytes", &host_bytes);
+  m.def("empty_like_dtype", &empty_like_dtype);
 }

@@ -95,6 +95,15 @@ int adfl_stage_decode_range(const int8_t* h_q, int8_t* d_q, int64_t lo, int64_t 
                             int64_t e0, int64_t e1, void* stream, void* d2h_stream, void* ev_compute,
                             void* ev_copied);
 
+/* Stochastic decode (codec ADFL_CODEC_QSGD / RQSGD / CNAT of adfl_stoch.h): both byte planes' range H2D; then
+ * the codec's dequantize over the chunk range (adfl_qsgd / rqsgd / cnat_dequantize_batched; d_levels holds
+ * CNAT's int8 exponents; d_mins only for RQSGD) into d_out, and floats [e0, e1) back into h_out. */
+int adfl_stage_stoch_decode_range(int32_t codec, int bits, const uint8_t* h_levels, uint8_t* d_levels,
+                                  const int8_t* h_signs, int8_t* d_signs, int64_t lo, int64_t hi,
+                                  const adfl_slq_chunk* d_chunks, int64_t chunk_begin, int64_t count,
+                                  const float* d_norms, const float* d_mins, float* d_out, float* h_out, int64_t e0,
+                                  int64_t e1, void* stream, void* d2h_stream, void* ev_compute, void* ev_copied);
+
 /* Threads the pool would use for nthreads <= 0 (for logging and tests): the CPUs in this process's affinity
  * mask, at most 8, or ADFL_HOST_THREADS when set. */
 int32_t adfl_host_threads(void);

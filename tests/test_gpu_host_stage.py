@@ -170,3 +170,72 @@ def test_channel_payload_and_scales_are_the_devices(monkeypatch):
         if p.data.is_quantized:
             assert q.data.q_scale() == p.data.q_scale()
             assert torch.equal(q.data.int_repr(), p.data.int_repr())
+
+
+@pytest.mark.parametrize("codec", ["qsgd", "rqsgd", "cnat"])
+@pytest.mark.parametrize("sizes,nranges", [([3, 8192, 8193, 5, 70000, 1, 16385], 4),
+                                           ([8192 * 7 + 3, 2, 40_000, 123_457], 32)])
+def test_stoch_decode_ranges_match_one_launch(codec, sizes, nranges):
+    """adfl_stage_stoch_decode_range: both byte planes staged range by range, each completed chunk range decoded
+    by the codec's kernel, floats back through pinned memory — equal to the one-launch decode bit for bit."""
+    from adfl_amd import stoch as sops
+    lib = _lib.load()
+    lay = _layout(sizes)
+    g = torch.Generator().manual_seed(nranges + len(codec))
+    bits = 4
+    if codec == "cnat":
+        lv = torch.randint(-20, 3, (lay.total,), generator=g, dtype=torch.int8).view(torch.uint8)
+    else:
+        lv = torch.randint(0, 16, (lay.total,), generator=g, dtype=torch.uint8)
+    sg = (torch.randint(0, 2, (lay.total,), generator=g, dtype=torch.int8) * 2 - 1)
+    norms = torch.rand(lay.ntensors, generator=g) * 3
+    norms[1] = 0.0                                   # the norm == 0 branch
+    mins = torch.rand(lay.ntensors, generator=g) * 1e-3
+    lv_h, sg_h = lv.pin_memory(), sg.pin_memory()
+    lv_d = torch.empty(lay.total, dtype=torch.uint8, device=DEV)
+    sg_d = torch.empty(lay.total, dtype=torch.int8, device=DEV)
+    out_d = torch.empty(lay.total, device=DEV)
+    out_h = torch.full((lay.total,), float("nan")).pin_memory()
+    n_d, m_d = norms.to(DEV), mins.to(DEV)
+    chunks = lay.device_chunks(DEV)
+    cm = quant._chunk_meta(lay)
+    evs = (ctypes.c_void_p * (2 * nranges))()
+    assert lib.adfl_stage_events_create(2 * nranges, evs) == 0
+    side = torch.cuda.Stream(DEV)
+    sh = torch.cuda.current_stream(DEV).cuda_stream
+    cid = {"qsgd": 0, "rqsgd": 1, "cnat": 2}[codec]
+    mp = m_d.data_ptr() if codec == "rqsgd" else None
+    c_made = 0
+    try:
+        for r, (lo, hi) in enumerate(_cuts(lay.total, nranges)):
+            c_end = int(np.searchsorted(cm.end, hi, side="right"))
+            cnt, e0, e1 = 0, 0, 0
+            if c_end > c_made:
+                cnt, e0, e1 = c_end - c_made, int(cm.start[c_made]), int(cm.end[c_end - 1])
+            rc = lib.adfl_stage_stoch_decode_range(cid, bits, lv_h.data_ptr(), lv_d.data_ptr(), sg_h.data_ptr(),
+                                                   sg_d.data_ptr(), lo, hi, chunks.data_ptr(), c_made if cnt else 0,
+                                                   cnt, n_d.data_ptr(), mp, out_d.data_ptr(), out_h.data_ptr(), e0,
+                                                   e1, sh, side.cuda_stream, evs[2 * r], evs[2 * r + 1])
+            assert rc == 0
+            c_made = max(c_made, c_end)
+        torch.cuda.synchronize()
+        lvd, sgd = lv.to(DEV), sg.to(DEV)
+        if codec == "qsgd":
+            ref = sops.qsgd_decode_batched(lvd, sgd, n_d, lay, bits)
+        elif codec == "rqsgd":
+            ref = sops.rqsgd_decode_batched(lvd, sgd, n_d, m_d, lay, bits)
+        else:
+            ref = sops.cnat_decode_batched(lvd.view(torch.int8), sgd, n_d, lay)
+        assert torch.equal(out_h.view(torch.int32), ref.cpu().view(torch.int32))
+        # RQSGD without mins, or an unknown codec: refused
+        assert lib.adfl_stage_stoch_decode_range(1, bits, lv_h.data_ptr(), lv_d.data_ptr(), sg_h.data_ptr(),
+                                                 sg_d.data_ptr(), 0, 0, chunks.data_ptr(), 0, 1, n_d.data_ptr(), None,
+                                                 out_d.data_ptr(), out_h.data_ptr(), 0, 1, sh, side.cuda_stream,
+                                                 evs[0], evs[1]) == E_ARG
+        assert lib.adfl_stage_stoch_decode_range(7, bits, lv_h.data_ptr(), lv_d.data_ptr(), sg_h.data_ptr(),
+                                                 sg_d.data_ptr(), 0, 0, chunks.data_ptr(), 0, 0, n_d.data_ptr(), None,
+                                                 out_d.data_ptr(), out_h.data_ptr(), 0, 0, sh, side.cuda_stream,
+                                                 evs[0], evs[1]) == E_ARG
+    finally:
+        torch.cuda.synchronize()
+        lib.adfl_stage_events_destroy(evs, 2 * nranges)

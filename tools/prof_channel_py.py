@@ -1,13 +1,16 @@
 import cProfile, pstats, sys, os, time, torch
 sys.path.insert(0, os.path.join(os.environ.get("GRAFT_REPO_ROOT", "/root/repo"), "ad-federatedlearning_amd"))
-from adfl_amd.Channel import SLQChannel
+import importlib
+C = importlib.import_module("adfl_amd.Channel")
+# python tools/prof_channel_py.py [SLQChannel|QSGDChannel|CNATChannel|...] (default SLQChannel)
+CH = getattr(C, sys.argv[1] if len(sys.argv) > 1 else "SLQChannel")
 base, rem = divmod(11_689_512, 256)
 g = torch.Generator().manual_seed(0)
 params = {}
 for i in range(256):
     params[f"layer{i}.weight"] = torch.randn(1, base + (1 if i < rem else 0), generator=g) * 1e-3
     params[f"layer{i}.bias"] = torch.randn(64, generator=g) * 1e-3
-ch = SLQChannel(8)
+ch = CH(8)
 for _ in range(5):
     qp, _ = ch.on_client_send(params); ch.on_server_receive(qp)
 ts=[]
