@@ -50,6 +50,7 @@ class _DeviceStaging:
         self._bufs: Dict[str, torch.Tensor] = {}
         self.layouts: "OrderedDict[Tuple[int, ...], ops.BucketLayout]" = OrderedDict()
         self._d2h: Optional[torch.cuda.Stream] = None
+        self._h2d: Optional[torch.cuda.Stream] = None
         self._events: List[int] = []
 
     def d2h_stream(self) -> torch.cuda.Stream:
@@ -58,6 +59,14 @@ class _DeviceStaging:
         if self._d2h is None:
             self._d2h = torch.cuda.Stream(self.device)
         return self._d2h
+
+    def h2d_stream(self) -> torch.cuda.Stream:
+        """The stochastic host encode's staging stream: each range's H2D runs here and the compute stream waits
+        only for the ranges its kernels read, so the copies run at the link's rate however long the calling
+        thread spends on a range's kernels and outputs."""
+        if self._h2d is None:
+            self._h2d = torch.cuda.Stream(self.device)
+        return self._h2d
 
     def events(self, n: int) -> List[int]:
         """n hipEvent_t handles (timing-free, on this device) for the range-pipelined host paths: a range's

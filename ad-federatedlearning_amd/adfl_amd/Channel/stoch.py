@@ -33,6 +33,7 @@ op rounded to the dtype; uniforms on torch.rand's grid for the dtype): one bucke
 *_dt kernels (csrc/stoch_dtype.hip). Their payloads decode like fp32 ones (the reference decodes to fp32).
 """
 
+import ctypes
 import os
 import time
 from typing import Dict, List, Tuple
@@ -95,11 +96,14 @@ def _owned_host(buf: torch.Tensor, offsets, shapes: List[torch.Size]) -> List[to
 
 @_serialized
 def _encode_stoch(params: Parameters, names: List[str], codec: str, bits: int, uniforms=None, seed=None,
-                  torch_norm: bool = True):
+                  torch_norm: bool = True, emit=None, idle=None):
     """Encode the ndim > 1 fp32 tensors `names` of `params` in one bucketed pass.
 
     Returns {name: (data, signs, scale, scale_2)} with CPU tensors for CPU inputs (device tensors for
-    device inputs). `uniforms`: optional fp32 device plane over the compact bucket (tests)."""
+    device inputs). `uniforms`: optional fp32 device plane over the compact bucket (tests). For a dict of
+    contiguous CPU tensors the outputs are built while the copies run (_encode_stoch_host): emit(k, data,
+    signs) is called for each as soon as its planes exist (the scale follows in the return value) and idle()
+    (True while it has work left) between the ranges."""
     st = _staging()
     dev = st.device
     tensors = [params[n] for n in names]
@@ -107,27 +111,18 @@ def _encode_stoch(params: Parameters, names: List[str], codec: str, bits: int, u
     th = _torchhost.get()
     host_ok, numel, hptrs = th.host_bytes(tensors, 4)
     lay = st.layout(tuple(numel.tolist()))
-    x_dev = _stage_in(tensors, lay, st, "x", torch.float32, host_ptrs=hptrs.numpy().view(np.uint64) if host_ok else None)
     if seed is None:
         seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+    if host_ok and _quant._PIPELINE:
+        return _encode_stoch_host(tensors, names, hptrs.numpy().view(np.uint64), lay, st, codec, bits, uniforms,
+                                  seed, torch_norm, emit or (lambda k, d, g: None), idle or (lambda: False))
+    x_dev = _stage_in(tensors, lay, st, "x", torch.float32, host_ptrs=hptrs.numpy().view(np.uint64) if host_ok else None)
     ws = st.buf("stoch_ws", lay.nchunks * 16, torch.uint8)
     # staging buffers are cached by name: the level plane is always uint8 (CNAT views it as int8)
-    planes = dict(levels=st.buf("s_levels", lay.total, torch.uint8), signs=st.buf("s_signs", lay.total, torch.int8))
+    levels, signs = st.buf("s_levels", lay.total, torch.uint8), st.buf("s_signs", lay.total, torch.int8)
     norms = st.buf("s_norms", lay.ntensors, torch.float32)
-    mins = None
-    if codec == "qsgd":
-        lv, sg, norms = sops.qsgd_encode_batched(x_dev, lay, bits, uniforms=uniforms, seed=seed, counter=0,
-                                                 levels=planes["levels"], signs=planes["signs"], norms=norms, ws=ws,
-                                                 torch_norm=torch_norm)
-    elif codec == "rqsgd":
-        mins = st.buf("s_mins", lay.ntensors, torch.float32)
-        lv, sg, norms, mins = sops.rqsgd_encode_batched(x_dev, lay, bits, uniforms=uniforms, seed=seed, counter=0,
-                                                        levels=planes["levels"], signs=planes["signs"],
-                                                        norms=norms, mins=mins, ws=ws)
-    else:
-        lv, sg, norms = sops.cnat_encode_batched(x_dev, lay, bits, uniforms=uniforms, seed=seed, counter=0,
-                                                 exps=planes["levels"].view(torch.int8), signs=planes["signs"],
-                                                 norms=norms, ws=ws, torch_norm=torch_norm)
+    mins = st.buf("s_mins", lay.ntensors, torch.float32) if codec == "rqsgd" else None
+    lv, sg = _codec_encode(codec, x_dev, lay, bits, uniforms, seed, levels, signs, norms, mins, ws, torch_norm)
     nm_host = st.buf("s_norms_host", 2 * lay.ntensors, torch.float32, pinned=True)
     nm_host[:lay.ntensors].copy_(norms, non_blocking=True)
     if mins is not None:
@@ -183,6 +178,134 @@ def _encode_stoch(params: Parameters, names: List[str], codec: str, bits: int, u
     datas = [(lv_parts if cpu else lv_dev)[i] for i, cpu in enumerate(on_cpu)]
     signs = [(sg_parts if cpu else sg_dev)[i] for i, cpu in enumerate(on_cpu)]
     return _payloads(names, datas, signs, nm, lay.ntensors, codec)
+
+
+def _codec_encode(codec: str, x_dev, lay, bits: int, uniforms, seed: int, levels, signs, norms, mins, ws,
+                  torch_norm: bool):
+    """The codec's encode over `lay` (a whole bucket, or a caller-placed sub-layout of some of its tensors at
+    their bucket offsets: every kernel indexes x, the planes and the uniforms by absolute element, and the
+    norms by the layout's own tensor index, so `norms` / `mins` are then views at the first tensor). Returns
+    the (levels, signs) planes in the codec's dtypes."""
+    if codec == "qsgd":
+        lv, sg, _ = sops.qsgd_encode_batched(x_dev, lay, bits, uniforms=uniforms, seed=seed, counter=0, levels=levels,
+                                             signs=signs, norms=norms, ws=ws, torch_norm=torch_norm)
+    elif codec == "rqsgd":
+        lv, sg, _, _ = sops.rqsgd_encode_batched(x_dev, lay, bits, uniforms=uniforms, seed=seed, counter=0,
+                                                 levels=levels, signs=signs, norms=norms, mins=mins, ws=ws)
+    else:
+        lv, sg, _ = sops.cnat_encode_batched(x_dev, lay, bits, uniforms=uniforms, seed=seed, counter=0,
+                                             exps=levels.view(torch.int8), signs=signs, norms=norms, ws=ws,
+                                             torch_norm=torch_norm)
+    return lv, sg
+
+
+def _sub_layout(lay, t0: int, t1: int):
+    """Tensors [t0, t1) of `lay` at their bucket offsets, as a layout of their own (cached on `lay`: the staging
+    ranges of a layout complete the same tensor runs every call)."""
+    cache = lay.__dict__.setdefault("_sub_layouts", {})
+    sub = cache.get((t0, t1))
+    if sub is None:
+        sub = cache[(t0, t1)] = ops.BucketLayout(lay.sizes[t0:t1].tolist(), offsets=lay.offsets[t0:t1].tolist())
+    return sub
+
+
+def _encode_stoch_host(tensors, names, hptrs: np.ndarray, lay, st, codec: str, bits: int, uniforms, seed: int,
+                       torch_norm: bool, emit, idle):
+    """A CPU fp32 dict's QSGD / RQSGD / CNAT encode, pipelined range by range as SLQ's host encode is: the
+    gathers into the pinned bucket queued on the native pool at once; as range r lands its H2D is enqueued
+    (adfl_stage_encode_range with no kernel), and the tensors whose every byte is now staged are encoded at
+    once by the codec's kernels over a sub-layout of just those tensors (_codec_encode: the same bytes as the
+    whole-bucket encode, norms included), their level and sign bytes go back D2H on the side stream behind an
+    event (adfl_stage_d2h), their outputs are created (one native call per plane) and the scatter of both
+    planes queued on the pool behind the event — so the planes' D2H overlaps the next ranges' H2D. The H2D
+    runs on a stream of its own, enqueued as soon as each gather lands, so a range's kernels and outputs
+    (longer on the calling thread than a range's copy) never hold the link back."""
+    _host_heap(lay)
+    dev = st.device
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+    lib = _lib.load()
+    th = _torchhost.get()
+    x_dev = st.buf("x", lay.total, torch.float32)
+    host = st.buf("x_host", lay.total, torch.float32, pinned=True)
+    ws = st.buf("stoch_ws", lay.nchunks * 16, torch.uint8)
+    levels, signs = st.buf("s_levels", lay.total, torch.uint8), st.buf("s_signs", lay.total, torch.int8)
+    lv_host = st.buf("s_levels_host", lay.total, torch.uint8, pinned=True)
+    sg_host = st.buf("s_signs_host", lay.total, torch.int8, pinned=True)
+    norms = st.buf("s_norms", lay.ntensors, torch.float32)
+    mins = st.buf("s_mins", lay.ntensors, torch.float32) if codec == "rqsgd" else None
+    nm_host = st.buf("s_norms_host", 2 * lay.ntensors, torch.float32, pinned=True)
+    ranges = _ranges(lay, 4)
+    evs = st.events(2 * len(ranges))
+    d2h_h = st.d2h_stream().cuda_stream
+    hx, dx = host.data_ptr(), x_dev.data_ptr()
+    ld, lh, gd, gh = levels.data_ptr(), lv_host.data_ptr(), signs.data_ptr(), sg_host.data_ptr()
+    jobs = [hostcopy.submit_pieces(*_range_copies(hptrs, lay, hx, 4, lo, hi, to_bucket=True), keep=host)
+            for lo, hi in ranges]
+    ends = lay.offsets + lay.sizes
+    code = 1 if codec == "cnat" else 0
+    lv_parts: List[torch.Tensor] = []
+    sg_parts: List[torch.Tensor] = []
+    lv_ptrs = np.zeros(lay.ntensors, dtype=np.uint64)
+    sg_ptrs = np.zeros(lay.ntensors, dtype=np.uint64)
+    copies = (ctypes.c_void_p * 2)(), (ctypes.c_void_p * 2)(), (ctypes.c_int64 * 2)()
+    scatters = []
+    h2d = st.h2d_stream()
+    h2d_h = h2d.cuda_stream
+    h2d.wait_stream(stream)   # the staging buffers' last readers
+    landed = [torch.cuda.Event() for _ in ranges]
+    made = 0
+    r_h2d = 0
+    try:
+        for r, (lo, hi) in enumerate(ranges):
+            # every range whose gather has landed goes to the link at once, on its own stream (the compute
+            # stream waits only for the ranges its kernels read); block on a gather only when range r's is next
+            while r_h2d < len(ranges) and (r_h2d == r or jobs[r_h2d].done()):
+                jobs[r_h2d].wait()
+                a, b = ranges[r_h2d]
+                check(lib.adfl_stage_encode_range(hx, dx, a, b, None, None, 0, 0, 0, None, None, None, 0, 0, h2d_h,
+                                                  None, None, None))
+                landed[r_h2d].record(h2d)
+                r_h2d += 1
+            done = int(np.searchsorted(ends, hi, side="right"))   # tensors whose every byte is staged
+            if done <= made:
+                continue
+            stream.wait_event(landed[r])
+            _codec_encode(codec, x_dev, _sub_layout(lay, made, done), bits, uniforms, seed, levels, signs,
+                          norms[made:], mins[made:] if mins is not None else None, ws, torch_norm)
+            e0, e1 = int(lay.offsets[made]), int(ends[done - 1])
+            src, dst, nb = copies
+            src[0], src[1], dst[0], dst[1] = ld + e0, gd + e0, lh + e0, gh + e0
+            nb[0] = nb[1] = e1 - e0
+            check(lib.adfl_stage_d2h(src, dst, nb, 2, sh, d2h_h, evs[2 * r], evs[2 * r + 1]))
+            lts, lpt = th.empty_like_dtype(tensors[made:done], code)
+            gts, gpt = th.empty_like_dtype(tensors[made:done], 1)
+            lv_parts.extend(lts)
+            sg_parts.extend(gts)
+            lv_ptrs[made:done] = lpt.numpy().view(np.uint64)
+            sg_ptrs[made:done] = gpt.numpy().view(np.uint64)
+            a = _range_copies(lv_ptrs, lay, lh, 1, e0, e1, to_bucket=False)
+            b = _range_copies(sg_ptrs, lay, gh, 1, e0, e1, to_bucket=False)
+            scatters.append(hostcopy.submit_pieces(*(np.concatenate([u, v]) for u, v in zip(a, b)), stream=True,
+                                                   event=evs[2 * r + 1], keep=(lv_host, sg_host)))
+            for k in range(made, done):   # the caller's payload objects, their scales filled in at the end
+                emit(k, lv_parts[k], sg_parts[k])
+            made = done
+            idle()
+        nm_host[:lay.ntensors].copy_(norms, non_blocking=True)
+        if mins is not None:
+            nm_host[lay.ntensors:].copy_(mins, non_blocking=True)
+        norms_ready = torch.cuda.Event()
+        norms_ready.record(stream)
+        while idle():   # the caller's remaining objects, while the last copies land
+            pass
+    finally:
+        for j in jobs:
+            j.wait()
+        for j in scatters:
+            j.wait()
+    norms_ready.synchronize()
+    return _payloads(names, lv_parts, sg_parts, nm_host.tolist(), lay.ntensors, codec)
 
 
 # Philox block-counter base of each dtype bucket: one seed serves an fp32 bucket and every fp16 / bf16 / fp64
@@ -562,28 +685,60 @@ class _StochChannel(Channel):
             raise ValueError(f"{self.__class__.__name__}: injected uniforms ({uniforms.dtype}) cover one dtype bucket; "
                              f"this dict also holds {sorted(str(d) for d in {params[n].dtype for n in names})}")
         tn = reference_norm()
+        qp = QuantParameter
+        made: Dict[str, QuantParameter] = {}
+        size = [0]
+        f32_numel = numel[coded & is_f32].tolist()
+
+        def emit(k, data, signs):   # an encoded fp32 entry, built as soon as its planes exist; scale set below
+            n = f32[k]
+            p = params[n]
+            made[n] = qp(data, bits, 0, signs, p.shape, p.dtype, data.dtype, 0)
+            size[0] += f32_numel[k]   # one byte per element
+
+        pass_signs = torch.zeros(1, dtype=torch.uint8)  # passthrough entries' unused signs, one per call
+        rest = iter([items[i] for i in np.nonzero(ndim <= 1)[0].tolist()])
+
+        def idle(batch=32):   # passthrough entries, a batch per staging range
+            for _ in range(batch):
+                e = next(rest, None)
+                if e is None:
+                    return False
+                t = e[1]
+                made[e[0]] = qp(t, bits, 0, pass_signs, t.shape, t.dtype, t.dtype, 0)
+                size[0] += t.nbytes
+            return True
+
         encoded = (_encode_stoch(params, f32, self.CODEC, bits, uniforms if uniforms is None or
-                                 uniforms.dtype == torch.float32 else None, seed, tn) if f32 else {})
+                                 uniforms.dtype == torch.float32 else None, seed, tn, emit=emit, idle=idle)
+                   if f32 else {})
         if len(f32) < len(names):
             for dtype in sops.DT_DTYPES:   # fp16 / bf16 / fp64: one bucket per dtype, in that dtype's arithmetic
                 group = [n for n in names if params[n].dtype == dtype]
                 if group:
                     encoded.update(_encode_stoch_dt(params, group, self.CODEC, bits, uniforms, seed, tn))
-        q_params = QuantParameters({}, 0)
-        pass_signs = torch.zeros(1, dtype=torch.uint8)  # passthrough entries' unused signs, one per call
-        for name, param in params.items():
-            if name in encoded:
-                data, signs, scale, scale_2 = encoded[name]
-            elif param.ndim > 1:  # empty: vector_norm is 0 -> zero branch
-                _require_codable(name, param, self.__class__.__name__)
-                data = torch.zeros_like(param, dtype=torch.uint8)
-                signs, scale, scale_2 = torch.ones_like(param, dtype=torch.int8), torch.tensor(0.0, dtype=param.dtype), 0
-            else:
-                data, signs, scale, scale_2 = param, pass_signs, 0, 0
-            q_params.params[name] = QuantParameter(data=data, bits=bits, scale=scale, signs=signs, shape=param.shape,
-                                                   dtype=param.dtype, q_dtype=data.dtype, scale_2=scale_2)
-            q_params.size += data.nbytes
-        return q_params
+        for name, param in items:
+            o = made.get(name)
+            e = encoded.get(name)
+            if e is not None:
+                data, signs, scale, scale_2 = e
+                if o is None:
+                    made[name] = qp(data, bits, scale, signs, param.shape, param.dtype, data.dtype, scale_2)
+                    size[0] += data.nbytes
+                else:   # built while the copies ran: its scale now (and the zero-norm branch's uint8 view)
+                    if data is not o.data:
+                        o.data, o.q_dtype = data, data.dtype
+                    o.scale, o.scale_2 = scale, scale_2
+            elif o is None:
+                if param.ndim > 1:  # empty: vector_norm is 0 -> zero branch
+                    _require_codable(name, param, self.__class__.__name__)
+                    data = torch.zeros_like(param, dtype=torch.uint8)
+                    made[name] = qp(data, bits, torch.tensor(0.0, dtype=param.dtype),
+                                    torch.ones_like(param, dtype=torch.int8), param.shape, param.dtype, data.dtype, 0)
+                else:
+                    made[name] = qp(param, bits, 0, pass_signs, param.shape, param.dtype, param.dtype, 0)
+                size[0] += made[name].data.nbytes
+        return QuantParameters({name: made[name] for name in params}, size[0])
 
 
 class QSGDChannel(_StochChannel):

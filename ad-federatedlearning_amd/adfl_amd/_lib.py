@@ -109,6 +109,7 @@ SIGNATURES = {
     "adfl_event_synchronize": (INT, [P]),
     "adfl_stage_events_create": (INT, [I32, P]),
     "adfl_stage_events_destroy": (INT, [P, I32]),
+    "adfl_stage_d2h": (INT, [P, P, P, I32, P, P, P, P]),
     "adfl_stage_encode_range": (INT, [P, P, I64, I64, P, P, I64, I64, INT, P, P, P, I64, I64, P, P, P, P]),
     "adfl_stage_decode_range": (INT, [P, P, I64, I64, P, I64, I64, P, P, P, I64, I64, P, P, P, P]),
     "adfl_stage_stoch_decode_range": (INT, [I32, INT, P, P, P, P, I64, I64, P, I64, I64, P, P, P, P, I64, I64, P, P,

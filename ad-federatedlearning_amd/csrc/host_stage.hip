@@ -69,6 +69,21 @@ int adfl_stage_events_destroy(void* const* events, int32_t n) {
   return first;
 }
 
+int adfl_stage_d2h(const void* const* d_srcs, void* const* h_dsts, const int64_t* nbytes, int32_t n, void* stream,
+                   void* d2h_stream, void* ev_compute, void* ev_copied) {
+  if (n < 1 || !d_srcs || !h_dsts || !nbytes || !d2h_stream || !ev_compute || !ev_copied) return ADFL_E_ARG;
+  for (int32_t i = 0; i < n; ++i)
+    if (!d_srcs[i] || !h_dsts[i] || nbytes[i] < 0) return ADFL_E_ARG;
+  hipStream_t st = static_cast<hipStream_t>(stream), d2h = static_cast<hipStream_t>(d2h_stream);
+  if (int s = hip_status(hipEventRecord(static_cast<hipEvent_t>(ev_compute), st))) return s;
+  if (int s = hip_status(hipStreamWaitEvent(d2h, static_cast<hipEvent_t>(ev_compute), 0))) return s;
+  for (int32_t i = 0; i < n; ++i)
+    if (nbytes[i] > 0)
+      if (int s = hip_status(hipMemcpyAsync(h_dsts[i], d_srcs[i], (size_t)nbytes[i], hipMemcpyDeviceToHost, d2h)))
+        return s;
+  return hip_status(hipEventRecord(static_cast<hipEvent_t>(ev_copied), d2h));
+}
+
 int adfl_stage_encode_range(const float* h_x, float* d_x, int64_t lo, int64_t hi, uint32_t* d_partials,
                             const adfl_slq_chunk* d_chunks, int64_t chunk_begin, int64_t count, int bits, int8_t* d_q,
                             float* d_scales, int8_t* h_q, int64_t e0, int64_t e1, void* stream, void* d2h_stream,

@@ -80,6 +80,13 @@ int adfl_event_synchronize(void* event);
 int adfl_stage_events_create(int32_t n, void** events);
 int adfl_stage_events_destroy(void* const* events, int32_t n);
 
+/* The copy-back half alone: record ev_compute on stream, make d2h_stream wait for it, then n D2H copies
+ * (d_srcs[i] -> h_dsts[i], nbytes[i] bytes, h_dsts pinned) on d2h_stream, then record ev_copied there. The
+ * stochastic encode runs its codec's kernels for the tensors a range completes, then hands both planes'
+ * bytes of those tensors back through this. */
+int adfl_stage_d2h(const void* const* d_srcs, void* const* h_dsts, const int64_t* nbytes, int32_t n, void* stream,
+                   void* d2h_stream, void* ev_compute, void* ev_copied);
+
 /* Encode: x range H2D; then, over the chunk range (whole tensors, every byte of them staged),
  * adfl_slq_absmax_batched_range into d_partials (one uint32 per chunk of the table) and
  * adfl_slq_quantize_batched_range into d_q / d_scales, and payload bytes [e0, e1) back into h_q. */

@@ -239,3 +239,30 @@ def test_stoch_decode_ranges_match_one_launch(codec, sizes, nranges):
     finally:
         torch.cuda.synchronize()
         lib.adfl_stage_events_destroy(evs, 2 * nranges)
+
+
+@pytest.mark.parametrize("cls", ["QSGDChannel", "RQSGDChannel", "CNATChannel"])
+def test_stoch_host_encode_ranges_match_whole_bucket(cls, monkeypatch):
+    """The range-pipelined stochastic host encode (each range's completed tensors encoded over a sub-layout at
+    their bucket offsets) gives the whole-bucket encode's bytes: same seed, same levels / exponents, signs,
+    norms and minima, with staging ranges cutting through tensors, a zero tensor and single elements."""
+    import importlib
+    C = importlib.import_module("adfl_amd.Channel")
+    ch = getattr(C, cls)(8)
+    g = torch.Generator().manual_seed(5)
+    sizes = [3 * 8192 + 5, 17, 100_000, 9, 70_001, 1, 250_000] + [4096] * 20
+    params = {f"w{i}": torch.randn(1, n, generator=g) * 1e-2 for i, n in enumerate(sizes)}
+    params["w3"].zero_()
+    params["b"] = torch.randn(10, generator=g)
+    monkeypatch.setattr(quant, "_PIECE_BYTES", 1 << 16)   # many ranges
+    got = ch._quantize_params(params, 8, seed=1234)
+    monkeypatch.setattr(quant, "_PIPELINE", False)
+    want = ch._quantize_params(params, 8, seed=1234)
+    for n in params:
+        a, b = got.params[n], want.params[n]
+        assert float(a.scale) == float(b.scale) and float(a.scale_2) == float(b.scale_2), n
+        if params[n].ndim > 1:
+            assert a.data.dtype == b.data.dtype and a.data.shape == b.data.shape
+            assert torch.equal(a.data.view(torch.uint8), b.data.view(torch.uint8)), n
+            assert torch.equal(a.signs, b.signs), n
+    assert got.size == want.size

@@ -1,5 +1,5 @@
 """The bench line's host-to-host C3 dict leg (SLQChannel(8) on 256 weights + 256 biases, CPU in / CPU out) for a
-trace: warm-up calls, then `--calls` encode + decode pairs with a hipDeviceSynchronize-free marker between them
+trace (`--channel QSGDChannel` etc. for the other codecs): warm-up calls, then `--calls` encode + decode pairs with a hipDeviceSynchronize-free marker between them
 (a 1-element H2D copy of a recognisable size), so the copies, kernels and HIP API calls of one call can be cut
 out of a rocprofv3 trace:
 
@@ -16,7 +16,8 @@ import torch
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "ad-federatedlearning_amd"))
-from adfl_amd.Channel import SLQChannel  # noqa: E402
+import importlib  # noqa: E402
+C = importlib.import_module("adfl_amd.Channel")
 
 MARK_BYTES = 12345 * 4   # the marker copy's size (fp32 elements * 4)
 
@@ -24,6 +25,7 @@ MARK_BYTES = 12345 * 4   # the marker copy's size (fp32 elements * 4)
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--calls", type=int, default=6)
+    p.add_argument("--channel", default="SLQChannel", help="SLQChannel, QSGDChannel, CNATChannel, ...")
     args = p.parse_args()
     base, rem = divmod(11_689_512, 256)
     g = torch.Generator().manual_seed(0)
@@ -31,7 +33,7 @@ def main():
     for i in range(256):
         params[f"layer{i}.weight"] = torch.randn(1, base + (1 if i < rem else 0), generator=g) * 1e-3
         params[f"layer{i}.bias"] = torch.randn(64, generator=g) * 1e-3
-    ch = SLQChannel(8)
+    ch = getattr(C, args.channel)(8)
     for _ in range(5):
         qp, _ = ch.on_client_send(params)
         ch.on_server_receive(qp)
