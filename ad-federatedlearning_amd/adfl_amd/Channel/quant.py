@@ -866,6 +866,29 @@ def _decode_mean(clients: List[List[torch.Tensor]], scales: List[List[float]], s
     return _hand_out(out_dev, lay, [torch.Size(s) for s in shapes], on_cpu, st, "m_out")
 
 
+@_serialized
+def _decode_mean_host(st: _DeviceStaging, like: List[torch.Tensor], numel: torch.Tensor, ptrs: List[np.ndarray],
+                      scales: torch.Tensor) -> List[torch.Tensor]:
+    """_decode_mean for K CPU qint8 payload lists already checked (SLQChannel._mean_host_updates): each client's
+    bytes gathered straight from the storages into its pinned row (one native gather per client, that row's
+    H2D enqueued as soon as it is staged), one decode-mean launch, and the fp32 means handed back as owned CPU
+    tensors shaped like `like`, created by one native call per staging range while the D2H runs."""
+    dev = st.device
+    lay = st.layout(tuple(numel.tolist()), align=1)
+    _host_heap(lay)
+    k = len(ptrs)
+    row = (lay.total + 15) // 16 * 16
+    rows = st.buf("mq", k * row, torch.uint8).view(k, row)
+    host = st.buf("mq_host", k * row, torch.uint8, pinned=True).view(k, row)
+    for r in range(k):
+        hostcopy.copy_pieces(*_range_copies(ptrs[r], lay, host[r].data_ptr(), 1, 0, lay.total, to_bucket=True))
+        rows[r].copy_(host[r], non_blocking=True)
+    s_dev = scales.to(dev, non_blocking=True)
+    out_dev = ops.dequantize_mean_batched(rows.view(torch.int8), s_dev, lay,
+                                          out=st.buf("m_out", lay.total, torch.float32))
+    return _hand_out(out_dev, lay, [None] * len(like), [True] * len(like), st, "m_out", like=like)
+
+
 def _simple_aggregate(values: List[torch.Tensor]) -> torch.Tensor:
     """One entry of simple_aggregate (Src/ADFL/model.py:221-234), as the reference computes it."""
     with torch.no_grad():
@@ -900,8 +923,33 @@ def _aggregate_entries(names: List[str], parts: List[Parameters]) -> Dict[str, t
     K >= 8 (torch's inner-sum kernel) and everything else go through simple_aggregate per entry."""
     k = len(parts)
     res: Dict[str, torch.Tensor] = {}
-    groups: Dict[torch.dtype, List[str]] = {}
     f32_ok = sum_order.self_check()
+    lists = [[p[n] for n in names] for p in parts]
+    if names and all(isinstance(v, torch.Tensor) for row in lists for v in row):
+        # the classification, the K rows and the owned results in native calls (adfl_torchhost)
+        th = _torchhost.get()
+        uni, code, numel = (a.numpy() for a in th.entry_meta_k(lists))
+        f32 = uni & (code == 0) & f32_ok & (numel > 0) & ~((numel == 1) & (k >= 8))
+        with torch.no_grad():
+            for sel, is_f32 in ((f32, True), (uni & (code == 1), False)):
+                idx = np.nonzero(sel)[0]
+                if idx.size < 2:
+                    continue
+                rows = th.concat_rows(lists, torch.from_numpy(idx))
+                if is_f32:
+                    acc = sum_order.sum_rows(rows, numel[idx].tolist())
+                else:   # int64: K elementwise adds from zero (exact in any order)
+                    acc = torch.zeros_like(rows[0])
+                    for r in rows.unbind(0):
+                        acc = acc + r
+                agg = acc / k
+                for i, t in zip(idx.tolist(), th.split_owned(agg, [lists[0][i] for i in idx.tolist()])):
+                    res[names[i]] = t
+        for n in names:
+            if n not in res:
+                res[n] = _simple_aggregate([p[n] for p in parts])
+        return res
+    groups: Dict[torch.dtype, List[str]] = {}
     for n in names:
         vals = [p[n] for p in parts]
         t0 = vals[0]
@@ -1093,17 +1141,25 @@ class SLQChannel(Channel):
             assert isinstance(c, QuantParameters)
         s_time = time.perf_counter()
         names = list(all_c_params[0].params.keys())
-        fused = [n for n in names if all(n in c.params and self._fusable(c.params[n]) for c in all_c_params)
-                 and len({tuple(c.params[n].shape) for c in all_c_params}) == 1] if device_mean_order_ok() else []
+        order_ok = device_mean_order_ok()
         out: Parameters = {}
-        if fused:
-            decoded = self._mean_payloads(all_c_params, fused)
+        fast = self._mean_host_updates(all_c_params, names) if order_ok else None
+        plain = None
+        if fast is not None:   # every update a CPU dict of the same entries: classified in native calls
+            fused, decoded, plain = fast
             out.update(zip(fused, decoded))
+        else:
+            fused = [n for n in names if all(n in c.params and self._fusable(c.params[n]) for c in all_c_params)
+                     and len({tuple(c.params[n].shape) for c in all_c_params}) == 1] if order_ok else []
+            if fused:
+                decoded = self._mean_payloads(all_c_params, fused)
+                out.update(zip(fused, decoded))
         rest = [n for n in names if n not in out]
         if rest:
             # passthrough entries decode to their own payload tensor (quant.py:111-112): used as they are
             # (the values _receive hands back, without its per-entry work); the rest through _receive
-            plain = [n for n in rest if all(self._passthrough(c.params[n]) for c in all_c_params)]
+            if plain is None:
+                plain = [n for n in rest if all(self._passthrough(c.params[n]) for c in all_c_params)]
             other = [n for n in rest if n not in set(plain)]
             parts = []
             for c in all_c_params:
@@ -1113,6 +1169,37 @@ class SLQChannel(Channel):
                 parts.append(part)
             out.update(_aggregate_entries(rest, parts))
         return {n: out[n] for n in names}, time.perf_counter() - s_time
+
+    @staticmethod
+    def _mean_host_updates(all_c_params: List[QuantParameters], names: List[str]):
+        """receive_mean's common case in a few native calls: K updates of one model whose entries come in the
+        same order, every ndim > 1 payload a non-empty per-tensor qint8 CPU tensor with zero point 0 of the same
+        shape in every update. Returns (fused names, their means) — the means from one decode-mean launch
+        over rows staged straight from the payloads' storages, the outputs created by one native call per
+        staging range — or None when the updates are anything else (receive_mean then classifies entry by
+        entry)."""
+        if any(list(c.params.keys()) != names for c in all_c_params):
+            return None
+        th = _torchhost.get()
+        datas = [[p.data for p in c.params.values()] for c in all_c_params]
+        kinds = np.stack([th.payload_kinds(d).numpy() for d in datas])
+        if (kinds == 2).any() or (kinds != kinds[0]).any():
+            return None
+        idx = np.nonzero(kinds[0] == 1)[0].tolist()
+        plain = [names[i] for i in np.nonzero(kinds[0] == 0)[0].tolist()]   # ndim <= 1 in every update
+        if not idx:
+            return [], [], plain
+        qs = [[d[i] for i in idx] for d in datas]
+        metas = [th.qint8_meta(q) for q in qs]   # (ok, all contiguous CPU, numel, fp32 scales, data pointers)
+        numel = metas[0][2]
+        if not all(m[0] and m[1] and torch.equal(m[2], numel) for m in metas) or int(numel.min()) == 0:
+            return None
+        if not th.shapes_equal(qs):
+            return None
+        fused = [names[i] for i in idx]
+        st = _staging()
+        return fused, _decode_mean_host(st, qs[0], numel, [m[4].numpy().view(np.uint64) for m in metas],
+                                        torch.stack([m[3] for m in metas])), plain
 
     @staticmethod
     def _passthrough(p: QuantParameter) -> bool:
@@ -1242,6 +1329,12 @@ class PackedSLQChannel(SLQChannel):
 
     def _passthrough(self, p: QuantParameter) -> bool:
         return isinstance(p.data, torch.Tensor) and p.data.ndim <= 1 and not self._is_packed(p)
+
+    @staticmethod
+    def _mean_host_updates(all_c_params: List[QuantParameters], names: List[str]):
+        """Packed payloads are 1-D byte buffers whose shape lives in the payload object: the native
+        classification of SLQChannel's qint8 updates does not apply (receive_mean classifies entry by entry)."""
+        return None
 
     def _mean_payloads(self, all_c_params: List[QuantParameters], names: List[str]) -> List[torch.Tensor]:
         return _decode_mean([[c.params[n].data for n in names] for c in all_c_params],

@@ -540,6 +540,35 @@ def _decode_mean_stoch(all_c_params: List[QuantParameters], names: List[str], co
     return _hand_out(out_dev, lay, [first[n].data.shape for n in names], on_cpu, st, "sm_out")
 
 
+@_serialized
+def _decode_mean_stoch_host(like: List[torch.Tensor], numel: torch.Tensor, lv_ptrs: List[np.ndarray],
+                            sg_ptrs: List[np.ndarray], norms: torch.Tensor, mins, codec: str,
+                            bits: int) -> List[torch.Tensor]:
+    """_decode_mean_stoch for K CPU updates already checked (_StochChannel._mean_host_updates): both planes of
+    every client gathered straight from the storages into pinned rows (one native gather per client and
+    plane, each row's H2D enqueued as soon as it is staged), one decode-mean launch, the fp32 means handed
+    back as owned CPU tensors shaped like `like`, created by one native call per staging range."""
+    st = _staging()
+    dev = st.device
+    lay = st.layout(tuple(numel.tolist()))
+    _host_heap(lay)
+    k = len(lv_ptrs)
+    row = (lay.total + 15) // 16 * 16
+    rows = {}
+    for key, ptrs, dt in (("sm_levels", lv_ptrs, torch.uint8), ("sm_signs", sg_ptrs, torch.int8)):
+        d = st.buf(key, k * row, torch.uint8).view(k, row)
+        h = st.buf(key + "_host", k * row, torch.uint8, pinned=True).view(k, row)
+        for r in range(k):
+            hostcopy.copy_pieces(*_range_copies(ptrs[r], lay, h[r].data_ptr(), 1, 0, lay.total, to_bucket=True))
+            d[r].copy_(h[r], non_blocking=True)
+        rows[key] = d if dt == torch.uint8 else d.view(torch.int8)
+    nd = norms.to(dev, non_blocking=True)
+    md = mins.to(dev, non_blocking=True) if mins is not None else None
+    out_dev = sops.dequantize_mean_batched(codec, rows["sm_levels"], rows["sm_signs"], nd, lay, bits, mins=md,
+                                           out=st.buf("sm_out", lay.total, torch.float32))
+    return _hand_out(out_dev, lay, [None] * len(like), [True] * len(like), st, "sm_out", like=like)
+
+
 class _StochChannel(Channel):
     """Shared body of the three bi-directional stochastic channels."""
 
@@ -620,11 +649,17 @@ class _StochChannel(Channel):
             assert isinstance(c, QuantParameters)
         s_time = time.perf_counter()
         names = list(all_c_params[0].params.keys())
-        fused = [n for n in names if all(n in c.params and self._fusable(c.params[n]) for c in all_c_params)
-                 and len({tuple(c.params[n].data.shape) for c in all_c_params}) == 1] if device_mean_order_ok() else []
+        order_ok = device_mean_order_ok()
         out: Parameters = {}
-        if fused:
-            out.update(zip(fused, _decode_mean_stoch(all_c_params, fused, self.CODEC, self.bits)))
+        fast = self._mean_host_updates(all_c_params, names) if order_ok else None
+        if fast is not None:   # every update a CPU dict of the same entries: classified in native calls
+            fused, decoded = fast
+            out.update(zip(fused, decoded))
+        else:
+            fused = [n for n in names if all(n in c.params and self._fusable(c.params[n]) for c in all_c_params)
+                     and len({tuple(c.params[n].data.shape) for c in all_c_params}) == 1] if order_ok else []
+            if fused:
+                out.update(zip(fused, _decode_mean_stoch(all_c_params, fused, self.CODEC, self.bits)))
         rest = [n for n in names if n not in out]
         if rest:
             parts = [self._receive(QuantParameters({n: c.params[n] for n in rest}, 0))[0] for c in all_c_params]
@@ -661,6 +696,40 @@ class _StochChannel(Channel):
                     for n, d in decoded.items():
                         t[n].mul_(1).add_(d.to(t[n].device), alpha=1)
         return time.perf_counter() - s_time
+
+    def _mean_host_updates(self, all_c_params: List[QuantParameters], names: List[str]):
+        """receive_mean's common case in a few native calls: K updates of one model whose entries come in the
+        same order and whose every non-empty ndim > 1 entry is a pair of contiguous CPU byte planes of one
+        element count and, across updates, one shape. Returns (those names, their means), or None when the
+        updates are anything else (receive_mean then classifies entry by entry)."""
+        if any(list(c.params.keys()) != names for c in all_c_params):
+            return None
+        th = _torchhost.get()
+        ps = [list(c.params.values()) for c in all_c_params]
+        datas = [[p.data for p in c] for c in ps]
+        metas = [th.tensor_meta(d) for d in datas]
+        ndim, numel = metas[0][0].numpy(), metas[0][1].numpy()
+        if any(not (torch.equal(m[0], metas[0][0]) and torch.equal(m[1], metas[0][1])) for m in metas):
+            return None
+        idx = np.nonzero((ndim > 1) & (numel > 0))[0].tolist()
+        if not idx:
+            return [], []
+        lv = [[d[i] for i in idx] for d in datas]
+        sg = [[c[i].signs for i in idx] for c in ps]
+        lvm = [th.byte_planes(x) for x in lv]
+        sgm = [th.byte_planes(x) for x in sg]
+        n0 = lvm[0][1]
+        if not all(a[0] and b[0] and torch.equal(a[1], n0) and torch.equal(b[1], n0) for a, b in zip(lvm, sgm)):
+            return None
+        if not th.shapes_equal(lv):
+            return None
+        norms = torch.tensor([[float(c[i].scale) for i in idx] for c in ps], dtype=torch.float32)
+        mins = (torch.tensor([[float(c[i].scale_2) for i in idx] for c in ps], dtype=torch.float32)
+                if self.CODEC == "rqsgd" else None)
+        means = _decode_mean_stoch_host(lv[0], n0, [m[2].numpy().view(np.uint64) for m in lvm],
+                                        [m[2].numpy().view(np.uint64) for m in sgm], norms, mins, self.CODEC,
+                                        self.bits)
+        return [names[i] for i in idx], means
 
     @staticmethod
     def _fusable(p: QuantParameter) -> bool:

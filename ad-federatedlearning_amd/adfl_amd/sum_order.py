@@ -20,6 +20,7 @@ the reference's even on a torch build whose order differs."""
 
 from typing import List, Optional
 
+import numpy as np
 import torch
 
 _CHECKED: Optional[bool] = None
@@ -71,18 +72,16 @@ def sum_rows(stacked: torch.Tensor, sizes: List[int]) -> torch.Tensor:
     (torch's inner-sum kernel handles them otherwise; the caller routes those per entry)."""
     rows = list(stacked.unbind(0))
     seq = _cascade(rows)
-    mask = torch.zeros(stacked.shape[1], dtype=torch.bool)
-    off = 0
-    any_tail = False
-    for n in sizes:
-        e = seq_end(n)
-        if e < n:
-            mask[off + e:off + n] = True
-            any_tail = True
-        off += n
-    if not any_tail:
+    n = np.asarray(sizes, dtype=np.int64)
+    e = np.where(n == 1, 0, np.where(n >= 8, n & ~31, n & ~3))   # seq_end of every entry
+    off = np.concatenate([[0], np.cumsum(n)[:-1]])
+    tail = e < n
+    if not tail.any():
         return seq
-    idx = mask.nonzero().squeeze(1)
+    edge = np.zeros(int(n.sum()) + 1, dtype=np.int64)   # +1 where an entry's tail starts, -1 where it ends
+    np.add.at(edge, (off + e)[tail], 1)
+    np.add.at(edge, (off + n)[tail], -1)
+    idx = torch.from_numpy(np.nonzero(np.cumsum(edge[:-1]) > 0)[0])
     tail = _ilp4([r.index_select(0, idx) for r in rows])
     seq[idx] = tail
     return seq

@@ -20,11 +20,21 @@
 //                                   element counts and data pointers (the stochastic channels' planes and inputs)
 //   empty_like_dtype(like, code)    fresh contiguous CPU tensors shaped like `like`, uint8 / int8 / fp32 (code
 //                                   0 / 1 / 2): the stochastic encode's level and sign planes
+//   byte_planes(ts)                 whether every tensor is a contiguous CPU uint8 / int8 plane (the stochastic
+//                                   codecs' levels, exponents and signs), their element counts and data pointers
+//   shapes_equal(lists)             whether every list holds tensors of the first list's shapes, index by index
+//                                   (receive_mean's K updates of one model)
+//   entry_meta_k(lists)             for K lists of one model's entries: per entry, whether all K are contiguous
+//                                   CPU tensors of one dtype and shape, its dtype (0 fp32, 1 int64, 2 other) and
+//                                   element count (receive_mean's host aggregate of biases and statistics)
+//   concat_rows(lists, idx)         [K, total]: row k = list k's entries idx concatenated (one copy each)
+//   split_owned(flat, like)         owned tensors shaped like `like`, filled from consecutive pieces of flat
 // Every returned pointer table is an int64 CPU tensor (the native copy pool's piece lists).
 #include <torch/extension.h>
 
 #include <algorithm>
 #include <cstdint>
+#include <cstring>
 #include <tuple>
 #include <vector>
 
@@ -150,6 +160,97 @@ std::tuple<std::vector<at::Tensor>, at::Tensor> empty_like_dtype(const std::vect
   return {std::move(out), ptrs};
 }
 
+std::tuple<bool, at::Tensor, at::Tensor> byte_planes(const std::vector<at::Tensor>& ts) {
+  const int64_t n = (int64_t)ts.size();
+  at::Tensor numel = at::empty({n}, at::kLong), ptrs = at::empty({n}, at::kLong);
+  int64_t* ne = numel.data_ptr<int64_t>();
+  int64_t* pt = ptrs.data_ptr<int64_t>();
+  bool ok = true;
+  for (int64_t k = 0; k < n; ++k) {
+    const at::Tensor& t = ts[k];
+    ok = ok && !t.is_cuda() && t.is_contiguous() && t.element_size() == 1 && !t.is_quantized() &&
+         !t.is_floating_point() && t.scalar_type() != at::kBool;
+    ne[k] = t.numel();
+    pt[k] = (int64_t)(intptr_t)t.data_ptr();
+  }
+  return {ok, numel, ptrs};
+}
+
+bool shapes_equal(const std::vector<std::vector<at::Tensor>>& lists) {
+  if (lists.empty()) return true;
+  const auto& a = lists[0];
+  for (size_t r = 1; r < lists.size(); ++r) {
+    const auto& b = lists[r];
+    if (b.size() != a.size()) return false;
+    for (size_t k = 0; k < a.size(); ++k)
+      if (!a[k].sizes().equals(b[k].sizes())) return false;
+  }
+  return true;
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> entry_meta_k(const std::vector<std::vector<at::Tensor>>& lists) {
+  TORCH_CHECK(!lists.empty(), "entry_meta_k: no lists");
+  const size_t n = lists[0].size();
+  for (const auto& l : lists) TORCH_CHECK(l.size() == n, "entry_meta_k: lists of different lengths");
+  at::Tensor uni = at::empty({(int64_t)n}, at::kBool), code = at::empty({(int64_t)n}, at::kChar),
+             numel = at::empty({(int64_t)n}, at::kLong);
+  bool* u = uni.data_ptr<bool>();
+  int8_t* c = code.data_ptr<int8_t>();
+  int64_t* ne = numel.data_ptr<int64_t>();
+  for (size_t i = 0; i < n; ++i) {
+    const at::Tensor& t0 = lists[0][i];
+    bool ok = !t0.is_cuda() && t0.is_contiguous();
+    for (size_t r = 1; ok && r < lists.size(); ++r) {
+      const at::Tensor& t = lists[r][i];
+      ok = !t.is_cuda() && t.is_contiguous() && t.scalar_type() == t0.scalar_type() && t.sizes().equals(t0.sizes());
+    }
+    u[i] = ok;
+    c[i] = t0.scalar_type() == at::kFloat ? 0 : (t0.scalar_type() == at::kLong ? 1 : 2);
+    ne[i] = t0.numel();
+  }
+  return {uni, code, numel};
+}
+
+at::Tensor concat_rows(const std::vector<std::vector<at::Tensor>>& lists, const at::Tensor& idx) {
+  TORCH_CHECK(!lists.empty() && idx.scalar_type() == at::kLong && idx.numel() > 0, "concat_rows: bad arguments");
+  const int64_t* ix = idx.data_ptr<int64_t>();
+  const int64_t m = idx.numel();
+  const at::Tensor& first = lists[0][ix[0]];
+  int64_t total = 0;
+  for (int64_t j = 0; j < m; ++j) total += lists[0][ix[j]].numel();
+  at::Tensor out = at::empty({(int64_t)lists.size(), total}, first.options());
+  const int64_t es = (int64_t)first.element_size();
+  for (size_t r = 0; r < lists.size(); ++r) {
+    char* dst = static_cast<char*>(out[r].data_ptr());
+    for (int64_t j = 0; j < m; ++j) {
+      const at::Tensor& t = lists[r][ix[j]];
+      TORCH_CHECK(!t.is_cuda() && t.is_contiguous() && t.scalar_type() == first.scalar_type(),
+                  "concat_rows: entries must be contiguous CPU tensors of one dtype");
+      const int64_t nb = t.numel() * es;
+      std::memcpy(dst, t.data_ptr(), (size_t)nb);
+      dst += nb;
+    }
+  }
+  return out;
+}
+
+std::vector<at::Tensor> split_owned(const at::Tensor& flat, const std::vector<at::Tensor>& like) {
+  TORCH_CHECK(!flat.is_cuda() && flat.is_contiguous(), "split_owned: a contiguous CPU tensor");
+  std::vector<at::Tensor> out;
+  out.reserve(like.size());
+  const char* src = static_cast<const char*>(flat.data_ptr());
+  const int64_t es = (int64_t)flat.element_size();
+  int64_t off = 0;
+  for (const auto& l : like) {
+    at::Tensor t = at::empty(l.sizes(), flat.options());
+    TORCH_CHECK(off + t.numel() <= flat.numel(), "split_owned: flat too short");
+    std::memcpy(t.data_ptr(), src + off * es, (size_t)(t.numel() * es));
+    off += t.numel();
+    out.push_back(std::move(t));
+  }
+  return out;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -162,4 +263,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("tensor_meta", &tensor_meta);
   m.def("host_bytes", &host_bytes);
   m.def("empty_like_dtype", &empty_like_dtype);
+  m.def("shapes_equal", &shapes_equal);
+  m.def("byte_planes", &byte_planes);
+  m.def("entry_meta_k", &entry_meta_k);
+  m.def("concat_rows", &concat_rows);
+  m.def("split_owned", &split_owned);
 }

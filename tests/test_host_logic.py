@@ -214,3 +214,26 @@ def test_packed_channel_host_rules():
     assert PackedSLQChannel(4).to_json() == {"name": "PackedSLQChannel", "bits": 4}
     assert PackedSLQChannel(4).simulate_bandwidth(_bw_params(), 1e12) == SLQChannel(4).simulate_bandwidth(
         _bw_params(), 1e12)
+
+
+@pytest.mark.parametrize("k", [1, 2, 4, 5, 8, 9, 16, 20])
+def test_aggregate_entries_matches_simple_aggregate(k):
+    """receive_mean's host aggregate of the passthrough entries (biases, counters, running statistics: native
+    classification, K concatenated rows, torch's sum order, owned results) equals simple_aggregate
+    (Src/ADFL/model.py:221-234) entry by entry, bit for bit: fp32 of every tail shape, int64 counters (-> fp32),
+    one-element entries, empty and fp16 entries (per entry through torch)."""
+    import torch
+    from adfl_amd.Channel import quant
+    g = torch.Generator().manual_seed(k)
+    names = [f"b{i}" for i in range(40)] + ["cnt", "one", "e", "h"]
+    parts = []
+    for r in range(k):
+        p = {f"b{i}": torch.randn(1 + i * 7, generator=g) for i in range(40)}
+        p.update(cnt=torch.tensor(5 + r, dtype=torch.int64), one=torch.randn(1, generator=g), e=torch.empty(0),
+                 h=torch.randn(3, generator=g).half())
+        parts.append(p)
+    got = quant._aggregate_entries(names, parts)
+    for n in names:
+        want = quant._simple_aggregate([p[n] for p in parts])
+        assert got[n].dtype == want.dtype and got[n].shape == want.shape, n
+        assert torch.equal(got[n].reshape(-1).view(torch.uint8), want.reshape(-1).view(torch.uint8)), n
