@@ -989,8 +989,10 @@ def _encode_dict_packed(params: Parameters, names: List[str], bits: int, stats: 
     st = _staging()
     dev = st.device
     tensors = [params[n] for n in names]
-    lay = st.layout(tuple(int(t.numel()) for t in tensors), align=2)
-    x_dev = _stage_in(tensors, lay, st, "x", torch.float32)
+    th = _torchhost.get()
+    host_ok, numel, hptrs = th.host_bytes(tensors, 4)   # sizes, and contiguous CPU fp32 storages, in one call
+    lay = st.layout(tuple(numel.tolist()), align=2)
+    x_dev = _stage_in(tensors, lay, st, "x", torch.float32, host_ptrs=hptrs.numpy().view(np.uint64) if host_ok else None)
     p_dev, s_dev = ops.encode_batched_int4(x_dev, lay, bits, packed=st.buf("p", lay.total // 2, torch.uint8),
                                            scales=st.buf("scales", lay.ntensors, torch.float32),
                                            partials=st.buf("partials", lay.nchunks, torch.int32))
@@ -1001,9 +1003,14 @@ def _encode_dict_packed(params: Parameters, names: List[str], bits: int, stats: 
     scales_host.copy_(s_dev, non_blocking=True)
     torch.cuda.current_stream(dev).synchronize()
     scales = scales_host.tolist()
-    on_cpu = [not t.is_cuda for t in tensors]
     # packed-byte layout: with align=2 tensor k's ceil(n/2) bytes sit at offsets[k] / 2
     p_lay = st.layout(tuple(int(n) // 2 for n in lay.padded.tolist()), align=1)
+    if host_ok:   # the owned int8 payloads created by one native call per staging range while the D2H runs
+        p_numel = (numel + 1) // 2
+        parts = _PendingD2H(p_dev.view(torch.int8), p_lay, st, "p").finish_building(
+            None, len(tensors), make_batch=lambda a, b: th.empty_1d(p_numel[a:b], 1))
+        return {name: (pt, sc) for name, pt, sc in zip(names, parts, scales)}
+    on_cpu = [not t.is_cuda for t in tensors]
     shapes = [torch.Size([(int(t.numel()) + 1) // 2]) for t in tensors]
     # int8, as compression.py:pack_4bit returns; each tensor owns its bytes (the staging is reused)
     parts = _hand_out(p_dev.view(torch.int8), p_lay, shapes, on_cpu, st, "p")
@@ -1342,18 +1349,25 @@ class PackedSLQChannel(SLQChannel):
                             [torch.Size(all_c_params[0].params[n].shape) for n in names], packed=True)
 
     def _quantize_params(self, params: Parameters, bits: int, stats: Optional[list] = None) -> QuantParameters:
-        names = [name for name, p in params.items() if p.ndim > 1]
-        for name in names:
-            ops.require_quantizable(params[name])
+        items = list(params.items())
+        # every entry's ndim / numel / dtype in one native call (adfl_torchhost.tensor_meta)
+        ndim, numel, f32, _ = (a.numpy() for a in _torchhost.get().tensor_meta([p for _, p in items]))
+        qi = np.nonzero(ndim > 1)[0]
+        names = [items[i][0] for i in qi.tolist()]
+        bad = qi[(numel[qi] == 0) | ~f32[qi]]
+        if bad.size:
+            ops.require_quantizable(items[int(bad[0])][1])   # raises the reference's error for that tensor
         encoded = _encode_dict_packed(params, names, bits, stats) if names else {}
-        q_params = QuantParameters({}, 0)
-        for name, param in params.items():
+        signs = torch.zeros(1, dtype=torch.uint8)  # the unused field (compression.py:102), one object per call
+        qp = QuantParameter
+        out: Dict[str, QuantParameter] = {}
+        size = 0
+        for name, param in items:
             q_param, scale = encoded[name] if name in encoded else (param, 1)
-            q_params.params[name] = QuantParameter(
-                data=q_param, bits=bits, scale=scale, signs=torch.zeros(1, dtype=torch.uint8),
-                shape=param.shape, dtype=param.dtype, q_dtype=q_param.dtype)
-            q_params.size += q_param.nbytes
-        return q_params
+            # positional: QuantParameter(data, bits, scale, signs, shape, dtype, q_dtype) (model.py:21-31)
+            out[name] = qp(q_param, bits, scale, signs, param.shape, param.dtype, q_param.dtype)
+            size += q_param.nbytes
+        return QuantParameters(out, size)
 
 
 HipSLQChannel = SLQChannel

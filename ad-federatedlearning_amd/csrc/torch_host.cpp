@@ -22,6 +22,8 @@
 //                                   0 / 1 / 2): the stochastic encode's level and sign planes
 //   byte_planes(ts)                 whether every tensor is a contiguous CPU uint8 / int8 plane (the stochastic
 //                                   codecs' levels, exponents and signs), their element counts and data pointers
+//   empty_1d(numel, code)           fresh 1-D CPU tensors of the given element counts, uint8 / int8 / fp32 (the
+//                                   packed int4 channel's payloads: ceil(n/2) bytes each)
 //   shapes_equal(lists)             whether every list holds tensors of the first list's shapes, index by index
 //                                   (receive_mean's K updates of one model)
 //   entry_meta_k(lists)             for K lists of one model's entries: per entry, whether all K are contiguous
@@ -176,6 +178,24 @@ std::tuple<bool, at::Tensor, at::Tensor> byte_planes(const std::vector<at::Tenso
   return {ok, numel, ptrs};
 }
 
+std::tuple<std::vector<at::Tensor>, at::Tensor> empty_1d(const at::Tensor& numel, int64_t code) {
+  TORCH_CHECK(numel.scalar_type() == at::kLong && !numel.is_cuda() && numel.is_contiguous(), "empty_1d: int64 counts");
+  TORCH_CHECK(code >= 0 && code <= 2, "empty_1d: code 0 (uint8), 1 (int8) or 2 (float32)");
+  const at::ScalarType st = code == 0 ? at::kByte : (code == 1 ? at::kChar : at::kFloat);
+  const int64_t n = numel.numel();
+  const int64_t* ne = numel.data_ptr<int64_t>();
+  std::vector<at::Tensor> out;
+  out.reserve((size_t)n);
+  at::Tensor ptrs = at::empty({n}, at::kLong);
+  int64_t* p = ptrs.data_ptr<int64_t>();
+  const auto opts = at::TensorOptions().dtype(st);
+  for (int64_t k = 0; k < n; ++k) {
+    out.push_back(at::empty({ne[k]}, opts));
+    p[k] = (int64_t)(intptr_t)out.back().data_ptr();
+  }
+  return {std::move(out), ptrs};
+}
+
 bool shapes_equal(const std::vector<std::vector<at::Tensor>>& lists) {
   if (lists.empty()) return true;
   const auto& a = lists[0];
@@ -264,6 +284,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("host_bytes", &host_bytes);
   m.def("empty_like_dtype", &empty_like_dtype);
   m.def("shapes_equal", &shapes_equal);
+  m.def("empty_1d", &empty_1d);
   m.def("byte_planes", &byte_planes);
   m.def("entry_meta_k", &entry_meta_k);
   m.def("concat_rows", &concat_rows);

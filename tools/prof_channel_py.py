@@ -10,7 +10,7 @@ params = {}
 for i in range(256):
     params[f"layer{i}.weight"] = torch.randn(1, base + (1 if i < rem else 0), generator=g) * 1e-3
     params[f"layer{i}.bias"] = torch.randn(64, generator=g) * 1e-3
-ch = CH(8)
+ch = CH(4 if sys.argv[1:2] == ["PackedSLQChannel"] else 8)
 for _ in range(5):
     qp, _ = ch.on_client_send(params); ch.on_server_receive(qp)
 ts=[]
