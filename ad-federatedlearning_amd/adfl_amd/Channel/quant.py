@@ -248,6 +248,12 @@ def _stage_in(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _DeviceSta
     host_ptrs: the tensors' data pointers when the caller knows them all to be contiguous CPU tensors of the
     bucket's element size (adfl_torchhost.qint8_meta checked them in one call)."""
     dev_buf = st.buf(key, lay.total, dtype)
+    if host_ptrs is None and tensors and tensors[0].is_cuda:
+        # a device dict: its pointers and sizes checked in one native call, then one gather launch
+        ok, numel, dptrs = _torchhost.get().device_ptrs(tensors, st.device.index, dev_buf.element_size())
+        if ok and np.array_equal(numel.numpy(), lay.sizes):
+            ops.bucket_gather(tensors, lay, dev_buf, checked=False, ptrs=dptrs)
+            return dev_buf
     kinds = {False} if host_ptrs is not None else {t.is_cuda for t in tensors}
     if kinds == {False}:
         _host_heap(lay)
@@ -450,8 +456,14 @@ def _hand_out(out_dev: torch.Tensor, lay: ops.BucketLayout, shapes: List[torch.S
         return pending.finish_building(lambda k: torch.empty(shapes[k], dtype=dt), len(shapes))
     if not any(on_cpu) and out_dev.device == st.device:
         # device dict: fresh owned tensors filled from the bucket by one launch (not one clone per tensor)
-        dev_outs = [torch.empty(s, dtype=out_dev.dtype, device=st.device) for s in shapes]
-        ops.bucket_scatter(out_dev, lay, dev_outs, checked=False)
+        th = _torchhost.get()
+        if (like is not None and out_dev.dtype == torch.float32
+                and th.device_ptrs(like, st.device.index, like[0].element_size())[0]):
+            dev_outs, ptrs = th.empty_f32_like(like)   # one native call, on like's (= the staging's) device
+            ops.bucket_scatter(out_dev, lay, dev_outs, checked=False, ptrs=ptrs)
+        else:
+            dev_outs = [torch.empty(s, dtype=out_dev.dtype, device=st.device) for s in shapes]
+            ops.bucket_scatter(out_dev, lay, dev_outs, checked=False)
         torch.cuda.current_stream(st.device).synchronize()
         return dev_outs
     for i, (off, n, s) in enumerate(zip(lay.offsets.tolist(), lay.sizes.tolist(), shapes)):
@@ -652,10 +664,10 @@ def _encode_dict(params: Parameters, names: List[str], bits: int, stats: Optiona
     torch.cuda.current_stream(dev).synchronize()
     scales = scales_host.tolist()
     if not any(on_cpu) and all(t.device == dev for t in tensors):
-        # device dict: the qint8 payloads allocated (no launch each) and filled from the bucket by one launch
-        qs = [torch._empty_affine_quantized(t.shape, scale=sc, zero_point=0, dtype=torch.qint8, device=dev)
-              for t, sc in zip(tensors, scales)]
-        ops.bucket_scatter(q_dev, lay, qs, checked=False)
+        # device dict: the qint8 payloads allocated by one native call (on the tensors' device, no launch each)
+        # and filled from the bucket by one launch
+        qs, qp = _torchhost.get().empty_qint8_like(tensors, scales_host)
+        ops.bucket_scatter(q_dev, lay, qs, checked=False, ptrs=qp)
         torch.cuda.current_stream(dev).synchronize()
         return {name: (qt, sc) for name, qt, sc in zip(names, qs, scales)}
     out = {}
@@ -708,7 +720,7 @@ def _decode_dict(items: List[Tuple[str, torch.Tensor]], idle=None) -> Dict[str, 
     with _ph("dec.kernel_launch"):
         out_dev = ops.decode_batched(q_dev, s_dev, lay, out=st.buf("d_out", lay.total, torch.float32))
     decoded = _hand_out(out_dev, lay, [q.shape for q in qlist] if not all_host else [None] * len(qlist), on_cpu, st,
-                        "d_out", like=qlist if all_host else None)
+                        "d_out", like=qlist if all_host or all_dev else None)
     return {name: t for (name, _), t in zip(items, decoded)}
 
 

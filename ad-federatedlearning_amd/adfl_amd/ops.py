@@ -379,12 +379,16 @@ def qerror_batched_int4(flat: torch.Tensor, packed: torch.Tensor, scales: torch.
     return tuple(partials.view(-1, 4).sum(0).tolist())
 
 
-def _bucket_ptr_table(tensors, layout: BucketLayout, bucket: torch.Tensor, what: str, checked: bool) -> torch.Tensor:
+def _bucket_ptr_table(tensors, layout: BucketLayout, bucket: torch.Tensor, what: str, checked: bool,
+                      ptrs: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Device int64 table of the tensors' data pointers, after checking them against the layout and bucket
-    (checked=False: tensors the caller has just allocated to match, as the Channel's outputs are)."""
+    (checked=False: tensors the caller has just allocated to match, as the Channel's outputs are; ptrs: their
+    pointers as a CPU int64 tensor when the caller already has them)."""
     dev = bucket.device
     if len(tensors) != layout.ntensors:
         raise ValueError(f"{what}: {len(tensors)} tensors for a layout of {layout.ntensors}")
+    if ptrs is not None and not checked:
+        return ptrs.to(dev, non_blocking=True)
     if checked:
         es = bucket.element_size()
         for t, (x, n) in enumerate(zip(tensors, layout.sizes.tolist())):
@@ -403,23 +407,25 @@ def _check_bucket(bucket: torch.Tensor, layout: BucketLayout, what: str) -> torc
     return bucket
 
 
-def bucket_gather(tensors, layout: BucketLayout, bucket: torch.Tensor, *, checked: bool = True) -> torch.Tensor:
+def bucket_gather(tensors, layout: BucketLayout, bucket: torch.Tensor, *, checked: bool = True,
+                  ptrs: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Copy every tensor into its slot of the device bucket (tensor t at layout.offsets[t]), one launch
     (adfl_bucket_gather). Tensors: contiguous, on the bucket's device, of its element size (any dtype,
     quantized included); pads between slots are left as they are."""
     bucket = _check_bucket(bucket, layout, "bucket_gather")
-    table = _bucket_ptr_table(tensors, layout, bucket, "bucket_gather", checked)
+    table = _bucket_ptr_table(tensors, layout, bucket, "bucket_gather", checked, ptrs)
     check(_lib.load().adfl_bucket_gather(bucket.data_ptr(), layout.device_chunks(bucket.device).data_ptr(),
                                          layout.nchunks, table.data_ptr(), bucket.element_size(),
                                          _stream(bucket.device)))
     return bucket
 
 
-def bucket_scatter(bucket: torch.Tensor, layout: BucketLayout, tensors, *, checked: bool = True) -> None:
+def bucket_scatter(bucket: torch.Tensor, layout: BucketLayout, tensors, *, checked: bool = True,
+                   ptrs: Optional[torch.Tensor] = None) -> None:
     """Copy every slot of the device bucket into its own tensor (tensor t from layout.offsets[t]), one launch
     (adfl_bucket_scatter): the owned per-tensor outputs of a bucketed decode or encode."""
     bucket = _check_bucket(bucket, layout, "bucket_scatter")
-    table = _bucket_ptr_table(tensors, layout, bucket, "bucket_scatter", checked)
+    table = _bucket_ptr_table(tensors, layout, bucket, "bucket_scatter", checked, ptrs)
     check(_lib.load().adfl_bucket_scatter(bucket.data_ptr(), layout.device_chunks(bucket.device).data_ptr(),
                                           layout.nchunks, table.data_ptr(), bucket.element_size(),
                                           _stream(bucket.device)))

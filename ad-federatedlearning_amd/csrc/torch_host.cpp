@@ -3,9 +3,10 @@
 // and expects 256 owned tensors back from every on_client_send / on_server_receive (quant.py:74-112): their
 // creation, and reading each payload's quantizer, cost ~2.5 us per tensor per Python call — about 0.6 ms per
 // direction on C3, as much as the PCIe copies they overlap. Here each batch is one call into ATen:
-//   empty_f32_like(like)            fresh contiguous fp32 CPU tensors shaped like `like` (the decode's outputs)
-//   empty_qint8_like(like, scales)  per-tensor affine qint8 CPU tensors, zero point 0, scale[k] (the payloads,
-//                                   as torch.quantize_per_tensor(x, scale, 0, torch.qint8) shapes them)
+//   empty_f32_like(like)            fresh contiguous fp32 tensors shaped like `like`, on each one's device (the
+//                                   decode's outputs)
+//   empty_qint8_like(like, scales)  per-tensor affine qint8 tensors, zero point 0, scale[k], on each like's
+//                                   device (the payloads, as torch.quantize_per_tensor(x, scale, 0, qint8) makes them)
 //   qint8_meta(q)                   for payload tensors: whether every one is a per-tensor affine qint8 tensor
 //                                   with zero point 0, whether all are contiguous CPU tensors, their element
 //                                   counts, fp32 scales (fbgemm uses q_scale() as fp32, quant.py:110) and
@@ -24,6 +25,9 @@
 //                                   codecs' levels, exponents and signs), their element counts and data pointers
 //   empty_1d(numel, code)           fresh 1-D CPU tensors of the given element counts, uint8 / int8 / fp32 (the
 //                                   packed int4 channel's payloads: ceil(n/2) bytes each)
+//   device_ptrs(ts, index, elem)    whether every tensor is a contiguous tensor of elem-byte elements on cuda:index,
+//                                   their element counts and data pointers (a device-resident dict's one-launch
+//                                   gather / scatter)
 //   shapes_equal(lists)             whether every list holds tensors of the first list's shapes, index by index
 //                                   (receive_mean's K updates of one model)
 //   entry_meta_k(lists)             for K lists of one model's entries: per entry, whether all K are contiguous
@@ -49,7 +53,7 @@ std::tuple<std::vector<at::Tensor>, at::Tensor> empty_f32_like(const std::vector
   int64_t* p = ptrs.data_ptr<int64_t>();
   const auto opts = at::TensorOptions().dtype(at::kFloat);
   for (size_t k = 0; k < like.size(); ++k) {
-    out.push_back(at::empty(like[k].sizes(), opts));
+    out.push_back(at::empty(like[k].sizes(), opts.device(like[k].device())));
     p[k] = (int64_t)(intptr_t)out.back().data_ptr();
   }
   return {std::move(out), ptrs};
@@ -67,7 +71,7 @@ std::tuple<std::vector<at::Tensor>, at::Tensor> empty_qint8_like(const std::vect
   int64_t* p = ptrs.data_ptr<int64_t>();
   const auto opts = at::TensorOptions().dtype(at::kQInt8);
   for (size_t k = 0; k < like.size(); ++k) {
-    out.push_back(at::_empty_affine_quantized(like[k].sizes(), opts, (double)s[k], 0));
+    out.push_back(at::_empty_affine_quantized(like[k].sizes(), opts.device(like[k].device()), (double)s[k], 0));
     p[k] = (int64_t)(intptr_t)out.back().data_ptr();
   }
   return {std::move(out), ptrs};
@@ -196,6 +200,23 @@ std::tuple<std::vector<at::Tensor>, at::Tensor> empty_1d(const at::Tensor& numel
   return {std::move(out), ptrs};
 }
 
+std::tuple<bool, at::Tensor, at::Tensor> device_ptrs(const std::vector<at::Tensor>& ts, int64_t device_index,
+                                                      int64_t elem) {
+  const int64_t n = (int64_t)ts.size();
+  at::Tensor numel = at::empty({n}, at::kLong), ptrs = at::empty({n}, at::kLong);
+  int64_t* ne = numel.data_ptr<int64_t>();
+  int64_t* p = ptrs.data_ptr<int64_t>();
+  bool ok = true;
+  for (int64_t k = 0; k < n; ++k) {
+    const at::Tensor& t = ts[k];
+    ok = ok && t.is_cuda() && t.device().index() == device_index && t.is_contiguous() &&
+         (int64_t)t.element_size() == elem;
+    ne[k] = t.numel();
+    p[k] = (int64_t)(intptr_t)t.data_ptr();
+  }
+  return {ok, numel, ptrs};
+}
+
 bool shapes_equal(const std::vector<std::vector<at::Tensor>>& lists) {
   if (lists.empty()) return true;
   const auto& a = lists[0];
@@ -284,6 +305,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("host_bytes", &host_bytes);
   m.def("empty_like_dtype", &empty_like_dtype);
   m.def("shapes_equal", &shapes_equal);
+  m.def("device_ptrs", &device_ptrs);
   m.def("empty_1d", &empty_1d);
   m.def("byte_planes", &byte_planes);
   m.def("entry_meta_k", &entry_meta_k);
