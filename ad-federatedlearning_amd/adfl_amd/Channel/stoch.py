@@ -79,8 +79,17 @@ def _owned(parts: List[torch.Tensor], shapes: List[torch.Size]) -> List[torch.Te
     return [p.view(s).clone() for p, s in zip(parts, shapes)]
 
 
-def _owned_dev(buf: torch.Tensor, lay, shapes: List[torch.Size]) -> List[torch.Tensor]:
-    """_owned for a device dict: fresh tensors filled from the bucket by one launch (ops.bucket_scatter)."""
+_DTYPE_CODE = {torch.uint8: 0, torch.int8: 1, torch.float32: 2}   # adfl_torchhost.empty_like_dtype
+
+
+def _owned_dev(buf: torch.Tensor, lay, shapes: List[torch.Size], like=None) -> List[torch.Tensor]:
+    """_owned for a device dict: fresh tensors filled from the bucket by one launch (ops.bucket_scatter); with
+    `like` (the dict's tensors, all on the bucket's device) created by one native call."""
+    code = _DTYPE_CODE.get(buf.dtype)
+    if like is not None and code is not None:
+        outs, ptrs = _torchhost.get().empty_like_dtype(like, code)
+        ops.bucket_scatter(buf, lay, outs, checked=False, ptrs=ptrs)
+        return outs
     outs = [torch.empty(s, dtype=buf.dtype, device=buf.device) for s in shapes]
     ops.bucket_scatter(buf, lay, outs, checked=False)
     return outs
@@ -171,7 +180,9 @@ def _encode_stoch(params: Parameters, names: List[str], codec: str, bits: int, u
     lv_parts = _owned_host(lv_h, lay.offsets, shapes) if any(on_cpu) else None
     sg_parts = _owned_host(sg_h, lay.offsets, shapes) if any(on_cpu) else None
     if not any(on_cpu):   # device dict: one scatter launch per plane
-        lv_dev, sg_dev = _owned_dev(lv, lay, shapes), _owned_dev(sg, lay, shapes)
+        same = _torchhost.get().device_ptrs(tensors, dev.index, 4)[0]   # all on the staging's device
+        lv_dev = _owned_dev(lv, lay, shapes, like=tensors if same else None)
+        sg_dev = _owned_dev(sg, lay, shapes, like=tensors if same else None)
     else:
         lv_dev = _owned(split(lv), shapes) if not all(on_cpu) else None
         sg_dev = _owned(split(sg), shapes) if not all(on_cpu) else None
@@ -398,7 +409,7 @@ def _decode_stoch(items: List[Tuple[str, QuantParameter]], codec: str, bits: int
     datas = [p.data for _, p in items]
     on_cpu = [not d.is_cuda for d in datas]
     # CPU payloads: the fp32 outputs (shaped like the level planes) made in one native call per range
-    decoded = _hand_out(out_dev, lay, [d.shape for d in datas], on_cpu, st, "d_out", like=datas if all(on_cpu) else None)
+    decoded = _hand_out(out_dev, lay, [d.shape for d in datas], on_cpu, st, "d_out", like=datas)
     return {name: t for (name, _), t in zip(items, decoded)}
 
 

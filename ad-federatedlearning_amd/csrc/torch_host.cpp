@@ -19,8 +19,8 @@
 //                                   _quantize_params and the staging choose by, for a whole state dict at once
 //   host_bytes(ts, elem)            whether every tensor is a contiguous CPU tensor of elem-byte elements, their
 //                                   element counts and data pointers (the stochastic channels' planes and inputs)
-//   empty_like_dtype(like, code)    fresh contiguous CPU tensors shaped like `like`, uint8 / int8 / fp32 (code
-//                                   0 / 1 / 2): the stochastic encode's level and sign planes
+//   empty_like_dtype(like, code)    fresh contiguous tensors shaped like `like`, on each one's device, uint8 /
+//                                   int8 / fp32 (code 0 / 1 / 2): the stochastic encode's level and sign planes
 //   byte_planes(ts)                 whether every tensor is a contiguous CPU uint8 / int8 plane (the stochastic
 //                                   codecs' levels, exponents and signs), their element counts and data pointers
 //   empty_1d(numel, code)           fresh 1-D CPU tensors of the given element counts, uint8 / int8 / fp32 (the
@@ -160,7 +160,7 @@ std::tuple<std::vector<at::Tensor>, at::Tensor> empty_like_dtype(const std::vect
   int64_t* p = ptrs.data_ptr<int64_t>();
   const auto opts = at::TensorOptions().dtype(st);
   for (size_t k = 0; k < like.size(); ++k) {
-    out.push_back(at::empty(like[k].sizes(), opts));
+    out.push_back(at::empty(like[k].sizes(), opts.device(like[k].device())));
     p[k] = (int64_t)(intptr_t)out.back().data_ptr();
   }
   return {std::move(out), ptrs};
