@@ -287,6 +287,19 @@ def _stage_in(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _DeviceSta
 _PIPELINE = os.environ.get("ADFL_HOST_PIPELINE", "1") != "0"
 
 
+def _drain(*streams) -> None:
+    """A pipelined host path that fails part-way (an output allocation, a caller's emit / idle callback, a
+    native call) may leave H2D copies reading, and kernels and D2H copies writing, the staging buffers it
+    shares with the next call (the pinned buckets, the device buckets): wait for every stream it enqueued on
+    before the exception leaves, so the next call's gathers cannot overwrite a buffer still in use."""
+    for s in streams:
+        if s is not None:
+            try:
+                s.synchronize()
+            except Exception:   # the original exception is the one to report
+                pass
+
+
 class PhaseClock:
     """Wall milliseconds the calling thread spends in each phase of the host-to-host path (exclusive, no extra
     synchronisation): filled while a `phase_clock()` block is active, e.g. bench.py's channel_c3_dict."""
@@ -352,6 +365,7 @@ class _PendingD2H:
         self.host = st.buf(key + "_host", lay.total, dev_buf.dtype, pinned=True)
         self.lay = lay
         stream = torch.cuda.current_stream(st.device)
+        self.stream = stream
         self.ranges = _ranges(lay, self.host.element_size())
         self.events = []
         for lo, hi in self.ranges:
@@ -412,6 +426,9 @@ class _PendingD2H:
             while k < count:   # tensors past the last range (none for a bucket layout; kept for safety)
                 outs.append(make(k))
                 k += 1
+        except BaseException:
+            _drain(self.stream)
+            raise
         finally:
             with _ph("out.scatter_wait"):
                 for pd in pending:
@@ -589,6 +606,9 @@ def _encode_host_dict(tensors: List[torch.Tensor], lay: ops.BucketLayout, st: _D
                     stream=True, event=ev, keep=q_host))
             with _ph("enc.passthrough"):
                 idle()
+    except BaseException:
+        _drain(stream, d2h)
+        raise
     finally:
         for j in jobs:
             j.wait()
@@ -795,6 +815,9 @@ def _decode_host_dict(qlist: List[torch.Tensor], lay: ops.BucketLayout, st: _Dev
         if idle is not None:
             with _ph("dec.passthrough"):
                 idle()
+    except BaseException:
+        _drain(stream, d2h)
+        raise
     finally:
         for j in jobs:
             j.wait()

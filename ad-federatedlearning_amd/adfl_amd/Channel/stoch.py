@@ -47,8 +47,8 @@ from .._lib import check
 from ..model import CompressedParameters, Parameters, QuantParameter, QuantParameters, get_parameter_info
 from .channel import Channel, IdentityChannel
 from . import quant as _quant
-from .quant import (_PendingD2H, _aggregate_entries, _chunk_meta, _hand_out, _host_heap, _ph, _range_copies,
-                    _ranges, _serialized, _stage_in, _stage_rows, _staging, device_mean_order_ok)
+from .quant import (_PendingD2H, _aggregate_entries, _chunk_meta, _drain, _hand_out, _host_heap, _ph,
+                    _range_copies, _ranges, _serialized, _stage_in, _stage_rows, _staging, device_mean_order_ok)
 
 _CODECS = ("qsgd", "rqsgd", "cnat")
 
@@ -310,6 +310,9 @@ def _encode_stoch_host(tensors, names, hptrs: np.ndarray, lay, st, codec: str, b
         norms_ready.record(stream)
         while idle():   # the caller's remaining objects, while the last copies land
             pass
+    except BaseException:
+        _drain(h2d, stream, st.d2h_stream())
+        raise
     finally:
         for j in jobs:
             j.wait()
@@ -485,6 +488,9 @@ def _decode_stoch_host(st, items, datas, numel: torch.Tensor, lptrs: np.ndarray,
             scatters.append(hostcopy.submit_pieces(
                 *_range_copies(out_ptrs, lay, oh, 4, e0, e1, to_bucket=False),
                 stream=True, event=evs[2 * r + 1], keep=out_host))
+    except BaseException:
+        _drain(torch.cuda.current_stream(dev), st.d2h_stream())
+        raise
     finally:
         for j in jobs:
             j.wait()

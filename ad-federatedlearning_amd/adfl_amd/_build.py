@@ -45,6 +45,13 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
 TORCH_HOST_SRC = os.path.join(SRC_ROOT, "csrc", "torch_host.cpp")
 TORCH_HOST_PATH = os.path.join(LIB_DIR, "adfl_torchhost.so")
+TORCH_HOST_STAMP = TORCH_HOST_PATH + ".torch"   # the torch build it was compiled against
+
+
+def torch_host_stamp() -> str:
+    """The torch version and C++ ABI adfl_torchhost.so links against (libc10 / libtorch symbols)."""
+    import torch
+    return f"{torch.__version__} cxx11abi={int(torch._C._GLIBCXX_USE_CXX11_ABI)}"
 
 
 def build_torch_host(force: bool = False, verbose: bool = False) -> str:
@@ -55,7 +62,9 @@ def build_torch_host(force: bool = False, verbose: bool = False) -> str:
     import torch
     from torch.utils import cpp_extension as ce
     os.makedirs(LIB_DIR, exist_ok=True)
-    if (not force and os.path.exists(TORCH_HOST_PATH)
+    stamp = torch_host_stamp()
+    built = open(TORCH_HOST_STAMP).read().strip() if os.path.exists(TORCH_HOST_STAMP) else None
+    if (not force and os.path.exists(TORCH_HOST_PATH) and built == stamp
             and os.path.getmtime(TORCH_HOST_PATH) >= os.path.getmtime(TORCH_HOST_SRC)):
         return TORCH_HOST_PATH
     abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
@@ -68,6 +77,8 @@ def build_torch_host(force: bool = False, verbose: bool = False) -> str:
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
+    with open(TORCH_HOST_STAMP, "w") as f:
+        f.write(stamp + "\n")
     return TORCH_HOST_PATH
 
 

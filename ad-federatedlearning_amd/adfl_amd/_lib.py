@@ -23,7 +23,7 @@ INT = ctypes.c_int
 ALIGN_ELEMS = 64     # ADFL_SLQ_ALIGN_ELEMS
 CHUNK_ELEMS = 8192   # ADFL_SLQ_CHUNK_ELEMS
 RESIDENT_CHUNKS = 8  # ADFL_SLQ_RESIDENT_CHUNKS
-ABI_VERSION = 1      # ADFL_SLQ_ABI_VERSION
+ABI_VERSION = 2      # ADFL_SLQ_ABI_VERSION
 
 
 class AdflError(RuntimeError):

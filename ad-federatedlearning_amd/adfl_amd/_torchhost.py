@@ -19,6 +19,11 @@ def get():
             raise ImportError(f"adfl_amd: {path} is missing; build it with "
                               "`python -c 'import __graft_entry__ as g; g.build()'`")
         import torch  # noqa: F401  (libc10 / libtorch loaded first)
+        stamp = open(_build.TORCH_HOST_STAMP).read().strip() if os.path.exists(_build.TORCH_HOST_STAMP) else None
+        if stamp != _build.torch_host_stamp():
+            raise ImportError(f"adfl_amd: {path} was built against torch {stamp or '(unknown)'}, this process runs "
+                              f"{_build.torch_host_stamp()}; rebuild it with "
+                              "`python -c 'import __graft_entry__ as g; g.build()'`")
         loader = importlib.machinery.ExtensionFileLoader("adfl_torchhost", path)
         spec = importlib.util.spec_from_loader("adfl_torchhost", loader)
         mod = importlib.util.module_from_spec(spec)

@@ -144,6 +144,10 @@ def reference_norms(flat: torch.Tensor, layout: BucketLayout, *, threads: Option
         return out64, out32
     L = _lib.load()
     threads = torch.get_num_threads() if threads is None else int(threads)
+    if flat.dtype == torch.float16:   # at::parallel_for splits a tensor into at most ceil(n / GRAIN) pieces
+        threads = min(threads, max(1, -(-int(max(layout.sizes)) // 32768)))
+    elif threads < 1:
+        raise ValueError("adfl_amd.stoch: threads must be >= 1")
     short_max = L.adfl_torch_norm_short_max()
     kinds = (1 if min(layout.sizes) <= short_max else 0) | (2 if max(layout.sizes) > short_max else 0)
     need = L.adfl_torch_norm_scratch_bytes(layout.nchunks, layout.ntensors)

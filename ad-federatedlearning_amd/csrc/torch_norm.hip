@@ -1275,6 +1275,223 @@ __device__ typename Acc<Dt<DT>::kWide>::T resolve_chain(const void* x, const Ten
   return acc;
 }
 
+// ---- short fp32 tensors: k_tn_short, one block per tensor, one wave per chain, one launch
+// The fp32 form of the binade model, with no fp64 and no integer conversion. On binade G (ulp u = 2^(G-23),
+// A = acc / u in [2^23, 2^24); G = -126 also holds the subnormals) a step adds R(x^2 / u) * u, which is exactly
+// fma(x, x, B) - B for B = 2^G (A = 2^23, even) whenever x^2 < 2^G — the fma rounds B + x^2 on G's own grid —
+// and for B = +0 on G = -126 (RN(x^2) is then on the subnormal grid). Increments and their sums are multiples of
+// u, exact in fp32 below 2^24 u; above it every sum still rounds to at least 2^24 u (RN is monotone and the terms
+// are >= 0), so acc + the sum of a run stays below 2^(G+1) exactly when the run is covered, and a step of
+// x^2 >= 2^G (whose fma leaves the binade) is never covered. The increment agrees with the even-A rounding of the
+// step; odd A differs only on a tie (x^2 / u = f + 1/2), and a tie on G or on G + 1 needs x^2 to be a multiple
+// of u / 2: 2 lsb(x) >= G - 24, with lsb(x) = E - 150 + ctz(mantissa | 2^23) for x's biased exponent E (a
+// subnormal x squares far below u / 2). A lane whose 16 steps cannot rule that out sends its round down the
+// exact map path (lane_map_exact, fp64). Measured against k_norm_walk (the chains run in order) and torch
+// itself: tests/test_gpu_torch_norm.py, test_gpu_torch_norm_dt.py.
+constexpr int kShThreads = 512;                 // wave c runs chain c
+constexpr int kShSeg = 8 * kSeg;                // 8192 elements: 1024 steps of each chain
+constexpr int kShLS = 20;                       // floats per lane's run in LDS (16 steps + 4: 16-byte reads)
+constexpr int kShRow = 64 * kShLS + 8;          // floats per chain (+8: chains c and c + 4 alone share banks)
+constexpr int kShLoads = kShSeg / kShThreads;   // 16 loads per thread per segment
+
+// the n % 8 tail after the lane sum (and the whole sum below 8 elements) as torch's compiled scalar loop runs
+// it: 4 rounded squares added in order when there are 4 or more, the rest with fma (as k_norm_walk's tail_sum)
+__device__ __forceinline__ float tail32(const float* x, int64_t d, int64_t n, float b) {
+  if (n - d >= 4) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float sq = x[d + k] * x[d + k];
+      b = b + sq;
+    }
+    d += 4;
+  }
+  for (int64_t i = d; i < n; ++i) b = __builtin_fmaf(x[i], x[i], b);
+  return b;
+}
+
+template <int CTRL, int RM>
+__device__ __forceinline__ float dpp0(float v) {  // the DPP-moved value, +0 where the lane has no source
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, RM, 0xf, false));
+}
+// inclusive wave scan in fp32 by DPP (row shifts, then the row broadcasts 15 and 31): exact on multiples of u
+// whose sums stay below 2^24 u, a lower bound of 2^24 u otherwise (any summation tree of terms >= 0)
+__device__ __forceinline__ float wave_incl_f(float v) {
+  v += dpp0<0x111, 0xf>(v);  // row_shr:1
+  v += dpp0<0x112, 0xf>(v);  // row_shr:2
+  v += dpp0<0x114, 0xf>(v);  // row_shr:4
+  v += dpp0<0x118, 0xf>(v);  // row_shr:8
+  v += dpp0<0x142, 0xa>(v);  // row_bcast:15 into rows 1 and 3
+  v += dpp0<0x143, 0xc>(v);  // row_bcast:31 into rows 2 and 3
+  return v;
+}
+__device__ __forceinline__ float lane_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+// One segment of a chain (lane l: steps 16 l .. 16 l + 15, in order) from the exact accumulator acc (wave-uniform).
+__device__ __forceinline__ float short_segment(const float (&v)[kLane], float acc, int lane) {
+  uint32_t lsb = 0;  // max over the lane's steps of E + ctz(mantissa | 2^23)
+#pragma unroll
+  for (int i = 0; i < kLane; ++i) {
+    const uint32_t b = __float_as_uint(v[i]);
+    lsb = max(lsb, ((b >> 23) & 0xffu) + (uint32_t)__builtin_ctz(b | 0x800000u));
+  }
+  int start = 0;
+  for (;;) {
+    if (!__builtin_isfinite(acc)) {  // inf stays inf unless a NaN follows; NaN stays NaN
+      bool nan = false;
+#pragma unroll
+      for (int i = 0; i < kLane; ++i) nan |= __builtin_isnan(v[i]);
+      if (__ballot(nan && lane >= start)) acc = __builtin_nanf("");
+      return acc;
+    }
+    const int G = grid_of(acc);
+    if (__ballot(lane >= start && 2 * (int)lsb >= G + 276) == 0ull) {
+      const float B0 = G > -126 ? pow2f(G) : 0.0f, B1 = pow2f(G + 1);  // B1 = +inf above the top binade
+      float K0a = 0.0f, K0b = 0.0f, K1a = 0.0f, K1b = 0.0f;
+#pragma unroll
+      for (int i = 0; i < kLane; i += 2) {
+        K0a += __builtin_fmaf(v[i], v[i], B0) - B0;
+        K1a += __builtin_fmaf(v[i], v[i], B1) - B1;
+        K0b += __builtin_fmaf(v[i + 1], v[i + 1], B0) - B0;
+        K1b += __builtin_fmaf(v[i + 1], v[i + 1], B1) - B1;
+      }
+      const float K0 = lane >= start ? K0a + K0b : 0.0f, K1 = K1a + K1b;
+      const float I0 = wave_incl_f(K0), out = acc + I0;
+      const unsigned long long ball = __ballot(lane >= start && !(out < B1));
+      if (ball == 0ull) return lane_f(out, 63);
+      // the first lane that leaves G runs its steps with fma from its exact start
+      const int ls = __builtin_ctzll(ball);
+      float a = acc + (ls > 0 ? lane_f(I0, ls - 1) : 0.0f);
+      if (lane == ls) {
+#pragma unroll
+        for (int i = 0; i < kLane; ++i) a = __builtin_fmaf(v[i], v[i], a);
+      }
+      acc = lane_f(a, ls);
+      start = ls + 1;
+      if (start == 64) return acc;
+      // on from lane ls + 1 with the increments on G + 1, if that is where acc went
+      if (__builtin_isfinite(acc) && grid_of(acc) == G + 1) {
+        const float I1 = wave_incl_f(lane > ls ? K1 : 0.0f), out1 = acc + I1;
+        const unsigned long long b1 = __ballot(lane > ls && !(out1 < pow2f(G + 2)));
+        if (b1 == 0ull) return lane_f(out1, 63);
+        const int l1 = __builtin_ctzll(b1);
+        a = acc + lane_f(I1, l1 - 1);
+        if (lane == l1) {
+#pragma unroll
+          for (int i = 0; i < kLane; ++i) a = __builtin_fmaf(v[i], v[i], a);
+        }
+        acc = lane_f(a, l1);
+        start = l1 + 1;
+        if (start == 64) return acc;
+      }
+      continue;
+    }
+    // a tie is possible in some lane: this round by exact maps (what the run adds to an even / an odd A)
+    Map m = lane_map_exact<false>(v, G);
+    if (lane < start) m = Map{0.0, 0.0};
+    const double A = a_of(acc);
+    const double Al = apply(wave_excl(m, lane), A);
+    const double out = apply(m, Al);
+    const unsigned long long ball = __ballot(lane >= start && !(out < Acc<false>::kTop));
+    if (ball == 0ull) return rebuild<false>(__shfl(out, 63, 64), G);
+    const int ls = __builtin_ctzll(ball);
+    float a = rebuild<false>(__shfl(Al, ls, 64), G);
+    if (lane == ls) {
+#pragma unroll
+      for (int i = 0; i < kLane; ++i) a = __builtin_fmaf(v[i], v[i], a);
+    }
+    acc = lane_f(a, ls);
+    start = ls + 1;
+    if (start == 64) return acc;
+  }
+}
+
+// One block per tensor of at most max_n elements (grid: the chunk table; blocks not at a tensor's first chunk
+// return). The 8 waves stream the tensor in 8192-element segments: every thread loads 16 consecutive-lane
+// dwords per segment (buffer loads whose range ends at the chain steps' end, so the rest reads as +0, which no
+// chain notices), two segments ahead in registers, and stages them chain-major into LDS; wave c then reads its
+// lanes' 16-step runs of chain c (4 ds_read_b128 each) and advances the chain by short_segment. Then the lane
+// sum left to right, the n % 8 tail and the sqrt, as k_norm_walk does.
+__global__ __launch_bounds__(kShThreads) void k_tn_short(const float* __restrict__ x, const adfl_slq_chunk* __restrict__ chunks,
+                                                         int64_t max_n, double* __restrict__ norms64,
+                                                         float* __restrict__ norms32) {
+  __shared__ __attribute__((aligned(16))) float buf[8 * kShRow];
+  __shared__ float s_acc[8];
+  const adfl_slq_chunk ch = chunks[blockIdx.x];
+  if ((int64_t)blockIdx.x != ch.first_chunk) return;
+  const int64_t n = (int64_t)(ch.nchunks - 1) * ADFL_SLQ_CHUNK_ELEMS + chunks[blockIdx.x + ch.nchunks - 1].len;
+  if (n > max_n) return;
+  const float* xt = x + ch.start;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (n < 8) {
+    if (tid == 0) {
+      const float b = tail32(xt, 0, n, 0.0f);
+      const float r = n == 1 ? __builtin_fabsf(xt[0]) : (float)__builtin_sqrt((double)b);  // one element: |x|
+      if (norms32) norms32[ch.tensor] = r;
+      if (norms64) norms64[ch.tensor] = r;
+    }
+    return;
+  }
+  const int64_t nv = n - n % 8, nseg = (nv + kShSeg - 1) / kShSeg;
+  const auto load = [&](float (&r)[kShLoads], int64_t sg) {
+    const int64_t base = sg * kShSeg, left = nv - base;
+    const int bytes = left <= 0 ? 0 : (int)(min(left, (int64_t)kShSeg) * 4);
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xt + (left <= 0 ? 0 : base)), 0, bytes,
+                                                      0x00020000);
+#pragma unroll
+    for (int i = 0; i < kShLoads; ++i)
+      r[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (i * kShThreads + tid) * 4, 0, 0));
+  };
+  // element i * 512 + tid of a segment is step s = 64 i + tid / 8 of chain tid % 8: lane s / 16, slot s % 16
+  float* const stg = buf + (tid & 7) * kShRow + (tid >> 7) * kShLS + ((tid >> 3) & 15);
+  const auto stage = [&](const float (&r)[kShLoads]) {
+#pragma unroll
+    for (int i = 0; i < kShLoads; ++i) stg[i * 4 * kShLS] = r[i];
+  };
+  const float4* const rd = reinterpret_cast<const float4*>(buf + wave * kShRow + lane * kShLS);
+  float acc = 0.0f;
+  const auto run = [&]() {
+    float v[kLane];
+#pragma unroll
+    for (int q = 0; q < kLane / 4; ++q) {
+      const float4 f = rd[q];
+      v[4 * q] = f.x;
+      v[4 * q + 1] = f.y;
+      v[4 * q + 2] = f.z;
+      v[4 * q + 3] = f.w;
+    }
+    acc = short_segment(v, acc, lane);
+  };
+  float ra[kShLoads], rb[kShLoads];
+  load(ra, 0);
+  load(rb, 1);
+  for (int64_t sg = 0; sg < nseg; sg += 2) {  // block-uniform control flow throughout
+    stage(ra);
+    __syncthreads();
+    load(ra, sg + 2);
+    run();
+    __syncthreads();
+    if (sg + 1 >= nseg) break;
+    stage(rb);
+    __syncthreads();
+    load(rb, sg + 3);
+    run();
+    __syncthreads();
+  }
+  if (lane == 0) s_acc[wave] = acc;
+  __syncthreads();
+  if (tid == 0) {  // lane sum left to right, the n % 8 tail, sqrt
+    float b = s_acc[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) b = b + s_acc[j];
+    b = tail32(xt, nv, n, b);
+    const float r = (float)__builtin_sqrt((double)b);  // correctly rounded fp32 sqrt
+    if (norms32) norms32[ch.tensor] = r;
+    if (norms64) norms64[ch.tensor] = r;
+  }
+}
+
 __device__ __forceinline__ float rn_bf16(float f) {
   const uint32_t b = __float_as_uint(f);
   if (__builtin_isnan(f)) return __uint_as_float((b | 0x00400000u) & 0xffff0000u);
@@ -1429,9 +1646,13 @@ int launch(const void* x, const adfl_slq_chunk* chunks, int64_t nchunks, int64_t
            int threads, void* scratch, double* n64, float* n32, hipStream_t st) {
   const Scratch s = carve(scratch, nchunks, ntensors);
   const bool any_long = (kinds & ADFL_TORCH_NORM_LONG) != 0, any_short = (kinds & ADFL_TORCH_NORM_SHORT) != 0;
-  const bool walk = DT == ADFL_DTYPE_F32;  // fp32 short tensors: the in-order walker
+  const bool walk = DT == ADFL_DTYPE_F32;  // fp32 short tensors: k_tn_short (ADFL_TN_WALKER builds: the in-order walker)
   if (walk && any_short) {
+#ifdef ADFL_TN_WALKER
     if (int e = adfl_tn::launch_walk((const float*)x, chunks, nchunks, n32, n64, st)) return e;
+#else
+    k_tn_short<<<(unsigned)nchunks, kShThreads, 0, st>>>((const float*)x, chunks, kShortMax, n64, n32);
+#endif
   }
   if (any_long) {
     k_tn_sums<DT><<<(unsigned)nchunks, 256, 0, st>>>(x, chunks, nchunks, threads, s.tfirst, s.S);
@@ -1472,7 +1693,9 @@ int adfl_torch_norms(int32_t dtype, const void* d_x, const adfl_slq_chunk* d_chu
   if (nchunks < 0 || ntensors < 0 || (nchunks > 0 && (!d_x || !d_chunks || !d_scratch)) || (!d_norms64 && !d_norms32))
     return ADFL_E_ARG;
   if (nchunks == 0) return ADFL_OK;
-  if (ntensors <= 0 || ntensors > nchunks || threads < 1 || threads > adfl_tnx::kMaxChains) return ADFL_E_ARG;
+  // threads only shapes fp16's split (at most kMaxChains pieces per tensor); the other dtypes ignore it
+  if (ntensors <= 0 || ntensors > nchunks || threads < 1 || (dtype == ADFL_DTYPE_F16 && threads > adfl_tnx::kMaxChains))
+    return ADFL_E_ARG;
   if (scratch_bytes < adfl_tnx::scratch_bytes(nchunks, ntensors)) return ADFL_E_WORKSPACE;
   if (((uintptr_t)d_scratch & 255) != 0) return ADFL_E_ALIGN;
   if (kinds == 0) kinds = ADFL_TORCH_NORM_SHORT | ADFL_TORCH_NORM_LONG;

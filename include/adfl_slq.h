@@ -27,7 +27,9 @@
 extern "C" {
 #endif
 
-#define ADFL_SLQ_ABI_VERSION 1
+/* 2 (round 5): adfl_stoch_norms_torch, adfl_stoch_torch_norm_scratch_bytes and adfl_stoch_torch_norm_walk_max
+ * were replaced by adfl_torch_norms (adfl_stoch.h); the absmax / quantize kernels took new arguments. */
+#define ADFL_SLQ_ABI_VERSION 2
 
 enum {
   ADFL_OK = 0,

@@ -65,7 +65,8 @@ enum { ADFL_TORCH_NORM_SHORT = 1, ADFL_TORCH_NORM_LONG = 2 };
  * Orders restated: oracle/slq_oracle.c
  * oracle_torch_l2_norm{,_bf16,_f16,_f64}.
  *   threads: torch.get_num_threads() of the process whose norm is reproduced (fp16 tensors of >= 32768
- *            elements are summed in that many contiguous pieces; 1..512; unused for the other dtypes).
+ *            elements are summed in min(threads, ceil(n / 32768)) contiguous pieces: 1..512 for fp16 buckets;
+ *            any value >= 1 for the other dtypes, which do not use it).
  *   kinds:   which tensors the bucket holds, so launches with nothing to do are skipped:
  *            ADFL_TORCH_NORM_SHORT (some of at most adfl_torch_norm_short_max() elements: fp32 ones are walked
  *            in order, one block per tensor) | ADFL_TORCH_NORM_LONG (some longer: the phased path); 0 = both.

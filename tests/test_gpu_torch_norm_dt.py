@@ -151,6 +151,21 @@ def test_reference_norms_one_big_tensor(dt, n):
     assert _same(n64.item(), want), (dt, n, n64.item(), want)
 
 
+@pytest.mark.parametrize("dt", list(DTYPES))
+def test_reference_norms_many_threads(dt):
+    """A host with more than 512 torch threads: fp32 / bf16 / fp64 do not depend on the count, fp16's split
+    is at most ceil(n / 32768) pieces whatever it is (stoch.reference_norms clamps it)."""
+    dtype = DTYPES[dt]
+    rng = np.random.default_rng(5)
+    xs = [_data("grad", n, rng, dtype) for n in (5, 32769, 100003, 300007)]
+    lay, flat = _bucket(xs, 1, dtype)
+    n64, _ = stoch.reference_norms(flat, lay, threads=1024)
+    got = n64.cpu().numpy()
+    for i, x in enumerate(xs):
+        # torch itself at 16 threads splits these fp16 tensors as it would at 1024 (at most 10 pieces)
+        assert _same(got[i], _torch_norm(x, 16)), (dt, i)
+
+
 def test_reference_norms_abi_rejects_bad_arguments():
     from adfl_amd import _lib
     L = _lib.load()
@@ -171,7 +186,11 @@ def test_reference_norms_abi_rejects_bad_arguments():
     assert call(args(x=None)) == -1
     assert call(args(dtype=7)) == -1
     assert call(args(threads=0)) == -1
-    assert call(args(threads=513)) == -1
+    assert call(args(threads=513)) == 0            # fp32 does not use threads
+    assert call(args(threads=1 << 20)) == 0
+    x16 = torch.zeros(100, dtype=torch.float16, device=DEV)
+    assert call(args(dtype=1, x=x16.data_ptr(), threads=512)) == 0
+    assert call(args(dtype=1, x=x16.data_ptr(), threads=513)) == -1   # fp16: at most 512 pieces
     assert call(args(n64=None)) == -1
     assert call(args(nt=2)) == -1
     assert L.adfl_torch_norm_short_max() == 1 << 16

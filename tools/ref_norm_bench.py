@@ -14,7 +14,9 @@ import torch
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "ad-federatedlearning_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
 from adfl_amd import ops, stoch  # noqa: E402
+import recipes  # noqa: E402
 
 DT = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16, "f64": torch.float64}
 
@@ -23,6 +25,7 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--reps", type=int, default=21)
     p.add_argument("--dtypes", default="f32,bf16,f16,f64")
+    p.add_argument("--cfgs", default="", help="comma-separated substrings of the config names to run (default all)")
     a = p.parse_args()
     dev = torch.device("cuda", 0)
     junk = torch.empty(128 << 20, device=dev)
@@ -31,7 +34,8 @@ def main():
     logu = np.exp(rng.uniform(np.log(64), np.log(2_400_000), 256)).astype(np.int64)
     cfgs = {"C2 flat 2^28": ops.BucketLayout([1 << 28], align=1),
             "C3 equal 256": ops.BucketLayout([base + (1 if i < rem else 0) for i in range(256)], align=1),
-            "C3 log-uniform 256": ops.BucketLayout(logu.tolist(), align=64)}
+            "C3 log-uniform 256": ops.BucketLayout(recipes.bucket_sizes("loguniform"), align=64),
+            "C3 log-uniform unscaled 256": ops.BucketLayout(logu.tolist(), align=64)}
     g = torch.Generator(device=dev).manual_seed(0)
 
     def timed(fn):
@@ -48,6 +52,8 @@ def main():
 
     res = {}
     for name, lay in cfgs.items():
+        if a.cfgs and not any(k in name for k in a.cfgs.split(",")):
+            continue
         x32 = torch.randn(lay.total, device=dev, generator=g) * 1e-3
         for dn in a.dtypes.split(","):
             x = x32.to(DT[dn])
