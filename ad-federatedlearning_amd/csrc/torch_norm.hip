@@ -61,8 +61,25 @@ __device__ unsigned long long g_tn_stats[8][10];  // window descents, tiles in d
 // detail, cycles waiting for segment loads, cycles in window descents, window scans, exact-path segment rounds,
 // cycles in segments
 #define TN_STAT(i, v) do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_tn_stats[blockIdx.y & 7][i], (unsigned long long)(v)); } while (0)
+// k_tn_short's counters, summed over its waves: segments, rounds, exact-map rounds, lanes run with fma, G + 1
+// continuations that finished the segment, cycles in short_segment, cycles per wave, (unused), waves, cycles in
+// stage() (its load waits included), cycles in barriers
+__device__ unsigned long long g_sh_stats[11];
+// one block's timeline (tools: stats builds): per wave, up to 48 (event, clock) pairs — 1 stage start, 2 stage
+// end, 3 run start (LDS read issued), 4 segment start (values in registers), 5 run end, 6 barrier end
+__device__ long long g_sh_tl[8][48][2];
+__device__ int g_sh_tln[8];
+#define SH_TL(e) do { if (shn < 48) { if ((threadIdx.x & 63) == 0) { s_tl[threadIdx.x >> 6][shn][0] = (e); \
+  s_tl[threadIdx.x >> 6][shn][1] = clock64(); } ++shn; } } while (0)  // in LDS: no vmcnt waits added
+#define SH_STAT(i, v) do { shs[i] += (unsigned long long)(v); } while (0)  // per wave, added once at the end
+#define SH_ARG , unsigned long long (&shs)[11]
+#define SH_PASS , shs
 #else
 #define TN_STAT(i, v) do { } while (0)
+#define SH_STAT(i, v) do { } while (0)
+#define SH_ARG
+#define SH_PASS
+#define SH_TL(e) do { } while (0)
 #endif
 
 constexpr int kChunk = ADFL_SLQ_CHUNK_ELEMS;      // 8192: a tile is a chunk's steps of one chain
@@ -1327,17 +1344,88 @@ __device__ __forceinline__ float wave_incl_f(float v) {
 __device__ __forceinline__ float lane_f(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
+__device__ __forceinline__ double lane_d(double v, int l) {  // readlane, so the compiler sees a uniform value
+  const long long b = __double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
 
-// One segment of a chain (lane l: steps 16 l .. 16 l + 15, in order) from the exact accumulator acc (wave-uniform).
-__device__ __forceinline__ float short_segment(const float (&v)[kLane], float acc, int lane) {
-  uint32_t lsb = 0;  // max over the lane's steps of E + ctz(mantissa | 2^23)
+// A lane's 16 steps on binade G (B = 2^G, or +0 for G = -126; h = u / 2): the sum of their increments and whether
+// one of them may be a tie. A tie x^2 / u = f + 1/2 puts B + x^2 exactly halfway between two neighbours, so the
+// residual x^2 - k of the increment k = fma(x, x, B) - B is exactly +-u / 2, which fma(x, x, -k) returns exactly;
+// any other residual rounds to +-u / 2 only within 2^-24 of it (rare false positives, which only cost time). On
+// G = -126, u / 2 = 2^-150 is not a float: there a residual of 0 from a nonzero x flags the lane instead (exact
+// squares on the subnormal grid included).
+template <bool SUB>
+__device__ __forceinline__ float lane_incs(const float (&v)[kLane], float B, float h, unsigned long long& ties) {
+  float Ka = 0.0f, Kb = 0.0f;
+  unsigned long long t = 0ull;  // wave masks straight from the compares (as bools the compiler rebuilt bit vectors)
+#pragma unroll
+  for (int i = 0; i < kLane; i += 2) {
+    const float ka = __builtin_fmaf(v[i], v[i], B) - B, kb = __builtin_fmaf(v[i + 1], v[i + 1], B) - B;
+    Ka += ka;
+    Kb += kb;
+    const float ra = __builtin_fmaf(-v[i], v[i], ka), rb = __builtin_fmaf(-v[i + 1], v[i + 1], kb);  // k - x^2
+    if constexpr (SUB) {  // h is +0 here, from an empty asm: these compares stay in this (rare) branch
+      t |= __ballot(ra == 0.0f && v[i] != h) | __ballot(rb == 0.0f && v[i + 1] != h);
+    } else {
+      t |= __ballot(__builtin_fabsf(ra) == h) | __ballot(__builtin_fabsf(rb) == h);
+    }
+  }
+  ties = t;
+  return Ka + Kb;
+}
+__device__ __forceinline__ float lane_incs(const float (&v)[kLane], int G, unsigned long long& ties) {
+  if (G > -126) return lane_incs<false>(v, pow2f(G), pow2f(G - 24), ties);
+  float z = 0.0f;  // through an empty asm: the loop-invariant subnormal-grid sums must not be hoisted out of the
+  __asm__ volatile("" : "+v"(z));  // round loop into every segment
+  return lane_incs<true>(v, z, z, ties);
+}
+
+// The lane that leaves the binade runs its steps with fma from its exact start a = acc + (the lanes before it).
+__device__ __forceinline__ float lane_fma(const float (&v)[kLane], float a, int lane, int ls) {
+  if (lane == ls) {
+#pragma unroll
+    for (int i = 0; i < kLane; ++i) a = __builtin_fmaf(v[i], v[i], a);
+  }
+  return lane_f(a, ls);
+}
+
+// A round by exact maps (what each lane's run adds to an even / an odd A), for a wave where a tie is possible.
+// Kept out of the fast path: the steps pass an empty asm first, so the fp64 conversions are not hoisted into
+// every round. Returns the new acc; `start` moves past the lane that left the binade (64: segment done).
+__device__ float short_exact_round(const float (&v)[kLane], float acc, int G, int lane, int& start) {
+  float w[kLane];
 #pragma unroll
   for (int i = 0; i < kLane; ++i) {
-    const uint32_t b = __float_as_uint(v[i]);
-    lsb = max(lsb, ((b >> 23) & 0xffu) + (uint32_t)__builtin_ctz(b | 0x800000u));
+    w[i] = v[i];
+    __asm__ volatile("" : "+v"(w[i]));
   }
+  Map m = lane_map_exact<false>(w, G);
+  if (lane < start) m = Map{0.0, 0.0};
+  const double Al = apply(wave_excl(m, lane), a_of(acc));
+  const double out = apply(m, Al);
+  const unsigned long long ball = __ballot(lane >= start && !(out < Acc<false>::kTop));
+  if (ball == 0ull) {
+    start = 64;
+    return rebuild<false>(lane_d(out, 63), G);
+  }
+  const int ls = __builtin_ctzll(ball);
+  start = ls + 1;
+  return lane_fma(w, rebuild<false>(lane_d(Al, ls), G), lane, ls);
+}
+
+// One segment of a chain (lane l: steps 16 l .. 16 l + 15, in order) from the exact accumulator acc (wave-uniform).
+__device__ __forceinline__ float short_segment(const float (&v)[kLane], float acc, int lane SH_ARG) {
   int start = 0;
-  for (;;) {
+  SH_STAT(0, 1);
+  if (acc == 0.0f) {  // a chain's start: every nonzero step crosses, so lane 0 runs its steps with fma at once
+    acc = lane_fma(v, 0.0f, lane, 0);
+    start = 1;
+  }
+  while (start < 64) {
+    SH_STAT(1, 1);
     if (!__builtin_isfinite(acc)) {  // inf stays inf unless a NaN follows; NaN stays NaN
       bool nan = false;
 #pragma unroll
@@ -1346,81 +1434,71 @@ __device__ __forceinline__ float short_segment(const float (&v)[kLane], float ac
       return acc;
     }
     const int G = grid_of(acc);
-    if (__ballot(lane >= start && 2 * (int)lsb >= G + 276) == 0ull) {
-      const float B0 = G > -126 ? pow2f(G) : 0.0f, B1 = pow2f(G + 1);  // B1 = +inf above the top binade
-      float K0a = 0.0f, K0b = 0.0f, K1a = 0.0f, K1b = 0.0f;
-#pragma unroll
-      for (int i = 0; i < kLane; i += 2) {
-        K0a += __builtin_fmaf(v[i], v[i], B0) - B0;
-        K1a += __builtin_fmaf(v[i], v[i], B1) - B1;
-        K0b += __builtin_fmaf(v[i + 1], v[i + 1], B0) - B0;
-        K1b += __builtin_fmaf(v[i + 1], v[i + 1], B1) - B1;
-      }
-      const float K0 = lane >= start ? K0a + K0b : 0.0f, K1 = K1a + K1b;
-      const float I0 = wave_incl_f(K0), out = acc + I0;
-      const unsigned long long ball = __ballot(lane >= start && !(out < B1));
-      if (ball == 0ull) return lane_f(out, 63);
-      // the first lane that leaves G runs its steps with fma from its exact start
-      const int ls = __builtin_ctzll(ball);
-      float a = acc + (ls > 0 ? lane_f(I0, ls - 1) : 0.0f);
-      if (lane == ls) {
-#pragma unroll
-        for (int i = 0; i < kLane; ++i) a = __builtin_fmaf(v[i], v[i], a);
-      }
-      acc = lane_f(a, ls);
-      start = ls + 1;
-      if (start == 64) return acc;
-      // on from lane ls + 1 with the increments on G + 1, if that is where acc went
-      if (__builtin_isfinite(acc) && grid_of(acc) == G + 1) {
-        const float I1 = wave_incl_f(lane > ls ? K1 : 0.0f), out1 = acc + I1;
-        const unsigned long long b1 = __ballot(lane > ls && !(out1 < pow2f(G + 2)));
-        if (b1 == 0ull) return lane_f(out1, 63);
-        const int l1 = __builtin_ctzll(b1);
-        a = acc + lane_f(I1, l1 - 1);
-        if (lane == l1) {
-#pragma unroll
-          for (int i = 0; i < kLane; ++i) a = __builtin_fmaf(v[i], v[i], a);
-        }
-        acc = lane_f(a, l1);
-        start = l1 + 1;
-        if (start == 64) return acc;
-      }
+    unsigned long long ties;
+    float K0 = lane_incs(v, G, ties);
+    if (ties >> start) {  // a possible tie in a lane still to run
+      SH_STAT(2, 1);
+      acc = short_exact_round(v, acc, G, lane, start);
       continue;
     }
-    // a tie is possible in some lane: this round by exact maps (what the run adds to an even / an odd A)
-    Map m = lane_map_exact<false>(v, G);
-    if (lane < start) m = Map{0.0, 0.0};
-    const double A = a_of(acc);
-    const double Al = apply(wave_excl(m, lane), A);
-    const double out = apply(m, Al);
-    const unsigned long long ball = __ballot(lane >= start && !(out < Acc<false>::kTop));
-    if (ball == 0ull) return rebuild<false>(__shfl(out, 63, 64), G);
+    if (lane < start) K0 = 0.0f;
+    const float top = pow2f(G + 1);  // +inf above the top binade
+    const float I0 = wave_incl_f(K0), out = acc + I0;
+    const unsigned long long ball = __ballot(lane >= start && !(out < top));
+    if (ball == 0ull) return lane_f(out, 63);
     const int ls = __builtin_ctzll(ball);
-    float a = rebuild<false>(__shfl(Al, ls, 64), G);
-    if (lane == ls) {
-#pragma unroll
-      for (int i = 0; i < kLane; ++i) a = __builtin_fmaf(v[i], v[i], a);
-    }
-    acc = lane_f(a, ls);
+    SH_STAT(3, 1);
+    acc = lane_fma(v, acc + (ls > 0 ? lane_f(I0, ls - 1) : 0.0f), lane, ls);
     start = ls + 1;
-    if (start == 64) return acc;
+    if (start == 64 || !__builtin_isfinite(acc) || grid_of(acc) != G + 1) continue;
+    // on from lane ls + 1 on G + 1, where acc went (the usual crossing): one more scan, no new round
+    unsigned long long ties1;
+    const float K1 = lane_incs<false>(v, top, pow2f(G - 23), ties1);
+    if (ties1 >> start) continue;  // start = ls + 1 < 64
+    const float I1 = wave_incl_f(lane > ls ? K1 : 0.0f), out1 = acc + I1;
+    const unsigned long long b1 = __ballot(lane > ls && !(out1 < pow2f(G + 2)));
+    if (b1 == 0ull) {
+      SH_STAT(4, 1);
+      return lane_f(out1, 63);
+    }
+    const int l1 = __builtin_ctzll(b1);
+    SH_STAT(3, 1);
+    acc = lane_fma(v, acc + lane_f(I1, l1 - 1), lane, l1);
+    start = l1 + 1;
   }
+  return acc;
 }
 
-// One block per tensor of at most max_n elements (grid: the chunk table; blocks not at a tensor's first chunk
-// return). The 8 waves stream the tensor in 8192-element segments: every thread loads 16 consecutive-lane
+// Every tensor's first chunk, tfirst[tensor] (the short kernel's work list: one block per tensor, so its blocks
+// spread over the XCDs, where one block per chunk put every working block of an equal layout with an even chunk
+// count per tensor on the same XCDs).
+__global__ __launch_bounds__(256) void k_tn_tfirst(const adfl_slq_chunk* __restrict__ chunks, int64_t nchunks,
+                                                   int* __restrict__ tfirst) {
+  const int64_t ci = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (ci >= nchunks) return;
+  const adfl_slq_chunk ch = chunks[ci];
+  if (ch.first_chunk == ci) tfirst[ch.tensor] = (int)ci;
+}
+
+// One block per tensor (blockIdx.x = tensor, its first chunk from tfirst) of at most max_n elements (longer
+// ones return). The 8 waves stream the tensor in 8192-element segments: every thread loads 16 consecutive-lane
 // dwords per segment (buffer loads whose range ends at the chain steps' end, so the rest reads as +0, which no
 // chain notices), two segments ahead in registers, and stages them chain-major into LDS; wave c then reads its
 // lanes' 16-step runs of chain c (4 ds_read_b128 each) and advances the chain by short_segment. Then the lane
 // sum left to right, the n % 8 tail and the sqrt, as k_norm_walk does.
 __global__ __launch_bounds__(kShThreads) void k_tn_short(const float* __restrict__ x, const adfl_slq_chunk* __restrict__ chunks,
-                                                         int64_t max_n, double* __restrict__ norms64,
-                                                         float* __restrict__ norms32) {
-  __shared__ __attribute__((aligned(16))) float buf[8 * kShRow];
+                                                         const int* __restrict__ tfirst, int64_t max_n,
+                                                         double* __restrict__ norms64, float* __restrict__ norms32) {
+  __shared__ __attribute__((aligned(16))) float buf[2][8 * kShRow];
   __shared__ float s_acc[8];
-  const adfl_slq_chunk ch = chunks[blockIdx.x];
-  if ((int64_t)blockIdx.x != ch.first_chunk) return;
-  const int64_t n = (int64_t)(ch.nchunks - 1) * ADFL_SLQ_CHUNK_ELEMS + chunks[blockIdx.x + ch.nchunks - 1].len;
+#ifdef ADFL_TN_STATS
+  unsigned long long shs[11] = {};
+  __shared__ long long s_tl[8][48][2];
+  int shn = 0;
+#endif
+  const int ci = tfirst[blockIdx.x];
+  const adfl_slq_chunk ch = chunks[ci];
+  const int64_t n = (int64_t)(ch.nchunks - 1) * ADFL_SLQ_CHUNK_ELEMS + chunks[ci + ch.nchunks - 1].len;
   if (n > max_n) return;
   const float* xt = x + ch.start;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1444,14 +1522,34 @@ __global__ __launch_bounds__(kShThreads) void k_tn_short(const float* __restrict
       r[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (i * kShThreads + tid) * 4, 0, 0));
   };
   // element i * 512 + tid of a segment is step s = 64 i + tid / 8 of chain tid % 8: lane s / 16, slot s % 16
-  float* const stg = buf + (tid & 7) * kShRow + (tid >> 7) * kShLS + ((tid >> 3) & 15);
-  const auto stage = [&](const float (&r)[kShLoads]) {
+  const int stg = (tid & 7) * kShRow + (tid >> 7) * kShLS + ((tid >> 3) & 15);
+  const auto stage = [&](const float (&r)[kShLoads], float* b) {
+    SH_TL(1);
+#ifdef ADFL_TN_STATS
+    const long long c0 = clock64();
+#endif
 #pragma unroll
-    for (int i = 0; i < kShLoads; ++i) stg[i * 4 * kShLS] = r[i];
+    for (int i = 0; i < kShLoads; ++i) b[stg + i * 4 * kShLS] = r[i];
+#ifdef ADFL_TN_STATS
+    SH_STAT(9, clock64() - c0);
+#endif
+    SH_TL(2);
   };
-  const float4* const rd = reinterpret_cast<const float4*>(buf + wave * kShRow + lane * kShLS);
+  const auto sync = [&]() {
+#ifdef ADFL_TN_STATS
+    const long long c0 = clock64();
+#endif
+    __syncthreads();
+#ifdef ADFL_TN_STATS
+    SH_STAT(10, clock64() - c0);
+#endif
+    SH_TL(6);
+  };
+  const int rdo = wave * kShRow + lane * kShLS;
   float acc = 0.0f;
-  const auto run = [&]() {
+  const auto run = [&](const float* b) {
+    SH_TL(3);
+    const float4* const rd = reinterpret_cast<const float4*>(b + rdo);
     float v[kLane];
 #pragma unroll
     for (int q = 0; q < kLane / 4; ++q) {
@@ -1461,24 +1559,57 @@ __global__ __launch_bounds__(kShThreads) void k_tn_short(const float* __restrict
       v[4 * q + 2] = f.z;
       v[4 * q + 3] = f.w;
     }
-    acc = short_segment(v, acc, lane);
+#ifdef ADFL_TN_STATS
+    __asm__ volatile("" ::"v"(v[0]), "v"(v[15]));  // the LDS reads have landed
+    SH_TL(4);
+    const long long r0 = clock64();
+#endif
+    acc = short_segment(v, acc, lane SH_PASS);
+#ifdef ADFL_TN_STATS
+    SH_STAT(5, clock64() - r0);
+    SH_TL(5);
+#endif
   };
+#ifdef ADFL_TN_STATS
+  const long long k0 = clock64();
+  SH_STAT(8, 1);
+#endif
+  // Two LDS buffers, two register sets: segment j is walked in one buffer, then segment j + 1 staged into the
+  // other, while segment j + 2 loads; one barrier per segment. Each register set is staged in the
+  // straight-line code that issued the other set's loads after it (never across the loop header), so the wait
+  // before a stage covers its own loads only (vmcnt(16)): staged at the loop head, the compiler's merged state
+  // at the header waited for both sets (vmcnt(0)) and every other segment exposed the full load latency.
   float ra[kShLoads], rb[kShLoads];
+  SH_TL(0);
   load(ra, 0);
+  __builtin_amdgcn_sched_barrier(0);
   load(rb, 1);
-  for (int64_t sg = 0; sg < nseg; sg += 2) {  // block-uniform control flow throughout
-    stage(ra);
-    __syncthreads();
+  stage(ra, buf[0]);
+  sync();
+  for (int64_t sg = 0;; sg += 2) {  // block-uniform control flow throughout
     load(ra, sg + 2);
-    run();
-    __syncthreads();
+    run(buf[0]);
+    stage(rb, buf[1]);  // after the walk: its loads have had the walk's time to land (past the end: zeros)
+    sync();
     if (sg + 1 >= nseg) break;
-    stage(rb);
-    __syncthreads();
     load(rb, sg + 3);
-    run();
-    __syncthreads();
+    run(buf[1]);
+    stage(ra, buf[0]);
+    sync();
+    if (sg + 2 >= nseg) break;
   }
+#ifdef ADFL_TN_STATS
+  SH_STAT(6, clock64() - k0);
+  if (lane == 0)
+    for (int i = 0; i < 11; ++i) atomicAdd(&g_sh_stats[i], shs[i]);
+  if (blockIdx.x == 7 && lane == 0) {
+    for (int k = 0; k < min(shn, 48); ++k) {
+      g_sh_tl[wave][k][0] = s_tl[wave][k][0];
+      g_sh_tl[wave][k][1] = s_tl[wave][k][1];
+    }
+    g_sh_tln[wave] = min(shn, 48);
+  }
+#endif
   if (lane == 0) s_acc[wave] = acc;
   __syncthreads();
   if (tid == 0) {  // lane sum left to right, the n % 8 tail, sqrt
@@ -1491,6 +1622,24 @@ __global__ __launch_bounds__(kShThreads) void k_tn_short(const float* __restrict
     if (norms64) norms64[ch.tensor] = r;
   }
 }
+
+#ifdef ADFL_TN_STATS
+__global__ void k_sh_stats_print() {
+  const unsigned long long* g = g_sh_stats;
+  const double w = g[8] ? (double)g[8] : 1.0;
+  printf("sh_stats waves %llu per wave: segments %.2f rounds %.2f exact-map rounds %.2f fma lanes %.2f g+1 finishes %.2f "
+         "cycles in segments %.0f in stage %.0f in barriers %.0f total %.0f\n", g[8], g[0] / w, g[1] / w, g[2] / w,
+         g[3] / w, g[4] / w, g[5] / w, g[9] / w, g[10] / w, g[6] / w);
+  for (int i = 0; i < 11; ++i) g_sh_stats[i] = 0;
+  const long long t0 = g_sh_tl[0][0][1];
+  for (int w = 0; w < 8; ++w) {
+    printf("sh_tl wave %d:", w);
+    for (int k = 0; k < g_sh_tln[w]; ++k) printf(" %lld@%lld", g_sh_tl[w][k][0], g_sh_tl[w][k][1] - t0);
+    printf("\n");
+    g_sh_tln[w] = 0;
+  }
+}
+#endif
 
 __device__ __forceinline__ float rn_bf16(float f) {
   const uint32_t b = __float_as_uint(f);
@@ -1651,7 +1800,11 @@ int launch(const void* x, const adfl_slq_chunk* chunks, int64_t nchunks, int64_t
 #ifdef ADFL_TN_WALKER
     if (int e = adfl_tn::launch_walk((const float*)x, chunks, nchunks, n32, n64, st)) return e;
 #else
-    k_tn_short<<<(unsigned)nchunks, kShThreads, 0, st>>>((const float*)x, chunks, kShortMax, n64, n32);
+    k_tn_tfirst<<<(unsigned)((nchunks + 255) / 256), 256, 0, st>>>(chunks, nchunks, s.tfirst);
+    k_tn_short<<<(unsigned)ntensors, kShThreads, 0, st>>>((const float*)x, chunks, s.tfirst, kShortMax, n64, n32);
+#ifdef ADFL_TN_STATS
+    k_sh_stats_print<<<1, 1, 0, st>>>();
+#endif
 #endif
   }
   if (any_long) {

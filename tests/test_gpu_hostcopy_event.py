@@ -21,40 +21,71 @@ DEV = torch.device("cuda", 0)
 
 @pytest.mark.parametrize("pieces", [1, 7])
 def test_copy_waits_for_the_event(pieces):
-    n = 1 << 26                                 # a 256 MiB D2H: milliseconds on the link, so it is still running
+    """Deterministic gate (verdict r05 item 4): a device-side sleep ahead of the D2H holds it back for tens of
+    milliseconds, so the event is pending at submit unless the D2H's enqueue itself blocked — which the
+    failure message then shows (enqueue and submit times)."""
+    n = 1 << 24                                 # a 64 MiB D2H
     pinned = torch.full((n,), -1.0).pin_memory()
     dst = torch.zeros(n)
     src_dev = torch.arange(n, dtype=torch.float32, device=DEV)
     stream = torch.cuda.current_stream(DEV)
-    scratch = torch.empty(n).pin_memory()
     cuts = np.linspace(0, n, pieces + 1).astype(np.int64)
     es = 4
     d = [dst.data_ptr() + int(a) * es for a in cuts[:-1]]
     s = [pinned.data_ptr() + int(a) * es for a in cuts[:-1]]
     b = [int(c - a) * es for a, c in zip(cuts[:-1], cuts[1:])]
-    # ~40 ms of D2H queued in front of the one the copy waits for; on a loaded host this thread can be
-    # descheduled for longer than that, so the gate grows until the event is still pending at submit
-    for gate in (8, 32, 128):
-        torch.cuda.synchronize()
-        for _ in range(gate):
-            scratch.copy_(src_dev, non_blocking=True)
-        pinned.copy_(src_dev, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record(stream)
-        t0 = time.perf_counter()
-        job = hostcopy.submit_pieces(d, s, b, event=ev, keep=(pinned, dst))
-        submit_s = time.perf_counter() - t0
-        if not ev.query():                      # the D2H is still behind the others: the copy must wait
-            break
-        job.wait()
-        pinned.fill_(-1.0)
-        dst.zero_()
-    else:
-        pytest.skip("every gate's D2H had landed before submit returned (host descheduled): not exercised")
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    torch.cuda._sleep(100_000_000)              # ~50 ms of device time before the D2H can start
+    pinned.copy_(src_dev, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record(stream)
+    enqueue_s = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    job = hostcopy.submit_pieces(d, s, b, event=ev, keep=(pinned, dst))
+    submit_s = time.perf_counter() - t1
+    pending = not ev.query()
     job.wait()
+    assert pending, (f"the D2H landed before submit returned: sleep + D2H enqueue took {enqueue_s * 1e3:.1f} ms, "
+                     f"submit {submit_s * 1e3:.1f} ms")
     assert ev.query()
     assert torch.equal(dst, src_dev.cpu()), "copied before the event completed"
     assert submit_s < 0.05                      # submit does not block on the event
+
+
+@pytest.mark.parametrize("how", ["torch_copy", "adfl_stage_d2h"])
+def test_d2h_enqueue_does_not_block(how):
+    """The range-pipelined host paths overlap each range's D2H with the host's work: the D2H of pinned staging
+    must enqueue without waiting for the device. Behind ~50 ms of device sleep, enqueueing a 64 MiB D2H (torch's
+    non_blocking copy_ into pinned memory, or the paths' own adfl_stage_d2h) returns in well under that."""
+    import ctypes
+    from adfl_amd import _lib
+    n = 1 << 24
+    pinned = torch.empty(n).pin_memory()
+    src_dev = torch.randn(n, device=DEV)
+    stream = torch.cuda.current_stream(DEV)
+    side = torch.cuda.Stream(DEV)
+    torch.cuda.synchronize()
+    torch.cuda._sleep(100_000_000)
+    t0 = time.perf_counter()
+    if how == "torch_copy":
+        pinned.copy_(src_dev, non_blocking=True)
+    else:
+        lib = _lib.load()
+        evs = (ctypes.c_void_p * 2)()
+        assert lib.adfl_stage_events_create(2, evs) == 0
+        src, dst, nb = (ctypes.c_void_p * 1)(src_dev.data_ptr()), (ctypes.c_void_p * 1)(pinned.data_ptr()), \
+            (ctypes.c_int64 * 1)(4 * n)
+        assert lib.adfl_stage_d2h(src, dst, nb, 1, stream.cuda_stream, side.cuda_stream, evs[0], evs[1]) == 0
+    enqueue_s = time.perf_counter() - t0
+    landed_early = torch.cuda.Event()
+    landed_early.record(side if how != "torch_copy" else stream)
+    pending = not landed_early.query()
+    torch.cuda.synchronize()
+    if how != "torch_copy":
+        lib.adfl_stage_events_destroy(evs, 2)
+    assert torch.equal(pinned, src_dev.cpu())
+    assert enqueue_s < 0.02 and pending, f"{how}: D2H enqueue took {enqueue_s * 1e3:.1f} ms behind 50 ms of sleep"
 
 
 def test_many_jobs_behind_one_event_keep_order():
