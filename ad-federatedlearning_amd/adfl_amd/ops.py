@@ -282,6 +282,7 @@ class BucketLayout:
         self.max_tensor_chunks = int(max(c.nchunks for c in self.chunks))
         self._device_chunks = {}
         self._device_work = {}
+        self._device_tfirst = {}
 
     def device_chunks(self, device: torch.device) -> torch.Tensor:
         key = (device.type, device.index)
@@ -290,6 +291,21 @@ class BucketLayout:
             host = torch.frombuffer(bytearray(bytes(self.chunks)), dtype=torch.uint8)
             t = host.to(device)
             self._device_chunks[key] = t
+        return t
+
+    def device_tfirst(self, device: torch.device) -> torch.Tensor:
+        """Every tensor's first chunk (int32, one per tensor) on `device`: the short-tensor norm kernel's work
+        list (adfl_torch_norms_work), cached like the chunk table."""
+        key = (device.type, device.index)
+        t = self._device_tfirst.get(key)
+        if t is None:
+            rec = np.frombuffer(bytes(self.chunks), dtype=np.dtype([("start", "<i8"), ("len", "<i4"), ("tensor", "<i4"),
+                                                                    ("first_chunk", "<i4"), ("nchunks", "<i4")]))
+            first = np.nonzero(rec["first_chunk"] == np.arange(self.nchunks))[0]
+            tf = np.zeros(self.ntensors, dtype=np.int32)
+            tf[rec["tensor"][first]] = first
+            t = torch.from_numpy(tf).to(device)
+            self._device_tfirst[key] = t
         return t
 
     def device_work(self, device: torch.device) -> torch.Tensor:

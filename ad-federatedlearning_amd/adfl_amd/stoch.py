@@ -152,10 +152,10 @@ def reference_norms(flat: torch.Tensor, layout: BucketLayout, *, threads: Option
     kinds = (1 if min(layout.sizes) <= short_max else 0) | (2 if max(layout.sizes) > short_max else 0)
     need = L.adfl_torch_norm_scratch_bytes(layout.nchunks, layout.ntensors)
     scratch = torch.empty(need, dtype=torch.uint8, device=dev)  # stream-ordered: no initialisation needed
-    check(L.adfl_torch_norms(_REF_NORM_DTYPES[flat.dtype], flat.data_ptr(), layout.device_chunks(dev).data_ptr(),
-                             layout.nchunks, layout.ntensors, kinds, threads, scratch.data_ptr(), need,
-                             out64.data_ptr() if out64 is not None else None,
-                             out32.data_ptr() if out32 is not None else None, _stream(dev)))
+    check(L.adfl_torch_norms_work(_REF_NORM_DTYPES[flat.dtype], flat.data_ptr(), layout.device_chunks(dev).data_ptr(),
+                                  layout.nchunks, layout.device_tfirst(dev).data_ptr(), layout.ntensors, kinds, threads,
+                                  scratch.data_ptr(), need, out64.data_ptr() if out64 is not None else None,
+                                  out32.data_ptr() if out32 is not None else None, _stream(dev)))
     return out64, out32
 
 

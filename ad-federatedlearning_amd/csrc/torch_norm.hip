@@ -1309,7 +1309,6 @@ constexpr int kShThreads = 512;                 // wave c runs chain c
 constexpr int kShSeg = 8 * kSeg;                // 8192 elements: 1024 steps of each chain
 constexpr int kShLS = 20;                       // floats per lane's run in LDS (16 steps + 4: 16-byte reads)
 constexpr int kShRow = 64 * kShLS + 8;          // floats per chain (+8: chains c and c + 4 alone share banks)
-constexpr int kShLoads = kShSeg / kShThreads;   // 16 loads per thread per segment
 
 // the n % 8 tail after the lane sum (and the whole sum below 8 elements) as torch's compiled scalar loop runs
 // it: 4 rounded squares added in order when there are 4 or more, the rest with fma (as k_norm_walk's tail_sum)
@@ -1416,21 +1415,31 @@ __device__ float short_exact_round(const float (&v)[kLane], float acc, int G, in
   return lane_fma(w, rebuild<false>(lane_d(Al, ls), G), lane, ls);
 }
 
+constexpr int kSerial = 16;  // lanes run in order at a chain's start (short_segment)
+
 // One segment of a chain (lane l: steps 16 l .. 16 l + 15, in order) from the exact accumulator acc (wave-uniform).
 __device__ __forceinline__ float short_segment(const float (&v)[kLane], float acc, int lane SH_ARG) {
   int start = 0;
   SH_STAT(0, 1);
-  if (acc == 0.0f) {  // a chain's start: every nonzero step crosses, so lane 0 runs its steps with fma at once
-    acc = lane_fma(v, 0.0f, lane, 0);
-    start = 1;
+  if (acc == 0.0f) {
+    // A chain's start: the accumulator doubles about every time the step count does (binade crossings at lanes 1,
+    // 3, 7, 15, 31, 63), and a crossing round costs about as much as 256 dependent fma: the first kSerial lanes
+    // run their steps with fma one after the other.
+#pragma unroll 1
+    for (int l = 0; l < kSerial; ++l) acc = lane_fma(v, acc, lane, l);
+    start = kSerial;
   }
   while (start < 64) {
     SH_STAT(1, 1);
     if (!__builtin_isfinite(acc)) {  // inf stays inf unless a NaN follows; NaN stays NaN
-      bool nan = false;
+      unsigned long long nan = 0ull;
 #pragma unroll
-      for (int i = 0; i < kLane; ++i) nan |= __builtin_isnan(v[i]);
-      if (__ballot(nan && lane >= start)) acc = __builtin_nanf("");
+      for (int i = 0; i < kLane; ++i) {  // through an empty asm: not hoisted into every segment
+        float w = v[i];
+        __asm__ volatile("" : "+v"(w));
+        nan |= __ballot(__builtin_isnan(w));
+      }
+      if (nan >> start) acc = __builtin_nanf("");
       return acc;
     }
     const int G = grid_of(acc);
@@ -1489,7 +1498,7 @@ __global__ __launch_bounds__(256) void k_tn_tfirst(const adfl_slq_chunk* __restr
 __global__ __launch_bounds__(kShThreads) void k_tn_short(const float* __restrict__ x, const adfl_slq_chunk* __restrict__ chunks,
                                                          const int* __restrict__ tfirst, int64_t max_n,
                                                          double* __restrict__ norms64, float* __restrict__ norms32) {
-  __shared__ __attribute__((aligned(16))) float buf[2][8 * kShRow];
+  __shared__ __attribute__((aligned(16))) float buf[2 * 8 * kShRow + 4];  // + the spare slot (off[] < 0 elements)
   __shared__ float s_acc[8];
 #ifdef ADFL_TN_STATS
   unsigned long long shs[11] = {};
@@ -1511,25 +1520,79 @@ __global__ __launch_bounds__(kShThreads) void k_tn_short(const float* __restrict
     }
     return;
   }
-  const int64_t nv = n - n % 8, nseg = (nv + kShSeg - 1) / kShSeg;
-  const auto load = [&](float (&r)[kShLoads], int64_t sg) {
-    const int64_t base = sg * kShSeg, left = nv - base;
-    const int bytes = left <= 0 ? 0 : (int)(min(left, (int64_t)kShSeg) * 4);
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xt + (left <= 0 ? 0 : base)), 0, bytes,
-                                                      0x00020000);
-#pragma unroll
-    for (int i = 0; i < kShLoads; ++i)
-      r[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (i * kShThreads + tid) * 4, 0, 0));
+  const int64_t nv = n - n % 8;
+  const int nseg = (int)((nv + kShSeg - 1) / kShSeg);
+  // 16-byte loads from the aligned block below the tensor's start: "aligned block" j is the 2048 vectors from
+  // vector 2048 j there (elements 8192 j - delta .. 8192 j + 8191 - delta of the tensor; delta = its start's
+  // offset in a vector, 0..3), plus vector 2048 (j + 1), whose first delta elements end segment j (every thread
+  // loads it, so every wave counts the same loads; thread 0 stages it). Segment j = elements 8192 j ..
+  // 8192 j + 8191 is thus staged from block j alone. Vectors holding an element of the tensor lie inside its
+  // allocation, so the buffer range ends at the last such vector; elements past the chain steps' end are zeroed.
+  const int delta = (int)(((uintptr_t)xt & 15) >> 2);
+  const float* const xa = xt - delta;
+  const int64_t vbytes = ((nv + delta) * 4 + 15) & ~(int64_t)15;
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  typedef float f3v __attribute__((ext_vector_type(3)));
+  struct Blk {
+    f4v r[4];
+    f3v t;  // 3 dwords: a dead 4th component's register was reused at once, which waited for the load (WAW)
   };
-  // element i * 512 + tid of a segment is step s = 64 i + tid / 8 of chain tid % 8: lane s / 16, slot s % 16
-  const int stg = (tid & 7) * kShRow + (tid >> 7) * kShLS + ((tid >> 3) & 15);
-  const auto stage = [&](const float (&r)[kShLoads], float* b) {
+  const auto load = [&](Blk& k, int j) {
+    const int64_t base = (int64_t)j * (kShSeg * 4), left = vbytes - base;
+    const int bytes = left <= 0 ? 0 : (int)min(left, (int64_t)kShSeg * 4 + 16);
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xa) + (left <= 0 ? 0 : (int64_t)j * kShSeg), 0,
+                                                      bytes, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      k.r[i] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, (i * kShThreads + tid) * 16, 0, 0));
+    k.t = __builtin_bit_cast(f3v, __builtin_amdgcn_raw_buffer_load_b96(rs, kShSeg * 4, 0, 0));
+  };
+  // Thread tid's element p of vector i is e = 8192 j + 2048 i + 4 tid + p - delta: chain e % 8, step e / 8 of the
+  // segment (lane step / 16, slot step % 16); i adds 256 steps (16 lanes). Thread 0's first delta elements of
+  // vector 0 belong to segment j - 1 (staged from its own extra vector): they go to a spare slot past the rows.
+  constexpr int kBufF = 8 * kShRow;
+  int off[4], off0[4];  // vector i > 0: off + 16 lanes per i; vector 0: off0 (the spare slot for e < 0)
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int e = 4 * tid + p - delta;  // e < 0 (thread 0): chain e & 7 at "lane -1, slot 15", so that vector i > 0
+    off[p] = (e & 7) * kShRow + (e >> 7) * kShLS + ((e >> 3) & 15);  // lands on step 256 i - 1
+    off0[p] = e < 0 ? 2 * kBufF + p : off[p];
+  }
+  const int nvi = (int)nv;
+  const auto stage = [&](const Blk& k, int j) {
     SH_TL(1);
 #ifdef ADFL_TN_STATS
     const long long c0 = clock64();
 #endif
+    float* const bj = buf + (j & 1) * kBufF;
+    const int e0 = j * kShSeg - delta + 4 * tid;                    // this thread's element of vector 0
+    const bool last = j * kShSeg - delta + kShSeg + 4 > nvi;         // the block holds the steps' end
+    const auto put = [&](const f4v (&r)[4]) {
 #pragma unroll
-    for (int i = 0; i < kShLoads; ++i) b[stg + i * 4 * kShLS] = r[i];
+      for (int p = 0; p < 4; ++p) (off0[p] < 2 * kBufF ? bj : buf)[off0[p]] = r[0][p];
+#pragma unroll
+      for (int i = 1; i < 4; ++i)
+#pragma unroll
+        for (int p = 0; p < 4; ++p) bj[off[p] + 16 * kShLS * i] = r[i][p];
+    };
+    if (!last) {
+      put(k.r);
+    } else {  // the block holding the steps' end: zeros past it
+      f4v z[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int p = 0; p < 4; ++p) z[i][p] = e0 + 2048 * i + p < nvi ? k.r[i][p] : 0.0f;
+      put(z);
+    }
+    if (tid == 0) {  // the extra vector's first delta elements: chains 8 - delta + p of step 1023
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        if (p < delta) {
+          const float val = (j + 1) * kShSeg - delta + p < nvi ? k.t[p] : 0.0f;
+          bj[(8 - delta + p) * kShRow + 63 * kShLS + 15] = val;
+        }
+    }
 #ifdef ADFL_TN_STATS
     SH_STAT(9, clock64() - c0);
 #endif
@@ -1547,9 +1610,9 @@ __global__ __launch_bounds__(kShThreads) void k_tn_short(const float* __restrict
   };
   const int rdo = wave * kShRow + lane * kShLS;
   float acc = 0.0f;
-  const auto run = [&](const float* b) {
+  const auto run = [&](int j) {
     SH_TL(3);
-    const float4* const rd = reinterpret_cast<const float4*>(b + rdo);
+    const float4* const rd = reinterpret_cast<const float4*>(buf + (j & 1) * kBufF + rdo);
     float v[kLane];
 #pragma unroll
     for (int q = 0; q < kLane / 4; ++q) {
@@ -1574,29 +1637,29 @@ __global__ __launch_bounds__(kShThreads) void k_tn_short(const float* __restrict
   const long long k0 = clock64();
   SH_STAT(8, 1);
 #endif
-  // Two LDS buffers, two register sets: segment j is walked in one buffer, then segment j + 1 staged into the
-  // other, while segment j + 2 loads; one barrier per segment. Each register set is staged in the
-  // straight-line code that issued the other set's loads after it (never across the loop header), so the wait
-  // before a stage covers its own loads only (vmcnt(16)): staged at the loop head, the compiler's merged state
-  // at the header waited for both sets (vmcnt(0)) and every other segment exposed the full load latency.
-  float ra[kShLoads], rb[kShLoads];
+  // Two LDS buffers (segment j in buffer j % 2), two register sets: segment j is walked in one buffer, then
+  // segment j + 1 staged into the other, while block j + 2 loads; one barrier per segment. Each set is staged in
+  // the half after the one that loaded it, after the other set's loads were issued, so the wait before a stage
+  // covers its own loads only (vmcnt(5)). (Staged at the loop head, or before the other set's loads, the
+  // compiler's merged state at the loop header waited for both sets, and the loads' latency was exposed.)
+  Blk ra, rb;
   SH_TL(0);
   load(ra, 0);
   __builtin_amdgcn_sched_barrier(0);
   load(rb, 1);
-  stage(ra, buf[0]);
+  stage(ra, 0);
   sync();
-  for (int64_t sg = 0;; sg += 2) {  // block-uniform control flow throughout
-    load(ra, sg + 2);
-    run(buf[0]);
-    stage(rb, buf[1]);  // after the walk: its loads have had the walk's time to land (past the end: zeros)
+  for (int j = 0;; j += 2) {  // block-uniform control flow throughout
+    load(ra, j + 2);
+    run(j);
+    stage(rb, j + 1);  // after the walk: its loads have had the walk's time to land (past the end: zeros)
     sync();
-    if (sg + 1 >= nseg) break;
-    load(rb, sg + 3);
-    run(buf[1]);
-    stage(ra, buf[0]);
+    if (j + 1 >= nseg) break;
+    load(rb, j + 3);
+    run(j + 1);
+    stage(ra, j + 2);
     sync();
-    if (sg + 2 >= nseg) break;
+    if (j + 2 >= nseg) break;
   }
 #ifdef ADFL_TN_STATS
   SH_STAT(6, clock64() - k0);
@@ -1791,8 +1854,8 @@ inline Scratch carve(void* p, int64_t nchunks, int64_t ntensors) {
 }
 
 template <int DT>
-int launch(const void* x, const adfl_slq_chunk* chunks, int64_t nchunks, int64_t ntensors, int32_t kinds,
-           int threads, void* scratch, double* n64, float* n32, hipStream_t st) {
+int launch(const void* x, const adfl_slq_chunk* chunks, int64_t nchunks, const int32_t* tfirst, int64_t ntensors,
+           int32_t kinds, int threads, void* scratch, double* n64, float* n32, hipStream_t st) {
   const Scratch s = carve(scratch, nchunks, ntensors);
   const bool any_long = (kinds & ADFL_TORCH_NORM_LONG) != 0, any_short = (kinds & ADFL_TORCH_NORM_SHORT) != 0;
   const bool walk = DT == ADFL_DTYPE_F32;  // fp32 short tensors: k_tn_short (ADFL_TN_WALKER builds: the in-order walker)
@@ -1800,8 +1863,11 @@ int launch(const void* x, const adfl_slq_chunk* chunks, int64_t nchunks, int64_t
 #ifdef ADFL_TN_WALKER
     if (int e = adfl_tn::launch_walk((const float*)x, chunks, nchunks, n32, n64, st)) return e;
 #else
-    k_tn_tfirst<<<(unsigned)((nchunks + 255) / 256), 256, 0, st>>>(chunks, nchunks, s.tfirst);
-    k_tn_short<<<(unsigned)ntensors, kShThreads, 0, st>>>((const float*)x, chunks, s.tfirst, kShortMax, n64, n32);
+    if (!tfirst) {  // no list from the caller: one launch builds it
+      k_tn_tfirst<<<(unsigned)((nchunks + 255) / 256), 256, 0, st>>>(chunks, nchunks, s.tfirst);
+      tfirst = s.tfirst;
+    }
+    k_tn_short<<<(unsigned)ntensors, kShThreads, 0, st>>>((const float*)x, chunks, tfirst, kShortMax, n64, n32);
 #ifdef ADFL_TN_STATS
     k_sh_stats_print<<<1, 1, 0, st>>>();
 #endif
@@ -1840,9 +1906,9 @@ int64_t adfl_torch_norm_scratch_bytes(int64_t nchunks, int64_t ntensors) {
 
 int64_t adfl_torch_norm_short_max(void) { return adfl_tnx::kShortMax; }
 
-int adfl_torch_norms(int32_t dtype, const void* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, int64_t ntensors,
-                     int32_t kinds, int32_t threads, void* d_scratch, int64_t scratch_bytes, double* d_norms64,
-                     float* d_norms32, void* stream) {
+int adfl_torch_norms_work(int32_t dtype, const void* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks,
+                          const int32_t* d_tfirst, int64_t ntensors, int32_t kinds, int32_t threads, void* d_scratch,
+                          int64_t scratch_bytes, double* d_norms64, float* d_norms32, void* stream) {
   if (nchunks < 0 || ntensors < 0 || (nchunks > 0 && (!d_x || !d_chunks || !d_scratch)) || (!d_norms64 && !d_norms32))
     return ADFL_E_ARG;
   if (nchunks == 0) return ADFL_OK;
@@ -1855,16 +1921,23 @@ int adfl_torch_norms(int32_t dtype, const void* d_x, const adfl_slq_chunk* d_chu
   hipStream_t st = (hipStream_t)stream;
   switch (dtype) {
     case ADFL_DTYPE_F32:
-      return adfl_tnx::launch<ADFL_DTYPE_F32>(d_x, d_chunks, nchunks, ntensors, kinds, threads, d_scratch, d_norms64, d_norms32, st);
+      return adfl_tnx::launch<ADFL_DTYPE_F32>(d_x, d_chunks, nchunks, d_tfirst, ntensors, kinds, threads, d_scratch, d_norms64, d_norms32, st);
     case ADFL_DTYPE_BF16:
-      return adfl_tnx::launch<ADFL_DTYPE_BF16>(d_x, d_chunks, nchunks, ntensors, kinds, threads, d_scratch, d_norms64, d_norms32, st);
+      return adfl_tnx::launch<ADFL_DTYPE_BF16>(d_x, d_chunks, nchunks, d_tfirst, ntensors, kinds, threads, d_scratch, d_norms64, d_norms32, st);
     case ADFL_DTYPE_F16:
-      return adfl_tnx::launch<ADFL_DTYPE_F16>(d_x, d_chunks, nchunks, ntensors, kinds, threads, d_scratch, d_norms64, d_norms32, st);
+      return adfl_tnx::launch<ADFL_DTYPE_F16>(d_x, d_chunks, nchunks, d_tfirst, ntensors, kinds, threads, d_scratch, d_norms64, d_norms32, st);
     case ADFL_DTYPE_F64:
-      return adfl_tnx::launch<ADFL_DTYPE_F64>(d_x, d_chunks, nchunks, ntensors, kinds, threads, d_scratch, d_norms64, d_norms32, st);
+      return adfl_tnx::launch<ADFL_DTYPE_F64>(d_x, d_chunks, nchunks, d_tfirst, ntensors, kinds, threads, d_scratch, d_norms64, d_norms32, st);
     default:
       return ADFL_E_ARG;
   }
+}
+
+int adfl_torch_norms(int32_t dtype, const void* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks, int64_t ntensors,
+                     int32_t kinds, int32_t threads, void* d_scratch, int64_t scratch_bytes, double* d_norms64,
+                     float* d_norms32, void* stream) {
+  return adfl_torch_norms_work(dtype, d_x, d_chunks, nchunks, nullptr, ntensors, kinds, threads, d_scratch,
+                               scratch_bytes, d_norms64, d_norms32, stream);
 }
 
 }  // extern "C"

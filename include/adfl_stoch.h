@@ -79,6 +79,11 @@ int64_t adfl_torch_norm_short_max(void);
 int adfl_torch_norms(int32_t dtype, const void* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks,
                      int64_t ntensors, int32_t kinds, int32_t threads, void* d_scratch, int64_t scratch_bytes,
                      double* d_norms64, float* d_norms32, void* stream);
+/* The same with the caller's list of every tensor's first chunk (d_tfirst[t], ntensors int32 on the device; the
+ * host has it from building the chunk table), which saves the launch that builds it; NULL: adfl_torch_norms. */
+int adfl_torch_norms_work(int32_t dtype, const void* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks,
+                          const int32_t* d_tfirst, int64_t ntensors, int32_t kinds, int32_t threads, void* d_scratch,
+                          int64_t scratch_bytes, double* d_norms64, float* d_norms32, void* stream);
 
 /* QSGD / RQSGD level quantization given per-tensor norms (quant.py:230-238 and :371-379), levels =
  * 2^bits - 1: scaled = fl(fl(levels*|x|) / norm); l = floor(scaled); q = u8(l + (u < scaled - l));
