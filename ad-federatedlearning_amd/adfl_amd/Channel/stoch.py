@@ -231,7 +231,8 @@ def _encode_stoch_host(tensors, names, hptrs: np.ndarray, lay, st, codec: str, b
     planes queued on the pool behind the event — so the planes' D2H overlaps the next ranges' H2D. The H2D
     runs on a stream of its own, enqueued as soon as each gather lands, so a range's kernels and outputs
     (longer on the calling thread than a range's copy) never hold the link back."""
-    _host_heap(lay)
+    with _ph("enc.heap"):
+        _host_heap(lay)
     dev = st.device
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
@@ -251,8 +252,9 @@ def _encode_stoch_host(tensors, names, hptrs: np.ndarray, lay, st, codec: str, b
     d2h_h = st.d2h_stream().cuda_stream
     hx, dx = host.data_ptr(), x_dev.data_ptr()
     ld, lh, gd, gh = levels.data_ptr(), lv_host.data_ptr(), signs.data_ptr(), sg_host.data_ptr()
-    jobs = [hostcopy.submit_pieces(*_range_copies(hptrs, lay, hx, 4, lo, hi, to_bucket=True), keep=host)
-            for lo, hi in ranges]
+    with _ph("enc.gather_submit"):
+        jobs = [hostcopy.submit_pieces(*_range_copies(hptrs, lay, hx, 4, lo, hi, to_bucket=True), keep=host)
+                for lo, hi in ranges]
     ends = lay.offsets + lay.sizes
     code = 1 if codec == "cnat" else 0
     lv_parts: List[torch.Tensor] = []
@@ -272,54 +274,64 @@ def _encode_stoch_host(tensors, names, hptrs: np.ndarray, lay, st, codec: str, b
             # every range whose gather has landed goes to the link at once, on its own stream (the compute
             # stream waits only for the ranges its kernels read); block on a gather only when range r's is next
             while r_h2d < len(ranges) and (r_h2d == r or jobs[r_h2d].done()):
-                jobs[r_h2d].wait()
-                a, b = ranges[r_h2d]
-                check(lib.adfl_stage_encode_range(hx, dx, a, b, None, None, 0, 0, 0, None, None, None, 0, 0, h2d_h,
-                                                  None, None, None))
-                landed[r_h2d].record(h2d)
+                with _ph("enc.gather_wait"):
+                    jobs[r_h2d].wait()
+                with _ph("enc.h2d_launch"):
+                    a, b = ranges[r_h2d]
+                    check(lib.adfl_stage_encode_range(hx, dx, a, b, None, None, 0, 0, 0, None, None, None, 0, 0, h2d_h,
+                                                      None, None, None))
+                    landed[r_h2d].record(h2d)
                 r_h2d += 1
             done = int(np.searchsorted(ends, hi, side="right"))   # tensors whose every byte is staged
             if done <= made:
                 continue
-            stream.wait_event(landed[r])
-            _codec_encode(codec, x_dev, _sub_layout(lay, made, done), bits, uniforms, seed, levels, signs,
-                          norms[made:], mins[made:] if mins is not None else None, ws, torch_norm)
-            e0, e1 = int(lay.offsets[made]), int(ends[done - 1])
-            src, dst, nb = copies
-            src[0], src[1], dst[0], dst[1] = ld + e0, gd + e0, lh + e0, gh + e0
-            nb[0] = nb[1] = e1 - e0
-            check(lib.adfl_stage_d2h(src, dst, nb, 2, sh, d2h_h, evs[2 * r], evs[2 * r + 1]))
-            lts, lpt = th.empty_like_dtype(tensors[made:done], code)
-            gts, gpt = th.empty_like_dtype(tensors[made:done], 1)
-            lv_parts.extend(lts)
-            sg_parts.extend(gts)
-            lv_ptrs[made:done] = lpt.numpy().view(np.uint64)
-            sg_ptrs[made:done] = gpt.numpy().view(np.uint64)
-            a = _range_copies(lv_ptrs, lay, lh, 1, e0, e1, to_bucket=False)
-            b = _range_copies(sg_ptrs, lay, gh, 1, e0, e1, to_bucket=False)
-            scatters.append(hostcopy.submit_pieces(*(np.concatenate([u, v]) for u, v in zip(a, b)), stream=True,
-                                                   event=evs[2 * r + 1], keep=(lv_host, sg_host)))
-            for k in range(made, done):   # the caller's payload objects, their scales filled in at the end
-                emit(k, lv_parts[k], sg_parts[k])
-            made = done
-            idle()
+            with _ph("enc.kernel_launch"):
+                stream.wait_event(landed[r])
+                _codec_encode(codec, x_dev, _sub_layout(lay, made, done), bits, uniforms, seed, levels, signs,
+                              norms[made:], mins[made:] if mins is not None else None, ws, torch_norm)
+                e0, e1 = int(lay.offsets[made]), int(ends[done - 1])
+                src, dst, nb = copies
+                src[0], src[1], dst[0], dst[1] = ld + e0, gd + e0, lh + e0, gh + e0
+                nb[0] = nb[1] = e1 - e0
+                check(lib.adfl_stage_d2h(src, dst, nb, 2, sh, d2h_h, evs[2 * r], evs[2 * r + 1]))
+            with _ph("enc.outputs"):
+                lts, lpt = th.empty_like_dtype(tensors[made:done], code)
+                gts, gpt = th.empty_like_dtype(tensors[made:done], 1)
+                lv_parts.extend(lts)
+                sg_parts.extend(gts)
+                lv_ptrs[made:done] = lpt.numpy().view(np.uint64)
+                sg_ptrs[made:done] = gpt.numpy().view(np.uint64)
+            with _ph("enc.scatter_submit"):
+                a = _range_copies(lv_ptrs, lay, lh, 1, e0, e1, to_bucket=False)
+                b = _range_copies(sg_ptrs, lay, gh, 1, e0, e1, to_bucket=False)
+                scatters.append(hostcopy.submit_pieces(*(np.concatenate([u, v]) for u, v in zip(a, b)), stream=True,
+                                                       event=evs[2 * r + 1], keep=(lv_host, sg_host)))
+            with _ph("enc.passthrough"):
+                for k in range(made, done):   # the caller's payload objects, their scales filled in at the end
+                    emit(k, lv_parts[k], sg_parts[k])
+                made = done
+                idle()
         nm_host[:lay.ntensors].copy_(norms, non_blocking=True)
         if mins is not None:
             nm_host[lay.ntensors:].copy_(mins, non_blocking=True)
         norms_ready = torch.cuda.Event()
         norms_ready.record(stream)
-        while idle():   # the caller's remaining objects, while the last copies land
-            pass
+        with _ph("enc.passthrough"):
+            while idle():   # the caller's remaining objects, while the last copies land
+                pass
     except BaseException:
         _drain(h2d, stream, st.d2h_stream())
         raise
     finally:
         for j in jobs:
             j.wait()
-        for j in scatters:
-            j.wait()
-    norms_ready.synchronize()
-    return _payloads(names, lv_parts, sg_parts, nm_host.tolist(), lay.ntensors, codec)
+        with _ph("enc.scatter_wait"):
+            for j in scatters:
+                j.wait()
+    with _ph("enc.norms_wait"):
+        norms_ready.synchronize()
+    with _ph("enc.payloads"):
+        return _payloads(names, lv_parts, sg_parts, nm_host.tolist(), lay.ntensors, codec)
 
 
 # Philox block-counter base of each dtype bucket: one seed serves an fp32 bucket and every fp16 / bf16 / fp64
@@ -428,7 +440,8 @@ def _decode_stoch_host(st, items, datas, numel: torch.Tensor, lptrs: np.ndarray,
     created (one native call) and their scatter queued on the pool behind the event. Bit-identical to the
     one-launch decode (each chunk is decoded by the same kernel)."""
     lay = st.layout(tuple(numel.tolist()))
-    _host_heap(lay)
+    with _ph("dec.heap"):
+        _host_heap(lay)
     dev = st.device
     sh = torch.cuda.current_stream(dev).cuda_stream
     lib = _lib.load()
@@ -454,11 +467,12 @@ def _decode_stoch_host(st, items, datas, numel: torch.Tensor, lptrs: np.ndarray,
     od, oh = out_dev.data_ptr(), out_host.data_ptr()
     cid = _CODEC_ID[codec]
     jobs = []
-    for lo, hi in ranges:
-        a = _range_copies(lptrs, lay, lh, 1, lo, hi, to_bucket=True)
-        b = _range_copies(sptrs, lay, gh, 1, lo, hi, to_bucket=True)
-        jobs.append(hostcopy.submit_pieces(*(np.concatenate([x, y]) for x, y in zip(a, b)),
-                                           keep=(lv_host, sg_host)))
+    with _ph("dec.gather_submit"):
+        for lo, hi in ranges:
+            a = _range_copies(lptrs, lay, lh, 1, lo, hi, to_bucket=True)
+            b = _range_copies(sptrs, lay, gh, 1, lo, hi, to_bucket=True)
+            jobs.append(hostcopy.submit_pieces(*(np.concatenate([x, y]) for x, y in zip(a, b)),
+                                               keep=(lv_host, sg_host)))
     offs = lay.offsets
     outs: List[torch.Tensor] = []
     out_ptrs = np.zeros(lay.ntensors, dtype=np.uint64)
@@ -466,36 +480,41 @@ def _decode_stoch_host(st, items, datas, numel: torch.Tensor, lptrs: np.ndarray,
     c_made = t_made = 0
     try:
         for r, ((lo, hi), job) in enumerate(zip(ranges, jobs)):
-            job.wait()
-            c_end = int(np.searchsorted(cm.end, hi, side="right"))   # chunks whose every byte is staged
-            if c_end <= c_made:
-                check(lib.adfl_stage_stoch_decode_range(cid, bits, lh, ld, gh, gd, lo, hi, chunks_ptr, 0, 0, nd, md, od,
-                                                        oh, 0, 0, sh, d2h_h, evs[2 * r], evs[2 * r + 1]))
-                continue
-            e0, e1 = int(cm.start[c_made]), int(cm.end[c_end - 1])
-            check(lib.adfl_stage_stoch_decode_range(cid, bits, lh, ld, gh, gd, lo, hi, chunks_ptr, c_made,
-                                                    c_end - c_made, nd, md, od, oh, e0, e1, sh, d2h_h, evs[2 * r],
-                                                    evs[2 * r + 1]))
-            c_made = c_end
-            t_end = int(np.searchsorted(offs, e1, side="left"))    # tensors starting below e1
-            if t_end > t_made:
-                ts, pt = th.empty_f32_like(datas[t_made:t_end])
-                outs.extend(ts)
-                out_ptrs[t_made:t_end] = pt.numpy().view(np.uint64)
-                for j in np.nonzero(lay.sizes[t_made:t_end] * 4 >= (4 << 20))[0].tolist():
-                    hostcopy.advise_huge([ts[j]])
-                t_made = t_end
-            scatters.append(hostcopy.submit_pieces(
-                *_range_copies(out_ptrs, lay, oh, 4, e0, e1, to_bucket=False),
-                stream=True, event=evs[2 * r + 1], keep=out_host))
+            with _ph("dec.gather_wait"):
+                job.wait()
+            with _ph("dec.kernel_launch"):
+                c_end = int(np.searchsorted(cm.end, hi, side="right"))   # chunks whose every byte is staged
+                if c_end <= c_made:
+                    check(lib.adfl_stage_stoch_decode_range(cid, bits, lh, ld, gh, gd, lo, hi, chunks_ptr, 0, 0, nd, md,
+                                                            od, oh, 0, 0, sh, d2h_h, evs[2 * r], evs[2 * r + 1]))
+                    continue
+                e0, e1 = int(cm.start[c_made]), int(cm.end[c_end - 1])
+                check(lib.adfl_stage_stoch_decode_range(cid, bits, lh, ld, gh, gd, lo, hi, chunks_ptr, c_made,
+                                                        c_end - c_made, nd, md, od, oh, e0, e1, sh, d2h_h, evs[2 * r],
+                                                        evs[2 * r + 1]))
+                c_made = c_end
+            with _ph("out.alloc"):
+                t_end = int(np.searchsorted(offs, e1, side="left"))    # tensors starting below e1
+                if t_end > t_made:
+                    ts, pt = th.empty_f32_like(datas[t_made:t_end])
+                    outs.extend(ts)
+                    out_ptrs[t_made:t_end] = pt.numpy().view(np.uint64)
+                    for j in np.nonzero(lay.sizes[t_made:t_end] * 4 >= (4 << 20))[0].tolist():
+                        hostcopy.advise_huge([ts[j]])
+                    t_made = t_end
+            with _ph("out.scatter_submit"):
+                scatters.append(hostcopy.submit_pieces(
+                    *_range_copies(out_ptrs, lay, oh, 4, e0, e1, to_bucket=False),
+                    stream=True, event=evs[2 * r + 1], keep=out_host))
     except BaseException:
         _drain(torch.cuda.current_stream(dev), st.d2h_stream())
         raise
     finally:
         for j in jobs:
             j.wait()
-        for j in scatters:
-            j.wait()
+        with _ph("out.scatter_wait"):
+            for j in scatters:
+                j.wait()
     return outs
 
 

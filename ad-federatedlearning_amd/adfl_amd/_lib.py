@@ -74,6 +74,7 @@ SIGNATURES = {
     "adfl_stoch_norms_batched": (INT, [P, P, I64, INT, P, I64, P, P, P]),
     "adfl_torch_norm_scratch_bytes": (I64, [I64, I64]),
     "adfl_torch_norm_short_max": (I64, []),
+    "adfl_torch_norm_short_max_dt": (I64, [I32]),
     "adfl_torch_norms": (INT, [I32, P, P, I64, I64, I32, I32, P, I64, P, P, P]),
     "adfl_torch_norms_work": (INT, [I32, P, P, I64, P, I64, I32, I32, P, I64, P, P, P]),
     "adfl_qerror_ref_plan": (I64, [P, I32, I32, P, I64]),

@@ -148,7 +148,7 @@ def reference_norms(flat: torch.Tensor, layout: BucketLayout, *, threads: Option
         threads = min(threads, max(1, -(-int(max(layout.sizes)) // 32768)))
     elif threads < 1:
         raise ValueError("adfl_amd.stoch: threads must be >= 1")
-    short_max = L.adfl_torch_norm_short_max()
+    short_max = L.adfl_torch_norm_short_max_dt(_REF_NORM_DTYPES[flat.dtype])
     kinds = (1 if min(layout.sizes) <= short_max else 0) | (2 if max(layout.sizes) > short_max else 0)
     need = L.adfl_torch_norm_scratch_bytes(layout.nchunks, layout.ntensors)
     scratch = torch.empty(need, dtype=torch.uint8, device=dev)  # stream-ordered: no initialisation needed

@@ -86,7 +86,12 @@ constexpr int kChunk = ADFL_SLQ_CHUNK_ELEMS;      // 8192: a tile is a chunk's s
 constexpr int kSlots = 8;                         // records per chunk: one per chain (strided) or piece (fp16)
 constexpr int kLane = 16;                         // steps per lane
 constexpr int kSeg = 64 * kLane;                  // 1024 steps: one wave's segment
-constexpr int64_t kShortMax = 1 << 16;            // tensors up to this size skip phases A-C
+constexpr int64_t kShortMax = 1 << 16;            // tensors up to this size skip phases A-C (fp16 / bf16 / fp64)
+#ifndef ADFL_TN_SHORT_MAX_F32
+#define ADFL_TN_SHORT_MAX_F32 (1 << 19)
+#endif
+constexpr int64_t kShortMaxF32 = ADFL_TN_SHORT_MAX_F32;  // fp32: k_tn_short (one block per tensor) up to this size
+template <int DT> constexpr int64_t short_max() { return DT == ADFL_DTYPE_F32 ? kShortMaxF32 : kShortMax; }
 constexpr int64_t kGrain = 32768;                 // at::internal::GRAIN_SIZE
 constexpr int kMaxChains = 512;                   // fp16: chains (torch threads) per tensor the combine holds
 constexpr double kMagic = 6755399441055744.0;     // 1.5 * 2^52: (v + kMagic) - kMagic = rint(v), 0 <= v < 2^51
@@ -482,7 +487,7 @@ __global__ __launch_bounds__(256) void k_tn_sums(const void* __restrict__ x, con
   const int ci = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const Tensor T = tensor_of(chunks, ci, nall);
   if (tid == 0 && ci == T.first) tfirst[T.tensor] = ci;
-  if (T.n <= kShortMax) return;
+  if (T.n <= short_max<DT>()) return;
   const Split sp = split_of(T.n, threads);
   const ChunkGeo G = geo_of<DT>(T, ci, sp);
   if (G.lim <= 0) return;  // a chunk of tail elements only: no tile
@@ -556,7 +561,7 @@ __global__ __launch_bounds__(256) void k_tn_winsums(const adfl_slq_chunk* __rest
   using D = Dt<DT>;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const Tensor T = tensor_of(chunks, tfirst[blockIdx.x], nall);
-  if (T.n <= kShortMax) return;
+  if (T.n <= short_max<DT>()) return;
   const Split sp = split_of(T.n, threads);
   const int nchains = D::kContig ? (int)sp.nt : D::NC;
   const int wstride = gridDim.z * 4;
@@ -586,7 +591,7 @@ __global__ __launch_bounds__(256) void k_tn_grids(const adfl_slq_chunk* __restri
   using D = Dt<DT>;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const Tensor T = tensor_of(chunks, tfirst[blockIdx.x], nall);
-  if (T.n <= kShortMax) return;
+  if (T.n <= short_max<DT>()) return;
   const Split sp = split_of(T.n, threads);
   const int nchains = D::kContig ? (int)sp.nt : D::NC;
   const int wstride = gridDim.z * 4;
@@ -652,7 +657,7 @@ __global__ __launch_bounds__(256) void k_tn_maps(const void* __restrict__ x, con
   __shared__ int s_g[8], s_slow, s_fl[4][8];
   const int ci = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const Tensor T = tensor_of(chunks, ci, nall);
-  if (T.n <= kShortMax) return;
+  if (T.n <= short_max<DT>()) return;
   const Split sp = split_of(T.n, threads);
   const ChunkGeo G = geo_of<DT>(T, ci, sp);
   if (G.lim <= 0) return;
@@ -931,7 +936,7 @@ __global__ __launch_bounds__(256) void k_tn_windows(const adfl_slq_chunk* __rest
   constexpr bool W = D::kWide;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const Tensor T = tensor_of(chunks, tfirst[blockIdx.x], nall);
-  if (T.n <= kShortMax) return;
+  if (T.n <= short_max<DT>()) return;
   const Split sp = split_of(T.n, threads);
   const int nchains = D::kContig ? (int)sp.nt : D::NC;
   const int wstride = gridDim.z * 4;
@@ -1306,9 +1311,14 @@ __device__ typename Acc<Dt<DT>::kWide>::T resolve_chain(const void* x, const Ten
 // exact map path (lane_map_exact, fp64). Measured against k_norm_walk (the chains run in order) and torch
 // itself: tests/test_gpu_torch_norm.py, test_gpu_torch_norm_dt.py.
 constexpr int kShThreads = 512;                 // wave c runs chain c
-constexpr int kShSeg = 8 * kSeg;                // 8192 elements: 1024 steps of each chain
-constexpr int kShLS = 20;                       // floats per lane's run in LDS (16 steps + 4: 16-byte reads)
+#ifndef ADFL_TN_SHORT_SL
+#define ADFL_TN_SHORT_SL 32
+#endif
+constexpr int kSL = ADFL_TN_SHORT_SL;           // steps per lane's run (a segment: 64 kSL steps of each chain)
+constexpr int kShSeg = 8 * 64 * kSL;            // elements per segment (16384)
+constexpr int kShLS = kSL + 4;                  // floats per lane's run in LDS (+4: 16-byte reads, no conflicts)
 constexpr int kShRow = 64 * kShLS + 8;          // floats per chain (+8: chains c and c + 4 alone share banks)
+constexpr int kShVec = kShSeg / 4 / kShThreads; // 16-byte loads per thread per segment
 
 // the n % 8 tail after the lane sum (and the whole sum below 8 elements) as torch's compiled scalar loop runs
 // it: 4 rounded squares added in order when there are 4 or more, the rest with fma (as k_norm_walk's tail_sum)
@@ -1357,11 +1367,11 @@ __device__ __forceinline__ double lane_d(double v, int l) {  // readlane, so the
 // G = -126, u / 2 = 2^-150 is not a float: there a residual of 0 from a nonzero x flags the lane instead (exact
 // squares on the subnormal grid included).
 template <bool SUB>
-__device__ __forceinline__ float lane_incs(const float (&v)[kLane], float B, float h, unsigned long long& ties) {
+__device__ __forceinline__ float lane_incs(const float (&v)[kSL], float B, float h, unsigned long long& ties) {
   float Ka = 0.0f, Kb = 0.0f;
   unsigned long long t = 0ull;  // wave masks straight from the compares (as bools the compiler rebuilt bit vectors)
 #pragma unroll
-  for (int i = 0; i < kLane; i += 2) {
+  for (int i = 0; i < kSL; i += 2) {
     const float ka = __builtin_fmaf(v[i], v[i], B) - B, kb = __builtin_fmaf(v[i + 1], v[i + 1], B) - B;
     Ka += ka;
     Kb += kb;
@@ -1375,7 +1385,7 @@ __device__ __forceinline__ float lane_incs(const float (&v)[kLane], float B, flo
   ties = t;
   return Ka + Kb;
 }
-__device__ __forceinline__ float lane_incs(const float (&v)[kLane], int G, unsigned long long& ties) {
+__device__ __forceinline__ float lane_incs(const float (&v)[kSL], int G, unsigned long long& ties) {
   if (G > -126) return lane_incs<false>(v, pow2f(G), pow2f(G - 24), ties);
   float z = 0.0f;  // through an empty asm: the loop-invariant subnormal-grid sums must not be hoisted out of the
   __asm__ volatile("" : "+v"(z));  // round loop into every segment
@@ -1383,10 +1393,10 @@ __device__ __forceinline__ float lane_incs(const float (&v)[kLane], int G, unsig
 }
 
 // The lane that leaves the binade runs its steps with fma from its exact start a = acc + (the lanes before it).
-__device__ __forceinline__ float lane_fma(const float (&v)[kLane], float a, int lane, int ls) {
+__device__ __forceinline__ float lane_fma(const float (&v)[kSL], float a, int lane, int ls) {
   if (lane == ls) {
 #pragma unroll
-    for (int i = 0; i < kLane; ++i) a = __builtin_fmaf(v[i], v[i], a);
+    for (int i = 0; i < kSL; ++i) a = __builtin_fmaf(v[i], v[i], a);
   }
   return lane_f(a, ls);
 }
@@ -1394,14 +1404,21 @@ __device__ __forceinline__ float lane_fma(const float (&v)[kLane], float a, int 
 // A round by exact maps (what each lane's run adds to an even / an odd A), for a wave where a tie is possible.
 // Kept out of the fast path: the steps pass an empty asm first, so the fp64 conversions are not hoisted into
 // every round. Returns the new acc; `start` moves past the lane that left the binade (64: segment done).
-__device__ float short_exact_round(const float (&v)[kLane], float acc, int G, int lane, int& start) {
-  float w[kLane];
+__device__ float short_exact_round(const float (&v)[kSL], float acc, int G, int lane, int& start) {
+  float w[kSL];
 #pragma unroll
-  for (int i = 0; i < kLane; ++i) {
+  for (int i = 0; i < kSL; ++i) {
     w[i] = v[i];
     __asm__ volatile("" : "+v"(w[i]));
   }
-  Map m = lane_map_exact<false>(w, G);
+  Map m{0.0, 0.0};
+#pragma unroll
+  for (int h = 0; h < kSL / kLane; ++h) {  // 16 steps at a time (lane_map_exact), composed in order
+    float u[kLane];
+#pragma unroll
+    for (int i = 0; i < kLane; ++i) u[i] = w[h * kLane + i];
+    m = compose(m, lane_map_exact<false>(u, G));
+  }
   if (lane < start) m = Map{0.0, 0.0};
   const double Al = apply(wave_excl(m, lane), a_of(acc));
   const double out = apply(m, Al);
@@ -1415,10 +1432,10 @@ __device__ float short_exact_round(const float (&v)[kLane], float acc, int G, in
   return lane_fma(w, rebuild<false>(lane_d(Al, ls), G), lane, ls);
 }
 
-constexpr int kSerial = 16;  // lanes run in order at a chain's start (short_segment)
+constexpr int kSerial = 256 / ADFL_TN_SHORT_SL;  // lanes (256 steps) run in order at a chain's start (short_segment)
 
 // One segment of a chain (lane l: steps 16 l .. 16 l + 15, in order) from the exact accumulator acc (wave-uniform).
-__device__ __forceinline__ float short_segment(const float (&v)[kLane], float acc, int lane SH_ARG) {
+__device__ __forceinline__ float short_segment(const float (&v)[kSL], float acc, int lane SH_ARG) {
   int start = 0;
   SH_STAT(0, 1);
   if (acc == 0.0f) {
@@ -1434,7 +1451,7 @@ __device__ __forceinline__ float short_segment(const float (&v)[kLane], float ac
     if (!__builtin_isfinite(acc)) {  // inf stays inf unless a NaN follows; NaN stays NaN
       unsigned long long nan = 0ull;
 #pragma unroll
-      for (int i = 0; i < kLane; ++i) {  // through an empty asm: not hoisted into every segment
+      for (int i = 0; i < kSL; ++i) {  // through an empty asm: not hoisted into every segment
         float w = v[i];
         __asm__ volatile("" : "+v"(w));
         nan |= __ballot(__builtin_isnan(w));
@@ -1534,7 +1551,7 @@ __global__ __launch_bounds__(kShThreads) void k_tn_short(const float* __restrict
   typedef float f4v __attribute__((ext_vector_type(4)));
   typedef float f3v __attribute__((ext_vector_type(3)));
   struct Blk {
-    f4v r[4];
+    f4v r[kShVec];
     f3v t;  // 3 dwords: a dead 4th component's register was reused at once, which waited for the load (WAW)
   };
   const auto load = [&](Blk& k, int j) {
@@ -1543,19 +1560,20 @@ __global__ __launch_bounds__(kShThreads) void k_tn_short(const float* __restrict
     const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xa) + (left <= 0 ? 0 : (int64_t)j * kShSeg), 0,
                                                       bytes, 0x00020000);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < kShVec; ++i)
       k.r[i] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, (i * kShThreads + tid) * 16, 0, 0));
     k.t = __builtin_bit_cast(f3v, __builtin_amdgcn_raw_buffer_load_b96(rs, kShSeg * 4, 0, 0));
   };
-  // Thread tid's element p of vector i is e = 8192 j + 2048 i + 4 tid + p - delta: chain e % 8, step e / 8 of the
-  // segment (lane step / 16, slot step % 16); i adds 256 steps (16 lanes). Thread 0's first delta elements of
+  // Thread tid's element p of vector i is e = kShSeg j + 2048 i + 4 tid + p - delta: chain e % 8, step e / 8 of
+  // the segment (lane step / kSL, slot step % kSL); i adds 256 steps (256 / kSL lanes). Thread 0's first delta elements of
   // vector 0 belong to segment j - 1 (staged from its own extra vector): they go to a spare slot past the rows.
   constexpr int kBufF = 8 * kShRow;
   int off[4], off0[4];  // vector i > 0: off + 16 lanes per i; vector 0: off0 (the spare slot for e < 0)
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
-    const int e = 4 * tid + p - delta;  // e < 0 (thread 0): chain e & 7 at "lane -1, slot 15", so that vector i > 0
-    off[p] = (e & 7) * kShRow + (e >> 7) * kShLS + ((e >> 3) & 15);  // lands on step 256 i - 1
+    const int e = 4 * tid + p - delta;  // e < 0 (thread 0): chain e & 7 at "lane -1, last slot", so that vector i > 0
+    const int st = e >> 3;              // lands on step 256 i - 1
+    off[p] = (e & 7) * kShRow + (st >= 0 ? st / kSL : -1) * kShLS + (st >= 0 ? st % kSL : kSL - 1);
     off0[p] = e < 0 ? 2 * kBufF + p : off[p];
   }
   const int nvi = (int)nv;
@@ -1567,30 +1585,30 @@ __global__ __launch_bounds__(kShThreads) void k_tn_short(const float* __restrict
     float* const bj = buf + (j & 1) * kBufF;
     const int e0 = j * kShSeg - delta + 4 * tid;                    // this thread's element of vector 0
     const bool last = j * kShSeg - delta + kShSeg + 4 > nvi;         // the block holds the steps' end
-    const auto put = [&](const f4v (&r)[4]) {
+    const auto put = [&](const f4v (&r)[kShVec]) {
 #pragma unroll
       for (int p = 0; p < 4; ++p) (off0[p] < 2 * kBufF ? bj : buf)[off0[p]] = r[0][p];
 #pragma unroll
-      for (int i = 1; i < 4; ++i)
+      for (int i = 1; i < kShVec; ++i)
 #pragma unroll
-        for (int p = 0; p < 4; ++p) bj[off[p] + 16 * kShLS * i] = r[i][p];
+        for (int p = 0; p < 4; ++p) bj[off[p] + (256 / kSL) * kShLS * i] = r[i][p];
     };
     if (!last) {
       put(k.r);
     } else {  // the block holding the steps' end: zeros past it
-      f4v z[4];
+      f4v z[kShVec];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < kShVec; ++i)
 #pragma unroll
         for (int p = 0; p < 4; ++p) z[i][p] = e0 + 2048 * i + p < nvi ? k.r[i][p] : 0.0f;
       put(z);
     }
-    if (tid == 0) {  // the extra vector's first delta elements: chains 8 - delta + p of step 1023
+    if (tid == 0) {  // the extra vector's first delta elements: chains 8 - delta + p of the segment's last step
 #pragma unroll
       for (int p = 0; p < 3; ++p)
         if (p < delta) {
           const float val = (j + 1) * kShSeg - delta + p < nvi ? k.t[p] : 0.0f;
-          bj[(8 - delta + p) * kShRow + 63 * kShLS + 15] = val;
+          bj[(8 - delta + p) * kShRow + 63 * kShLS + kSL - 1] = val;
         }
     }
 #ifdef ADFL_TN_STATS
@@ -1613,9 +1631,9 @@ __global__ __launch_bounds__(kShThreads) void k_tn_short(const float* __restrict
   const auto run = [&](int j) {
     SH_TL(3);
     const float4* const rd = reinterpret_cast<const float4*>(buf + (j & 1) * kBufF + rdo);
-    float v[kLane];
+    float v[kSL];
 #pragma unroll
-    for (int q = 0; q < kLane / 4; ++q) {
+    for (int q = 0; q < kSL / 4; ++q) {
       const float4 f = rd[q];
       v[4 * q] = f.x;
       v[4 * q + 1] = f.y;
@@ -1731,7 +1749,7 @@ __global__ __launch_bounds__(64) void k_tn_chains(const void* __restrict__ x, co
     ci = tfirst[blockIdx.x];
   }
   const Tensor T = tensor_of(chunks, ci, nall);
-  const bool long_ = T.n > kShortMax;
+  const bool long_ = T.n > short_max<DT>();
   if (skip_short && !long_) return;
   const Split sp = split_of(T.n, threads);
   const int nchains = D::kContig ? (int)sp.nt : D::NC;
@@ -1765,7 +1783,7 @@ __global__ __launch_bounds__(64) void k_tn_finish(const void* __restrict__ x, co
     ci = tfirst[blockIdx.x];
   }
   const Tensor T = tensor_of(chunks, ci, nall);
-  if (skip_short && T.n <= kShortMax) return;
+  if (skip_short && T.n <= short_max<DT>()) return;
 #ifdef ADFL_TN_STATS
   if (blockIdx.x == 0) {
     for (int w = 0; w < 8; ++w) {
@@ -1867,7 +1885,7 @@ int launch(const void* x, const adfl_slq_chunk* chunks, int64_t nchunks, const i
       k_tn_tfirst<<<(unsigned)((nchunks + 255) / 256), 256, 0, st>>>(chunks, nchunks, s.tfirst);
       tfirst = s.tfirst;
     }
-    k_tn_short<<<(unsigned)ntensors, kShThreads, 0, st>>>((const float*)x, chunks, tfirst, kShortMax, n64, n32);
+    k_tn_short<<<(unsigned)ntensors, kShThreads, 0, st>>>((const float*)x, chunks, tfirst, kShortMaxF32, n64, n32);
 #ifdef ADFL_TN_STATS
     k_sh_stats_print<<<1, 1, 0, st>>>();
 #endif
@@ -1905,6 +1923,11 @@ int64_t adfl_torch_norm_scratch_bytes(int64_t nchunks, int64_t ntensors) {
 }
 
 int64_t adfl_torch_norm_short_max(void) { return adfl_tnx::kShortMax; }
+
+int64_t adfl_torch_norm_short_max_dt(int32_t dtype) {
+  if (dtype < ADFL_DTYPE_F32 || dtype > ADFL_DTYPE_F64) return ADFL_E_ARG;
+  return dtype == ADFL_DTYPE_F32 ? adfl_tnx::kShortMaxF32 : adfl_tnx::kShortMax;
+}
 
 int adfl_torch_norms_work(int32_t dtype, const void* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks,
                           const int32_t* d_tfirst, int64_t ntensors, int32_t kinds, int32_t threads, void* d_scratch,

@@ -38,6 +38,7 @@ import time
 
 _T_START = time.perf_counter()  # bench_wall_s: process start to the line (the driver's run includes interpreter start)
 
+import numpy as np
 import torch
 
 REPO = os.path.dirname(os.path.abspath(__file__))
@@ -702,43 +703,73 @@ def channel_c3_dict(steps: int) -> dict:
                          "freed before each timed call", "parity": bool(dict_ok)}
 
 
-def extra_stoch_c3(dev, lib, steps: int) -> dict:
-    """The stochastic channels the reference's experiments run (QSGDChannel(8) beside SLQChannel(8),
-    Src/main.py:229,488) on C3, with the reference's own L2 norm (torch's CPU vector_norm order,
+def c3_sizes(layout: str) -> list:
+    """C3's 256 tensor sizes (tests/golden/recipes.bucket_sizes): "equal" (11,689,512 / 256) or
+    "loguniform" (seed-0 log-uniform draws in [64, 2.4 M] scaled to the same total)."""
+    if layout == "equal":
+        base, rem = divmod(RESNET18_PARAMS, 256)
+        return [base + (1 if i < rem else 0) for i in range(256)]
+    import math
+    rng = np.random.default_rng(0)
+    raw = np.exp(rng.uniform(math.log(64), math.log(2_400_000), size=256))
+    sizes = np.maximum(64, np.floor(raw / raw.sum() * RESNET18_PARAMS)).astype(np.int64)
+    sizes[int(np.argmax(sizes))] += RESNET18_PARAMS - int(sizes.sum())
+    return [int(v) for v in sizes]
+
+
+def _stoch_want(name: str, scale: float, data: torch.Tensor, signs: torch.Tensor, levels: int) -> torch.Tensor:
+    """The reference's _dequantize_tensor arithmetic on a payload (quant.py:251-252 QSGD, :545 CNAT), in fp32."""
+    if name == "qsgd":
+        return (scale * data.float() / levels) * signs.float()
+    return scale * signs.float() * (2 ** data.float())
+
+
+def _stoch_layout_leg(dev, sizes, seed: int, steps: int) -> dict:
+    """One C3 layout through the stochastic channels the reference's experiments run (QSGDChannel(8) beside
+    SLQChannel(8), Src/main.py:229,488), with the reference's own L2 norm (torch's CPU vector_norm order,
     csrc/torch_norm.hip; quant.py:226,512): (1) host to host, QSGDChannel(8) / CNATChannel(8) built with the
-    reference's constructor, on_client_send then on_server_receive of a CPU state dict of 256 weights
-    (11,689,512 fp32, equal layout) + 256 biases — medians of the calls; (2) device-resident, the bucket's
-    encode (norm + levels + signs, Philox uniforms) timed by HIP events, the Infinity Cache flushed before each.
-    parity: every weight's scale equals torch.linalg.vector_norm of the tensor (the reference's scale), and every
-    decoded tensor equals the reference's _dequantize_tensor arithmetic on the payload (quant.py:243-252,
-    :537-545); the device encode's norms equal torch's. (The levels themselves follow the Philox stream, not
-    torch's mt19937 draws, so they are compared to a reference run only statistically — tests/.)"""
+    reference's constructor, on_client_send then on_server_receive of a CPU state dict (the weights + 256 biases),
+    medians of the calls, with the calling thread's per-phase medians (quant.phase_clock); (2) device-resident, the
+    bucket's encode (norm + levels + signs, Philox uniforms) and decode, each timed by HIP events behind an
+    Infinity-Cache flush. parity: every weight's scale equals torch.linalg.vector_norm of the tensor (the
+    reference's scale) and every decoded tensor equals the reference's _dequantize_tensor arithmetic on the payload;
+    on the device, the norms equal torch's and the decode equals that arithmetic (torch's own ops on the device).
+    (The levels follow the Philox stream, not torch's mt19937 draws: compared with a reference run only
+    statistically — tests/.)"""
     from adfl_amd import ops, stoch
-    from adfl_amd.Channel import CNATChannel, QSGDChannel
-    base, rem = divmod(RESNET18_PARAMS, 256)
-    sizes = [base + (1 if i < rem else 0) for i in range(256)]
-    g = torch.Generator().manual_seed(13)
+    from adfl_amd.Channel import CNATChannel, QSGDChannel, quant
+    g = torch.Generator().manual_seed(seed)
     params = {}
     for i, m in enumerate(sizes):
         params[f"layer{i}.weight"] = torch.randn(1, m, generator=g) * 1e-3
         params[f"layer{i}.bias"] = torch.randn(64, generator=g) * 1e-3
     ref_norms = {k: torch.linalg.vector_norm(t).item() for k, t in params.items() if t.ndim > 1}
-    out = {"workload": "C3: a CPU state dict of 256 weights (11,689,512 fp32, equal layout) + 256 biases, bits=8, "
-                       "the reference's L2 norm"}
+    out = {}
+
+    def phases(rows):
+        keys = sorted({k for r in rows for k in r})
+        return {k: round(_median([r.get(k, 0.0) for r in rows]), 3) for k in keys}
     for name, cls in (("qsgd", QSGDChannel), ("cnat", CNATChannel)):
         ch = cls(8)
-        enc_t, dec_t = [], []
+        enc_t, dec_t, enc_ph, dec_ph = [], [], [], []
         qp = dp = None
         for k in range(3 + max(steps, 5)):
             dp = qp = None
-            t1 = time.perf_counter()
-            qp, _ = ch.on_client_send(params)
-            t2 = time.perf_counter()
-            dp, _ = ch.on_server_receive(qp)
-            t3 = time.perf_counter()
+            with quant.phase_clock() as ce:
+                t1 = time.perf_counter()
+                qp, _ = ch.on_client_send(params)
+                t2 = time.perf_counter()
+            with quant.phase_clock() as cd:
+                t3 = time.perf_counter()
+                dp, _ = ch.on_server_receive(qp)
+                t4 = time.perf_counter()
             if k >= 3:
                 enc_t.append(t2 - t1)
-                dec_t.append(t3 - t2)
+                dec_t.append(t4 - t3)
+                ce.ms["other"] = (t2 - t1) * 1e3 - sum(ce.ms.values())
+                cd.ms["other"] = (t4 - t3) * 1e3 - sum(cd.ms.values())
+                enc_ph.append(ce.ms)
+                dec_ph.append(cd.ms)
         ok = True
         for k, t in params.items():
             p = qp.params[k]
@@ -746,43 +777,95 @@ def extra_stoch_c3(dev, lib, steps: int) -> dict:
                 ok = ok and torch.equal(dp[k], t)
                 continue
             ok = ok and p.scale == ref_norms[k]
-            if name == "qsgd":   # quant.py:251-252
-                want = (p.scale * p.data.float() / ch.levels) * p.signs.float()
-            else:                # quant.py:545
-                want = p.scale * p.signs.float() * (2 ** p.data.float())
+            want = _stoch_want(name, p.scale, p.data, p.signs, ch.levels)
             ok = ok and torch.equal(dp[k].view(torch.int32), want.view(torch.int32))
         e_ms, d_ms = _median(enc_t) * 1e3, _median(dec_t) * 1e3
         out[f"{name}_host"] = {"encode_ms": round(e_ms, 3), "decode_ms": round(d_ms, 3),
-                               "round_trip_ms": round(e_ms + d_ms, 3), "rounds": len(enc_t), "parity": bool(ok)}
-    # device-resident encodes of the same bucket (norm in torch's order + levels + signs)
+                               "round_trip_ms": round(e_ms + d_ms, 3), "rounds": len(enc_t),
+                               "phases_ms": {"encode": phases(enc_ph), "decode": phases(dec_ph)}, "parity": bool(ok)}
+    # device-resident encode + decode of the same bucket (norm in torch's order + levels + signs; decode)
     lay = ops.BucketLayout(sizes, align=1)
-    xc = torch.cat([params[f"layer{i}.weight"].view(-1) for i in range(256)])
-    x = xc.to(dev)
+    x = torch.cat([params[f"layer{i}.weight"].view(-1) for i in range(len(sizes))]).to(dev)
+    want_n = torch.tensor([ref_norms[f"layer{i}.weight"] for i in range(len(sizes))], dtype=torch.float32)
+    out.update(_stoch_device_legs(dev, x, lay, want_n, steps))
+    return out
+
+
+def _stoch_device_legs(dev, x: torch.Tensor, lay, want_norms: torch.Tensor, steps: int) -> dict:
+    """QSGD / CNAT (bits 8) device encode with the reference's norm, then decode, of the bucket x: median HIP-event
+    ms of each behind an Infinity-Cache flush, the reference-order norm's own share, and parity (norms equal
+    want_norms — torch.linalg.vector_norm on the host — and the decode equals the reference's arithmetic computed
+    by torch on the device)."""
+    from adfl_amd import stoch
     lv = torch.empty(lay.total, dtype=torch.uint8, device=dev)
     sg = torch.empty(lay.total, dtype=torch.int8, device=dev)
     nrm = torch.empty(lay.ntensors, device=dev)
+    dq = torch.empty(lay.total, device=dev)
     ws = stoch.workspace(lay, dev)
     junk = torch.ones(128 << 20, device=dev)
     stream = torch.cuda.current_stream(dev)
-    want = torch.tensor([ref_norms[f"layer{i}.weight"] for i in range(256)], dtype=torch.float32)
-    for name in ("qsgd", "cnat"):
-        def enc():
-            if name == "qsgd":
-                stoch.qsgd_encode_batched(x, lay, 8, seed=1, levels=lv, signs=sg, norms=nrm, ws=ws, torch_norm=True)
-            else:
-                stoch.cnat_encode_batched(x, lay, 8, seed=1, exps=lv.view(torch.int8), signs=sg, norms=nrm, ws=ws,
-                                          torch_norm=True)
-        enc()
-        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(max(steps, 10))]
+    reps = max(steps, 10)
+    levels = (1 << 8) - 1
+    out = {}
+
+    def timed(fn):
+        fn()
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(reps)]
         for e in evs:
             junk.amax()
             e[0].record(stream)
-            enc()
+            fn()
             e[1].record(stream)
         torch.cuda.synchronize()
-        ms = _median([e[0].elapsed_time(e[1]) for e in evs])
-        out[f"{name}_device_encode"] = {"ms": round(ms, 4), "GiB_per_s": round(lay.total * 4 / GIB / (ms * 1e-3), 1),
-                                        "parity": bool(torch.equal(nrm.cpu().view(torch.int32), want.view(torch.int32)))}
+        return _median([e[0].elapsed_time(e[1]) for e in evs])
+    norm_ms = timed(lambda: stoch.reference_norms(x, lay, out32=nrm))
+    gib = lay.total * 4 / GIB
+    for name in ("qsgd", "cnat"):
+        if name == "qsgd":
+            enc = lambda: stoch.qsgd_encode_batched(x, lay, 8, seed=1, levels=lv, signs=sg, norms=nrm, ws=ws,  # noqa: E731
+                                                    torch_norm=True)
+            dec = lambda: stoch.qsgd_decode_batched(lv, sg, nrm, lay, 8, out=dq)  # noqa: E731
+        else:
+            enc = lambda: stoch.cnat_encode_batched(x, lay, 8, seed=1, exps=lv.view(torch.int8), signs=sg,  # noqa: E731
+                                                    norms=nrm, ws=ws, torch_norm=True)
+            dec = lambda: stoch.cnat_decode_batched(lv.view(torch.int8), sg, nrm, lay, out=dq)  # noqa: E731
+        e_ms = timed(enc)
+        d_ms = timed(dec)
+        ok = torch.equal(nrm.cpu().view(torch.int32), want_norms.view(torch.int32))
+        nr = torch.repeat_interleave(nrm, torch.as_tensor(lay.sizes, device=dev)) if lay.align == 1 else None
+        if nr is not None and lay.total == int(lay.sizes.sum()):
+            data = lv if name == "qsgd" else lv.view(torch.int8)
+            want = (nr * data.float() / levels) * sg.float() if name == "qsgd" else nr * sg.float() * (2 ** data.float())
+            ok = ok and torch.equal(dq.view(torch.int32), want.view(torch.int32))
+        out[f"{name}_device"] = {"encode_ms": round(e_ms, 4), "decode_ms": round(d_ms, 4),
+                                 "round_trip_GiB_per_s": round(gib / ((e_ms + d_ms) * 1e-3), 1),
+                                 "parity": bool(ok)}
+    out["reference_norm_ms"] = round(norm_ms, 4)
+    return out
+
+
+def extra_stoch_c3(dev, lib, steps: int) -> dict:
+    """The stochastic channels with the reference's norm on both C3 layouts (_stoch_layout_leg)."""
+    out = {"workload": "C3: a CPU state dict of 256 weights (11,689,512 fp32) + 256 biases, bits=8, the reference's "
+                       "L2 norm; 'equal' and 'loguniform' layouts (SURVEY.md §8d)"}
+    for layout, seed in (("equal", 13), ("loguniform", 14)):
+        out[layout] = _stoch_layout_leg(dev, c3_sizes(layout), seed, steps)
+    return out
+
+
+def extra_stoch_c2(dev, lib, steps: int) -> dict:
+    """C2's 1 GiB flat fp32 gradient through QSGD / CNAT bits 8 on the device with the reference's norm (the
+    default of QSGDChannel(8) / CNATChannel(8)): encode and decode (_stoch_device_legs), parity against
+    torch.linalg.vector_norm of the same tensor on the host."""
+    from adfl_amd import ops
+    g = torch.Generator().manual_seed(17)
+    xc = torch.randn(1 << 28, generator=g) * 1e-3
+    want = torch.linalg.vector_norm(xc).reshape(1).to(torch.float32)
+    x = xc.to(dev)
+    del xc
+    lay = ops.BucketLayout([1 << 28], align=1)
+    out = {"workload": "C2: one 2^28-element fp32 tensor, QSGD / CNAT bits=8, the reference's L2 norm"}
+    out.update(_stoch_device_legs(dev, x, lay, want, steps))
     return out
 
 
@@ -1076,7 +1159,7 @@ def main():
         # BASELINE's other single-GPU configs and the host-inclusive rate, after the timed headline (never in
         # `value`); each carries its own parity against the reference's ATen ops
         for key, fn, st in (("c3", extra_c3, 20), ("c5_int4", extra_c5, 10), ("pcie", extra_pcie, 5),
-                            ("stoch_c3", extra_stoch_c3, 5)):
+                            ("stoch_c3", extra_stoch_c3, 5), ("stoch_c2", extra_stoch_c2, 5)):
             try:
                 line[key] = fn(dev, lib, st)
             except Exception as e:  # noqa: BLE001

@@ -66,6 +66,54 @@ def test_send_with_q_error_equals_reference_model_sizes(name):
             assert mse == float(ref["mse"]) and cos == float(ref["cos"]), (name, bits, t, mse, cos, ref)
 
 
+@pytest.mark.parametrize("name", ["edges", "resnet18"])
+def test_worker_q_error_call_sequence_with_dropin_metrics(name):
+    """Src/ADFL/Client/worker.py:176,186-189 unchanged except for where the two metric functions come from
+    (adfl_amd.model's device drop-ins for ADFL.model's): on_client_send, then
+    on_server_receive of the payload, then parameter_relative_mse / parameter_cosine_similarity(exclude_bias=True)
+    == the reference's doubles (the reference executed in place, tests/golden/qerror_manifest.json)."""
+    from adfl_amd import model as am
+    m = json.load(open(os.path.join(GOLDEN, "qerror_manifest.json")))
+    e = m["dicts"][name]
+    spec = mgq.dicts()[name]
+    params = {}
+    for i, (n, s, mult) in enumerate(spec):
+        params[n] = torch.from_numpy(recipes.randn(s, e["seed0"] + i, mult))
+    for bits in mgq.BITS:
+        ch = SLQChannel(bits)
+        for t in (1, 8):
+            with _threads(t):
+                c_params, _ = ch.on_client_send(params)
+                d_params, _ = ch.on_server_receive(c_params)
+                mse = am.parameter_relative_mse(params, d_params, exclude_bias=True)
+                cos = am.parameter_cosine_similarity(params, d_params, exclude_bias=True)
+            ref = e["metrics"][f"slq{bits}_t{t}"]
+            assert mse == float(ref["mse"]) and cos == float(ref["cos"]), (name, bits, t, mse, cos, ref)
+
+
+def test_dropin_metrics_with_biases_and_errors():
+    """exclude_bias=False counts the 1-D entries too; an empty selection gives 0.0 / the cat error; key and shape
+    mismatches raise the reference's AssertionError (model.py:266-277, :303-312)."""
+    from adfl_amd import model as am
+    g = torch.Generator().manual_seed(3)
+    a = {"w": torch.randn(40, 33, generator=g), "b": torch.randn(40, generator=g), "n": torch.randn(70001, 1, generator=g)}
+    b = {k: v + torch.randn(v.shape, generator=g) * 1e-2 for k, v in a.items()}
+    for eb in (True, False):
+        keep = [k for k in a if not eb or a[k].ndim > 1]
+        num = sum(torch.sum((a[k] - b[k]) ** 2).item() for k in keep) / sum(a[k].numel() for k in keep)
+        den = sum(torch.sum((a[k] - 0) ** 2).item() for k in keep) / sum(a[k].numel() for k in keep)
+        cos = F.cosine_similarity(torch.cat([a[k].flatten() for k in keep]), torch.cat([b[k].flatten() for k in keep]),
+                                  dim=0).item()
+        assert am.parameter_relative_mse(a, b, eb) == num / den
+        assert am.parameter_cosine_similarity(a, b, eb) == cos
+    only_bias = {"b": a["b"]}
+    assert am.parameter_relative_mse(only_bias, {"b": b["b"]}, True) == 0.0
+    with pytest.raises(RuntimeError):
+        am.parameter_cosine_similarity(only_bias, {"b": b["b"]}, True)
+    with pytest.raises(AssertionError):
+        am.parameter_relative_mse(a, {"w": b["w"]}, True)
+
+
 def _torch_sums(xs, ds, t):
     """What model.py:256-323 reduces, by torch itself on the CPU with t threads."""
     with _threads(t):

@@ -73,7 +73,7 @@ def _data(kind: str, n: int, rng, dtype) -> torch.Tensor:
 KINDS = ["randn", "grad", "ints", "short", "const", "wide", "jump", "under", "sub", "over", "nan", "inf",
          "late_nan", "zeros"]
 SIZES = [1, 3, 4, 5, 7, 8, 9, 15, 16, 17, 31, 63, 64, 65, 1023, 1025, 4097, 8192, 8199, 12289, 32767, 32768,
-         32769, 45663, 65536, 65537, 65541, 100003, 131075, 200011]
+         32769, 45663, 65536, 65537, 65541, 100003, 131075, 200011, 524288, 524291]  # fp32 short bound 2^19
 
 
 def _torch_norm(x: torch.Tensor, threads: int) -> float:
