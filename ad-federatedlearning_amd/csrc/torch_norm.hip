@@ -1312,7 +1312,7 @@ __device__ typename Acc<Dt<DT>::kWide>::T resolve_chain(const void* x, const Ten
 // itself: tests/test_gpu_torch_norm.py, test_gpu_torch_norm_dt.py.
 constexpr int kShThreads = 512;                 // wave c runs chain c
 #ifndef ADFL_TN_SHORT_SL
-#define ADFL_TN_SHORT_SL 32
+#define ADFL_TN_SHORT_SL 16
 #endif
 constexpr int kSL = ADFL_TN_SHORT_SL;           // steps per lane's run (a segment: 64 kSL steps of each chain)
 constexpr int kShSeg = 8 * 64 * kSL;            // elements per segment (16384)
