@@ -236,7 +236,9 @@ __device__ __forceinline__ Map lane_map_exact(const E (&v)[kLane], int g) {
 // Lane maps on grids g and g + d (d = +1 or -1) in one pass. SQ (bf16 / fp16 inputs): x^2 has at most 22
 // significant bits, so hi = x^2 / u is exact in fp32 and its fraction decides ties: fp32 / int32 arithmetic,
 // no fp64 (a square that underflows is far below 1/2: no tie, increment 0). Otherwise lane_map_exact twice.
-__device__ __forceinline__ float pow2f(int k) { return __int_as_float((k + 127) << 23); }
+__device__ __forceinline__ float pow2f(int k) { return __int_as_float((k + 127) << 23); }  // -126 <= k <= 128
+// 2^k for -149 <= k <= 127, subnormal powers included (half-ulps of low binades: 2^(G-24) down to G = -125)
+__device__ __forceinline__ float pow2fs(int k) { return k >= -126 ? pow2f(k) : __int_as_float(1 << (k + 149)); }
 __device__ __forceinline__ void sq_step(float h, int& e, int& o) {
   const float k = (h + 12582912.0f) - 12582912.0f;  // rint, |h| < 2^22
   const float fr = h - k;
@@ -403,6 +405,7 @@ struct Rec {
 static_assert(sizeof(Rec) == 8, "record layout");
 constexpr uint32_t kSide = 1u;      // exact maps in the side table
 constexpr uint32_t kPad = 2u;       // phase D: past the chain's end (identity)
+constexpr uint32_t kNaN = 4u;       // fp32 (whose S is sampled): the tile holds a NaN
 constexpr uint32_t kNoK = 0xffffffu;  // a total of 2^24 - 1 or more (not covered)
 // fp32 accumulators: w0 = k0 | flags << 24, w1 = k1 | (g + 128) << 24; fp64 ones: w0 = flags << 24, w1 = g + 2048
 template <bool W> __device__ __forceinline__ Rec make_rec(double k0, double k1, int g, uint32_t flags) {
@@ -492,19 +495,30 @@ __global__ __launch_bounds__(256) void k_tn_sums(const void* __restrict__ x, con
   const ChunkGeo G = geo_of<DT>(T, ci, sp);
   if (G.lim <= 0) return;  // a chunk of tail elements only: no tile
   const V v(x, T.base + G.c0e, G.lim);
-  u32x4 r[NV];
+  // fp32: a sample — 16 of the chunk's 256 128-byte lines (every 16th, from an offset that rotates with the
+  // chunk), weighted 16 — since S only predicts binades (phase B) and may be off (by a margin, there); the
+  // other dtypes sum every element. A sampled line is 8 vectors; thread tid < 128 loads vector tid % 8 of line
+  // 16 (tid / 8) + rot (the same parity as tid, so the chain classes below hold).
+  constexpr bool kSampled = DT == ADFL_DTYPE_F32;
+  constexpr int NL = kSampled ? 1 : NV;
+  const auto fidx = [&](int i) -> int {
+    if constexpr (kSampled) return 128 * (tid >> 3) + 8 * ((ci * 7) & 15) + (tid & 7);
+    else return tid + 256 * i;
+  };
+  u32x4 r[NL];
 #pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int f = tid + 256 * i;
+  for (int i = 0; i < NL; ++i) {
+    const int f = fidx(i);
+    const bool in = f < v.nvec && (!kSampled || tid < 128);
     const u32x4 q = ld_x(v.vb + (f < v.nvec ? f : v.nvec - 1));  // unconditional (index clamped): all loads in flight
-    r[i] = f < v.nvec ? q : u32x4{0u, 0u, 0u, 0u};
+    r[i] = in ? q : u32x4{0u, 0u, 0u, 0u};
   }
   double acc[EPV], acc1 = 0.0;  // strided: per vector position; fp16: acc[0] / acc1 = piece 0 / 1
 #pragma unroll
   for (int p = 0; p < EPV; ++p) acc[p] = 0.0;
 #pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int f = tid + 256 * i;
+  for (int i = 0; i < NL; ++i) {
+    const int f = fidx(i);
 #pragma unroll
     for (int p = 0; p < EPV; ++p) {
       const int e = f * EPV + p - v.delta;
@@ -545,7 +559,8 @@ __global__ __launch_bounds__(256) void k_tn_sums(const void* __restrict__ x, con
       }
     }
     __syncthreads();
-    if (tid < D::NC) S[slot_of(ci, tid, T.nall)] = s_red[0][tid] + s_red[1][tid] + s_red[2][tid] + s_red[3][tid];
+    if (tid < D::NC)
+      S[slot_of(ci, tid, T.nall)] = (s_red[0][tid] + s_red[1][tid] + s_red[2][tid] + s_red[3][tid]) * (kSampled ? 16.0 : 1.0);
   }
 }
 
@@ -616,7 +631,11 @@ __global__ __launch_bounds__(256) void k_tn_grids(const adfl_slq_chunk* __restri
 #pragma unroll
       for (int k = 0; k < kTPL; ++k) {
         const int64_t t = w0 + lane * kTPL + k;
-        if (t < nt) recs[tile_of<DT>(T, c, sp, t).slot] = make_rec<D::kWide>(0.0, 0.0, grid_pred<D::kWide>(P), 0u);
+        // fp32's S is sampled: P is raised by a margin that covers the sample's error (a Gaussian tile's sampled
+        // sum is within about 18% of its own, a prefix of t tiles within 18% / sqrt(t)); P may overshoot the
+        // accumulator by up to 2x and still predict it (the maps are on g and g - 1), not undershoot it
+        const double Pm = DT == ADFL_DTYPE_F32 ? P * (1.0 + fmin(0.9, 1.0 / __builtin_sqrt((double)t + 1.0))) : P;
+        if (t < nt) recs[tile_of<DT>(T, c, sp, t).slot] = make_rec<D::kWide>(0.0, 0.0, grid_pred<D::kWide>(Pm), 0u);
         P += y[k];
       }
     }
@@ -796,6 +815,119 @@ __global__ __launch_bounds__(256) void k_tn_maps(const void* __restrict__ x, con
   if (tid == 0 && s_slow) exact_list[atomicAdd(exact_list - 1, 1)] = ci;  // the count sits just before the list
 }
 
+// fp32 phase C: a tile's totals on its predicted binade g and on g - 1 as exact increments, order-free: on a
+// normal grid G (ulp u = 2^(G-23)) a step adds fma(x, x, 2^G) - 2^G (k_tn_short's argument: exact unless x^2 is
+// at or above 2^G, which then makes the total at least 2^23 u — never covered from A >= 2^23), summed in fp32
+// (exact below 2^24 u, at least that above). A tie leaves the residual x^2 - k at exactly +-u/2, which
+// fma(-x, x, k) returns exactly, so a chunk where some |residual| equals u/2 (rarely a rounding, not a tie) goes
+// to k_tn_maps_exact; so does a chunk whose chains are predicted on the subnormal grid. A NaN sets kNaN (S is
+// sampled for fp32, so it cannot tell phase D). One read of x; no fp64.
+__global__ __launch_bounds__(256) void k_tn_maps_f32(const float* __restrict__ x, const adfl_slq_chunk* __restrict__ chunks,
+                                                     int64_t nall, Rec* __restrict__ recs, int* __restrict__ exact_list) {
+  using V = View<ADFL_DTYPE_F32>;
+  constexpr int EPV = V::EPV, NV = V::NV;
+  __shared__ float s_k[4][8][2];
+  __shared__ int s_g[8], s_slow, s_fl[4][8];
+  const int ci = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const Tensor T = tensor_of(chunks, ci, nall);
+  if (T.n <= kShortMaxF32) return;
+  const ChunkGeo G = geo_of<ADFL_DTYPE_F32>(T, ci, Split{1, T.n});
+  if (G.lim <= 0) return;
+  const V v(x, T.base + G.c0e, G.lim);
+  u32x4 r[NV];
+  load_chunk<ADFL_DTYPE_F32>(v, tid, r);  // first: the record load below must not hold the chunk's loads back
+  if (tid < 8) s_g[tid] = rec_g<false>(recs[slot_of(ci, tid, T.nall)]);
+  if (tid == 0) s_slow = 0;
+  __syncthreads();
+  // per position p: its chain's grids g (B0, h0) and g - 1 (B1, h1); a subnormal grid sends the chunk to the
+  // exact path (flag through sub)
+  float B0[EPV], h0[EPV], B1[EPV], h1[EPV];
+  bool sub = false;
+#pragma unroll
+  for (int p = 0; p < EPV; ++p) {
+    const int c = ((tid * EPV + p - v.delta) % 8 + 8) % 8;
+    const int g = s_g[c];
+    sub |= g - 1 <= -126;
+    B0[p] = pow2f(g);
+    h0[p] = pow2fs(g - 24);
+    B1[p] = pow2f(g - 1 < -126 ? -126 : g - 1);  // (g - 1 < -126: not a grid; e1 is +inf below)
+    h1[p] = pow2fs(g - 25 < -149 ? -149 : g - 25);
+  }
+  float K0[EPV], K1[EPV];
+  bool fl[EPV], nan = false;
+#pragma unroll
+  for (int p = 0; p < EPV; ++p) {
+    K0[p] = K1[p] = 0.0f;
+    fl[p] = false;
+  }
+  const auto step = [&](float xv, int p) {
+    const float k0 = __builtin_fmaf(xv, xv, B0[p]) - B0[p], k1 = __builtin_fmaf(xv, xv, B1[p]) - B1[p];
+    K0[p] += k0;
+    K1[p] += k1;
+    const float r0 = __builtin_fmaf(-xv, xv, k0), r1 = __builtin_fmaf(-xv, xv, k1);
+    fl[p] |= (__builtin_fabsf(r0) == h0[p]) | (__builtin_fabsf(r1) == h1[p]);
+    nan |= xv != xv;
+  };
+  if (v.delta == 0 && G.lim == kChunk) {  // a whole aligned chunk: no masks
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+#pragma unroll
+      for (int p = 0; p < EPV; ++p) step(V::elem(r[i], p), p);
+  } else {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int f = tid + 256 * i;
+#pragma unroll
+      for (int p = 0; p < EPV; ++p) {
+        const int e = f * EPV + p - v.delta;
+        step((e >= 0 && e < G.lim) ? V::elem(r[i], p) : 0.0f, p);
+      }
+    }
+  }
+  // lanes of one parity hold the same chains (positions p -> chains (4 tid + p - delta) % 8)
+#pragma unroll
+  for (int p = 0; p < EPV; ++p) {
+#pragma unroll
+    for (int o = 2; o < 64; o <<= 1) {
+      K0[p] += __shfl_xor(K0[p], o, 64);
+      K1[p] += __shfl_xor(K1[p], o, 64);
+    }
+    const unsigned long long b = __ballot(fl[p]);
+    fl[p] = (b & (0x5555555555555555ull << (lane & 1))) != 0ull;
+  }
+  const bool anynan = __ballot(nan) != 0ull;
+  if (lane < 2) {
+#pragma unroll
+    for (int p = 0; p < EPV; ++p) {
+      const int c = ((lane * EPV + p - v.delta) % 8 + 8) % 8;
+      s_k[wave][c][0] = K0[p];
+      s_k[wave][c][1] = K1[p];
+      s_fl[wave][c] = fl[p] | (anynan ? 2 : 0);
+    }
+  }
+  __syncthreads();
+  if (tid < 8) {
+    float k0 = 0.0f, k1 = 0.0f;
+    int f = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      k0 += s_k[w][tid][0];
+      k1 += s_k[w][tid][1];
+      f |= s_fl[w][tid];
+    }
+    const int g = s_g[tid];
+    // the totals in ulps of g and g - 1, exact integers below 2^24 (kNoK: not covered; NaN / inf included)
+    const double inf = __builtin_inf();
+    const double q0 = (double)k0 * pow2(23 - g), q1 = (double)k1 * pow2(24 - g);
+    const double e0 = q0 < (double)kNoK ? q0 : inf;
+    const double e1 = (g - 1 >= -126 && q1 < (double)kNoK) ? q1 : inf;
+    if (((f & 1) || sub) && (e0 < Acc<false>::kTop || e1 < Acc<false>::kTop)) s_slow = 1;
+    recs[slot_of(ci, tid, T.nall)] = make_rec<false>(e0, e1, g, (f & 2) ? kNaN : 0u);
+  }
+  __syncthreads();
+  if (tid == 0 && s_slow) exact_list[atomicAdd(exact_list - 1, 1)] = ci;  // the count sits just before the list
+}
+
 // The listed chunks, exactly: chain-major staging (16 steps per lane block, +1 pad), maps composed in order.
 template <int DT>
 __global__ __launch_bounds__(256) void k_tn_maps_exact(const void* __restrict__ x, const adfl_slq_chunk* __restrict__ chunks, int64_t nall,
@@ -810,6 +942,7 @@ __global__ __launch_bounds__(256) void k_tn_maps_exact(const void* __restrict__ 
   __shared__ E st[8 * 64 * kLS];  // 8 rows of 1024 steps (strided: chain-major; fp16: the chunk in order)
   __shared__ double s_m[4][2][4];
   __shared__ int s_g[8];
+  __shared__ uint32_t s_nf[8];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int count = exact_list[-1];
   for (int li = blockIdx.x; li < count; li += gridDim.x) {
@@ -818,7 +951,11 @@ __global__ __launch_bounds__(256) void k_tn_maps_exact(const void* __restrict__ 
     const Split sp = split_of(T.n, threads);
     const ChunkGeo G = geo_of<DT>(T, ci, sp);
     const int npieces = D::kContig ? (G.bnd < G.len ? 2 : 1) : D::NC;
-    if (tid < npieces) s_g[tid] = rec_g<W>(recs[slot_of(ci, tid, T.nall)]);
+    if (tid < npieces) {
+      const Rec q = recs[slot_of(ci, tid, T.nall)];
+      s_g[tid] = rec_g<W>(q);
+      s_nf[tid] = rec_flags(q) & kNaN;
+    }
     const V v(x, T.base + G.c0e, G.lim);
     u32x4 r[NV];
     load_chunk<DT>(v, tid, r);
@@ -918,7 +1055,7 @@ __global__ __launch_bounds__(256) void k_tn_maps_exact(const void* __restrict__ 
       if (g - 1 < Acc<W>::kGmin) a1 = Map{__builtin_inf(), __builtin_inf()};
       const int64_t slot = slot_of(ci, tid, T.nall);
       maps[slot] = make_double4(a0.e, a0.o, a1.e, a1.o);
-      recs[slot] = make_rec<W>(0.0, 0.0, g, kSide);
+      recs[slot] = make_rec<W>(0.0, 0.0, g, kSide | s_nf[tid]);
     }
     __syncthreads();
   }
@@ -1173,7 +1310,10 @@ __device__ typename Acc<Dt<DT>::kWide>::T resolve_window(const void* x, const Te
     TN_STAT(7, 1);
     if (!__builtin_isfinite(acc)) {  // inf stays inf unless a NaN follows: the remaining tiles' sums say
       bool nan = false;
-      for (int64_t u = w0 + start + lane; u < nt; u += 64) nan |= __builtin_isnan(S[tile_of<DT>(T, c, sp, u).slot]);
+      for (int64_t u = w0 + start + lane; u < nt; u += 64) {
+        const int64_t sl = tile_of<DT>(T, c, sp, u).slot;
+        nan |= __builtin_isnan(S[sl]) || (rec_flags(recs[sl]) & kNaN);
+      }
       if (__ballot(nan)) acc = (A_t)__builtin_nan("");
       return acc;
     }
@@ -1257,7 +1397,7 @@ __device__ typename Acc<Dt<DT>::kWide>::T resolve_chain(const void* x, const Ten
       if (!__builtin_isfinite(acc)) {  // inf stays inf unless a NaN follows: the remaining tiles' sums say
         bool nan = false;
         for (int64_t u = (wb + wstart) * kWinTiles + lane; u < nt; u += 64)
-          nan |= __builtin_isnan(S[tile_of<DT>(T, c, sp, u).slot]);
+          nan |= __builtin_isnan(S[tile_of<DT>(T, c, sp, u).slot]) || (rec_flags(recs[tile_of<DT>(T, c, sp, u).slot]) & kNaN);
         if (__ballot(nan)) acc = (A_t)__builtin_nan("");
         return acc;
       }
@@ -1386,7 +1526,7 @@ __device__ __forceinline__ float lane_incs(const float (&v)[kSL], float B, float
   return Ka + Kb;
 }
 __device__ __forceinline__ float lane_incs(const float (&v)[kSL], int G, unsigned long long& ties) {
-  if (G > -126) return lane_incs<false>(v, pow2f(G), pow2f(G - 24), ties);
+  if (G > -126) return lane_incs<false>(v, pow2f(G), pow2fs(G - 24), ties);
   float z = 0.0f;  // through an empty asm: the loop-invariant subnormal-grid sums must not be hoisted out of the
   __asm__ volatile("" : "+v"(z));  // round loop into every segment
   return lane_incs<true>(v, z, z, ties);
@@ -1479,7 +1619,7 @@ __device__ __forceinline__ float short_segment(const float (&v)[kSL], float acc,
     if (start == 64 || !__builtin_isfinite(acc) || grid_of(acc) != G + 1) continue;
     // on from lane ls + 1 on G + 1, where acc went (the usual crossing): one more scan, no new round
     unsigned long long ties1;
-    const float K1 = lane_incs<false>(v, top, pow2f(G - 23), ties1);
+    const float K1 = lane_incs<false>(v, top, pow2fs(G - 23), ties1);
     if (ties1 >> start) continue;  // start = ls + 1 < 64
     const float I1 = wave_incl_f(lane > ls ? K1 : 0.0f), out1 = acc + I1;
     const unsigned long long b1 = __ballot(lane > ls && !(out1 < pow2f(G + 2)));
@@ -1896,7 +2036,10 @@ int launch(const void* x, const adfl_slq_chunk* chunks, int64_t nchunks, const i
     k_tn_winsums<DT><<<dim3((unsigned)ntensors, 8, 8), 256, 0, st>>>(chunks, nchunks, s.tfirst, threads, s.S, s.wsum);
     k_tn_grids<DT><<<dim3((unsigned)ntensors, 8, 8), 256, 0, st>>>(chunks, nchunks, s.tfirst, threads, s.S, s.wsum, s.recs);
     if (hipError_t e = hipMemsetAsync(s.exact, 0, 4, st)) return (int)e;
-    k_tn_maps<DT><<<(unsigned)nchunks, 256, 0, st>>>(x, chunks, nchunks, threads, s.recs, s.maps, s.exact + 1);
+    if constexpr (DT == ADFL_DTYPE_F32)
+      k_tn_maps_f32<<<(unsigned)nchunks, 256, 0, st>>>((const float*)x, chunks, nchunks, s.recs, s.exact + 1);
+    else
+      k_tn_maps<DT><<<(unsigned)nchunks, 256, 0, st>>>(x, chunks, nchunks, threads, s.recs, s.maps, s.exact + 1);
     k_tn_maps_exact<DT><<<(unsigned)(nchunks < 1024 ? nchunks : 1024), 256, 0, st>>>(x, chunks, nchunks, threads, s.recs, s.maps,
                                                                                    s.exact + 1);
     k_tn_windows<DT><<<dim3((unsigned)ntensors, 8, 8), 256, 0, st>>>(chunks, nchunks, s.tfirst, threads, s.recs, s.maps, s.wing,

@@ -34,6 +34,8 @@ def _data(kind: str, n: int, rng, dtype) -> torch.Tensor:
         x = np.trunc(rng.standard_normal(n) * 20)
     elif kind == "short":  # few mantissa bits: ties
         x = np.round(rng.standard_normal(n) * 16) / 64
+    elif kind == "tiny_short":  # low binades (u / 2 subnormal) with ties: x^2 near 2^-112, few mantissa bits
+        x = np.round(rng.standard_normal(n) * 16) / 64 * 2.0 ** -56
     elif kind == "const":
         x = np.full(n, 0.6, f)
     elif kind == "wide":
@@ -70,7 +72,7 @@ def _data(kind: str, n: int, rng, dtype) -> torch.Tensor:
     return torch.from_numpy(x).to(dtype)
 
 
-KINDS = ["randn", "grad", "ints", "short", "const", "wide", "jump", "under", "sub", "over", "nan", "inf",
+KINDS = ["randn", "grad", "ints", "short", "tiny_short", "const", "wide", "jump", "under", "sub", "over", "nan", "inf",
          "late_nan", "zeros"]
 SIZES = [1, 3, 4, 5, 7, 8, 9, 15, 16, 17, 31, 63, 64, 65, 1023, 1025, 4097, 8192, 8199, 12289, 32767, 32768,
          32769, 45663, 65536, 65537, 65541, 100003, 131075, 200011, 524288, 524291]  # fp32 short bound 2^19
