@@ -26,7 +26,9 @@
 // a non-finite value, or a step of 2^24 ulps or more is not covered: the reference arithmetic (fma) runs it.
 //
 // Phases (long tensors: more than kShortMax elements), one launch each, every block independent:
-//   A  k_tn_sums: per 8192-element chunk and chain (fp16: piece), the fp64 sum S of x^2 (one read of x);
+//   A  k_tn_sums: per 8192-element chunk and chain (fp16: piece), the fp64 sum S of x^2 (one read of x;
+//      fp32, k_tn_sums_f32: of a 1/16 sample, weighted 16 — phase C's increments are exact there, so S only
+//      predicts binades and flags nothing);
 //   B  k_tn_winsums + k_tn_grids: per window of 512 tiles the sum of S, then per tile the exclusive prefix P
 //      (earlier windows + a wave scan) predicts the binade of the accumulator at the tile's start:
 //      g = binade(P (1 + 2^-8)) — a prediction only (a miss leaves the tile uncovered, resolved in D);
@@ -426,6 +428,7 @@ __device__ __forceinline__ double rec_k(Rec r, int j) {  // j = 0 / 1: the total
 }
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef float f2v __attribute__((ext_vector_type(2)));
 // x streams through phases A and C once each (1 GiB on C2, beyond the Infinity Cache): non-temporal loads
 // (measured: phase A 190 -> 171 us on C2)
 // (global address space, so they are global_load, not flat_load, and do not count on lgkmcnt)
@@ -479,6 +482,16 @@ __device__ __forceinline__ ChunkGeo geo_of(const Tensor& T, int ci, Split sp) {
   return g;
 }
 
+template <int DT>
+__device__ __forceinline__ void load_chunk(const View<DT>& v, int tid, u32x4 (&r)[View<DT>::NV]) {
+#pragma unroll
+  for (int i = 0; i < View<DT>::NV; ++i) {
+    const int f = tid + 256 * i;
+    const u32x4 q = ld_x(v.vb + (f < v.nvec ? f : v.nvec - 1));  // unconditional (index clamped): all loads in flight
+    r[i] = f < v.nvec ? q : u32x4{0u, 0u, 0u, 0u};
+  }
+}
+
 // ---- phase A: per chunk and chain (piece), the fp64 sum of x^2; also tfirst[t] = t's first chunk
 template <int DT>
 __global__ __launch_bounds__(256) void k_tn_sums(const void* __restrict__ x, const adfl_slq_chunk* __restrict__ chunks, int64_t nall,
@@ -495,30 +508,14 @@ __global__ __launch_bounds__(256) void k_tn_sums(const void* __restrict__ x, con
   const ChunkGeo G = geo_of<DT>(T, ci, sp);
   if (G.lim <= 0) return;  // a chunk of tail elements only: no tile
   const V v(x, T.base + G.c0e, G.lim);
-  // fp32: a sample — 16 of the chunk's 256 128-byte lines (every 16th, from an offset that rotates with the
-  // chunk), weighted 16 — since S only predicts binades (phase B) and may be off (by a margin, there); the
-  // other dtypes sum every element. A sampled line is 8 vectors; thread tid < 128 loads vector tid % 8 of line
-  // 16 (tid / 8) + rot (the same parity as tid, so the chain classes below hold).
-  constexpr bool kSampled = DT == ADFL_DTYPE_F32;
-  constexpr int NL = kSampled ? 1 : NV;
-  const auto fidx = [&](int i) -> int {
-    if constexpr (kSampled) return 128 * (tid >> 3) + 8 * ((ci * 7) & 15) + (tid & 7);
-    else return tid + 256 * i;
-  };
-  u32x4 r[NL];
-#pragma unroll
-  for (int i = 0; i < NL; ++i) {
-    const int f = fidx(i);
-    const bool in = f < v.nvec && (!kSampled || tid < 128);
-    const u32x4 q = ld_x(v.vb + (f < v.nvec ? f : v.nvec - 1));  // unconditional (index clamped): all loads in flight
-    r[i] = in ? q : u32x4{0u, 0u, 0u, 0u};
-  }
+  u32x4 r[NV];
+  load_chunk<DT>(v, tid, r);
   double acc[EPV], acc1 = 0.0;  // strided: per vector position; fp16: acc[0] / acc1 = piece 0 / 1
 #pragma unroll
   for (int p = 0; p < EPV; ++p) acc[p] = 0.0;
 #pragma unroll
-  for (int i = 0; i < NL; ++i) {
-    const int f = fidx(i);
+  for (int i = 0; i < NV; ++i) {
+    const int f = tid + 256 * i;
 #pragma unroll
     for (int p = 0; p < EPV; ++p) {
       const int e = f * EPV + p - v.delta;
@@ -560,7 +557,67 @@ __global__ __launch_bounds__(256) void k_tn_sums(const void* __restrict__ x, con
     }
     __syncthreads();
     if (tid < D::NC)
-      S[slot_of(ci, tid, T.nall)] = (s_red[0][tid] + s_red[1][tid] + s_red[2][tid] + s_red[3][tid]) * (kSampled ? 16.0 : 1.0);
+      S[slot_of(ci, tid, T.nall)] = s_red[0][tid] + s_red[1][tid] + s_red[2][tid] + s_red[3][tid];
+  }
+}
+
+// fp32 phase A: the same sample (16 of a chunk's 256 lines, weighted 16) and tfirst, one wave per chunk and
+// kSumsCPW chunks per wave with every load issued first — a block per chunk issued 2 KB and waited (66 us on C2,
+// latency-bound); lane l loads vectors f0 = 8 (16 (l / 8) + rot) + l % 8 and f0 + 1024 (lines l / 8 and
+// l / 8 + 8 of the sample), so the lanes of one parity hold the same chains and no LDS or barrier is needed.
+constexpr int kSumsCPW = 4;
+__global__ __launch_bounds__(256) void k_tn_sums_f32(const float* __restrict__ x, const adfl_slq_chunk* __restrict__ chunks,
+                                                     int64_t nall, int* __restrict__ tfirst, double* __restrict__ S) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t c0 = ((int64_t)blockIdx.x * 4 + wave) * kSumsCPW;
+  const u32x4* const x0 = (const u32x4*)((uintptr_t)x & ~(uintptr_t)15);  // a valid address for idle lanes
+  u32x4 r[kSumsCPW][2];
+  bool live[kSumsCPW];
+  int delta[kSumsCPW], lim[kSumsCPW], f0[kSumsCPW];
+#pragma unroll
+  for (int j = 0; j < kSumsCPW; ++j) {
+    const int64_t ci = c0 + j;
+    live[j] = false;
+    delta[j] = lim[j] = f0[j] = 0;
+    const u32x4* p0 = x0;
+    const u32x4* p1 = x0;
+    if (ci < nall) {
+      const Tensor T = tensor_of(chunks, (int)ci, nall);
+      if (lane == 0 && ci == T.first) tfirst[T.tensor] = (int)ci;
+      const ChunkGeo G = geo_of<ADFL_DTYPE_F32>(T, (int)ci, Split{1, T.n});
+      if (T.n > kShortMaxF32 && G.lim > 0) {
+        const View<ADFL_DTYPE_F32> v(x, T.base + G.c0e, G.lim);
+        live[j] = true;
+        delta[j] = v.delta;
+        lim[j] = G.lim;
+        f0[j] = 8 * (16 * (lane >> 3) + (int)((ci * 7) & 15)) + (lane & 7);
+        p0 = v.vb + (f0[j] < v.nvec ? f0[j] : v.nvec - 1);
+        p1 = v.vb + (f0[j] + 1024 < v.nvec ? f0[j] + 1024 : v.nvec - 1);
+      }
+    }
+    r[j][0] = ld_x(p0);
+    r[j][1] = ld_x(p1);
+  }
+#pragma unroll
+  for (int j = 0; j < kSumsCPW; ++j) {
+    if (!live[j]) continue;  // uniform over the wave
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int e = (f0[j] + 1024 * h) * 4 + p - delta[j];
+        const double d = (e >= 0 && e < lim[j]) ? (double)View<ADFL_DTYPE_F32>::elem(r[j][h], p) : 0.0;
+        acc[p] = __fma_rn(d, d, acc[p]);
+      }
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int o = 2; o < 64; o <<= 1) acc[p] += __shfl_xor(acc[p], o, 64);
+    if (lane < 2) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) S[slot_of(c0 + j, ((lane * 4 + p - delta[j]) % 8 + 8) % 8, nall)] = acc[p] * 16.0;
+    }
   }
 }
 
@@ -647,16 +704,6 @@ __global__ __launch_bounds__(256) void k_tn_grids(const adfl_slq_chunk* __restri
 // unless hi - k = +-1/2 (where the exact value decides, and a tie is possible) — and on g - 1, R(2 x^2 / u)
 // = 2 k + rint(2 (hi - k)), exact unless hi - k = +-1/4. A chunk where any lane meets one of those is listed
 // for k_tn_maps_exact: staged chain-major through LDS, each lane's 16 steps composed in order as maps.
-template <int DT>
-__device__ __forceinline__ void load_chunk(const View<DT>& v, int tid, u32x4 (&r)[View<DT>::NV]) {
-#pragma unroll
-  for (int i = 0; i < View<DT>::NV; ++i) {
-    const int f = tid + 256 * i;
-    const u32x4 q = ld_x(v.vb + (f < v.nvec ? f : v.nvec - 1));  // unconditional (index clamped): all loads in flight
-    r[i] = f < v.nvec ? q : u32x4{0u, 0u, 0u, 0u};
-  }
-}
-
 template <int DT>
 __global__ __launch_bounds__(256) void k_tn_maps(const void* __restrict__ x, const adfl_slq_chunk* __restrict__ chunks, int64_t nall,
                                                  int threads, Rec* __restrict__ recs, double4* __restrict__ maps,
@@ -820,8 +867,8 @@ __global__ __launch_bounds__(256) void k_tn_maps(const void* __restrict__ x, con
 // at or above 2^G, which then makes the total at least 2^23 u — never covered from A >= 2^23), summed in fp32
 // (exact below 2^24 u, at least that above). A tie leaves the residual x^2 - k at exactly +-u/2, which
 // fma(-x, x, k) returns exactly, so a chunk where some |residual| equals u/2 (rarely a rounding, not a tie) goes
-// to k_tn_maps_exact; so does a chunk whose chains are predicted on the subnormal grid. A NaN sets kNaN (S is
-// sampled for fp32, so it cannot tell phase D). One read of x; no fp64.
+// to k_tn_maps_exact; so does a chunk with a chain predicted on the subnormal grid. A NaN sets its tile's kNaN
+// (S is sampled for fp32, so it cannot tell phase D). One read of x; no fp64.
 __global__ __launch_bounds__(256) void k_tn_maps_f32(const float* __restrict__ x, const adfl_slq_chunk* __restrict__ chunks,
                                                      int64_t nall, Rec* __restrict__ recs, int* __restrict__ exact_list) {
   using V = View<ADFL_DTYPE_F32>;
@@ -839,34 +886,31 @@ __global__ __launch_bounds__(256) void k_tn_maps_f32(const float* __restrict__ x
   if (tid < 8) s_g[tid] = rec_g<false>(recs[slot_of(ci, tid, T.nall)]);
   if (tid == 0) s_slow = 0;
   __syncthreads();
-  // per position p: its chain's grids g (B0, h0) and g - 1 (B1, h1); a subnormal grid sends the chunk to the
-  // exact path (flag through sub)
-  float B0[EPV], h0[EPV], B1[EPV], h1[EPV];
-  bool sub = false;
+  // per position p: its chain's grids g and g - 1 as one pair (packed fp32: B = 2^g, 2^(g-1); h = the half-ulps)
+  f2v B[EPV], h[EPV];
 #pragma unroll
   for (int p = 0; p < EPV; ++p) {
-    const int c = ((tid * EPV + p - v.delta) % 8 + 8) % 8;
-    const int g = s_g[c];
-    sub |= g - 1 <= -126;
-    B0[p] = pow2f(g);
-    h0[p] = pow2fs(g - 24);
-    B1[p] = pow2f(g - 1 < -126 ? -126 : g - 1);  // (g - 1 < -126: not a grid; e1 is +inf below)
-    h1[p] = pow2fs(g - 25 < -149 ? -149 : g - 25);
+    const int g = s_g[((tid * EPV + p - v.delta) % 8 + 8) % 8];
+    B[p] = f2v{pow2f(g), pow2f(g - 1 < -126 ? -126 : g - 1)};  // (g - 1 < -126: not a grid; e1 is +inf below)
+    h[p] = f2v{pow2fs(g - 24), pow2fs(g - 25 < -149 ? -149 : g - 25)};
   }
-  float K0[EPV], K1[EPV];
-  bool fl[EPV], nan = false;
+  // per element: k = fma(x, x, B) - B and the residual fma(-x, x, k) on both grids (two packed fmas, a packed
+  // add, a packed accumulate); a half-ulp residual is a wave mask accumulated in scalar registers (one compare
+  // per grid). A NaN is left to propagate into K (every k >= 0, so K is NaN exactly when an input was).
+  f2v K[EPV];
+  unsigned long long fm[EPV];
 #pragma unroll
   for (int p = 0; p < EPV; ++p) {
-    K0[p] = K1[p] = 0.0f;
-    fl[p] = false;
+    K[p] = f2v{0.0f, 0.0f};
+    fm[p] = 0ull;
   }
   const auto step = [&](float xv, int p) {
-    const float k0 = __builtin_fmaf(xv, xv, B0[p]) - B0[p], k1 = __builtin_fmaf(xv, xv, B1[p]) - B1[p];
-    K0[p] += k0;
-    K1[p] += k1;
-    const float r0 = __builtin_fmaf(-xv, xv, k0), r1 = __builtin_fmaf(-xv, xv, k1);
-    fl[p] |= (__builtin_fabsf(r0) == h0[p]) | (__builtin_fabsf(r1) == h1[p]);
-    nan |= xv != xv;
+    const f2v xx = f2v{xv, xv};
+    const f2v k = __builtin_elementwise_fma(xx, xx, B[p]) - B[p];
+    K[p] += k;
+    const f2v rr = __builtin_elementwise_fma(-xx, xx, k);
+    fm[p] |= __ballot(__builtin_fabsf(rr.x) == h[p].x);
+    fm[p] |= __ballot(__builtin_fabsf(rr.y) == h[p].y);
   };
   if (v.delta == 0 && G.lim == kChunk) {  // a whole aligned chunk: no masks
 #pragma unroll
@@ -889,20 +933,17 @@ __global__ __launch_bounds__(256) void k_tn_maps_f32(const float* __restrict__ x
   for (int p = 0; p < EPV; ++p) {
 #pragma unroll
     for (int o = 2; o < 64; o <<= 1) {
-      K0[p] += __shfl_xor(K0[p], o, 64);
-      K1[p] += __shfl_xor(K1[p], o, 64);
+      K[p].x += __shfl_xor(K[p].x, o, 64);
+      K[p].y += __shfl_xor(K[p].y, o, 64);
     }
-    const unsigned long long b = __ballot(fl[p]);
-    fl[p] = (b & (0x5555555555555555ull << (lane & 1))) != 0ull;
   }
-  const bool anynan = __ballot(nan) != 0ull;
   if (lane < 2) {
 #pragma unroll
     for (int p = 0; p < EPV; ++p) {
       const int c = ((lane * EPV + p - v.delta) % 8 + 8) % 8;
-      s_k[wave][c][0] = K0[p];
-      s_k[wave][c][1] = K1[p];
-      s_fl[wave][c] = fl[p] | (anynan ? 2 : 0);
+      s_k[wave][c][0] = K[p].x;
+      s_k[wave][c][1] = K[p].y;
+      s_fl[wave][c] = (fm[p] & (0x5555555555555555ull << lane)) != 0ull;
     }
   }
   __syncthreads();
@@ -921,8 +962,9 @@ __global__ __launch_bounds__(256) void k_tn_maps_f32(const float* __restrict__ x
     const double q0 = (double)k0 * pow2(23 - g), q1 = (double)k1 * pow2(24 - g);
     const double e0 = q0 < (double)kNoK ? q0 : inf;
     const double e1 = (g - 1 >= -126 && q1 < (double)kNoK) ? q1 : inf;
-    if (((f & 1) || sub) && (e0 < Acc<false>::kTop || e1 < Acc<false>::kTop)) s_slow = 1;
-    recs[slot_of(ci, tid, T.nall)] = make_rec<false>(e0, e1, g, (f & 2) ? kNaN : 0u);
+    // a residual on the subnormal grid (g - 1 = -126) cannot show a tie: such a chain goes to the exact path
+    if ((f || g - 1 <= -126) && (e0 < Acc<false>::kTop || e1 < Acc<false>::kTop)) s_slow = 1;
+    recs[slot_of(ci, tid, T.nall)] = make_rec<false>(e0, e1, g, (k0 != k0 || k1 != k1) ? kNaN : 0u);
   }
   __syncthreads();
   if (tid == 0 && s_slow) exact_list[atomicAdd(exact_list - 1, 1)] = ci;  // the count sits just before the list
@@ -2032,7 +2074,11 @@ int launch(const void* x, const adfl_slq_chunk* chunks, int64_t nchunks, const i
 #endif
   }
   if (any_long) {
-    k_tn_sums<DT><<<(unsigned)nchunks, 256, 0, st>>>(x, chunks, nchunks, threads, s.tfirst, s.S);
+    if constexpr (DT == ADFL_DTYPE_F32)
+      k_tn_sums_f32<<<(unsigned)((nchunks + 4 * kSumsCPW - 1) / (4 * kSumsCPW)), 256, 0, st>>>((const float*)x, chunks, nchunks,
+                                                                                             s.tfirst, s.S);
+    else
+      k_tn_sums<DT><<<(unsigned)nchunks, 256, 0, st>>>(x, chunks, nchunks, threads, s.tfirst, s.S);
     k_tn_winsums<DT><<<dim3((unsigned)ntensors, 8, 8), 256, 0, st>>>(chunks, nchunks, s.tfirst, threads, s.S, s.wsum);
     k_tn_grids<DT><<<dim3((unsigned)ntensors, 8, 8), 256, 0, st>>>(chunks, nchunks, s.tfirst, threads, s.S, s.wsum, s.recs);
     if (hipError_t e = hipMemsetAsync(s.exact, 0, 4, st)) return (int)e;
