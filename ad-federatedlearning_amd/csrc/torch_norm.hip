@@ -39,9 +39,11 @@
 //   D  k_tn_chains: one wave per chain: windows 64 at a time on the exact accumulator's binade, the first one
 //      not covered tile by tile, the first tile not covered in segments of 1024 steps (lane sums or maps on
 //      G and G + 1, scanned; the lane that crosses runs its steps with fma); then k_tn_finish: the lane sum
-//      (fp16: piece sums in order), the tail, sqrt and the rounding to the dtype.
-// fp32 tensors up to kShortMax elements take the in-order walker (torch_norm_walk.h); other short tensors go
-// straight to D with every tile resolved in detail. DESIGN.md §10.
+//      (fp16: piece sums in order), the tail, sqrt and the rounding to the dtype. fp32 runs its segments with
+//      k_tn_short's short_segment and its window / tile scans in fp32 by DPP (integer totals below 2^24).
+// fp32 tensors up to kShortMaxF32 elements take k_tn_short (one block per tensor; ADFL_TN_WALKER builds: the
+// in-order walker, torch_norm_walk.h); other short tensors go straight to D with every tile resolved in detail.
+// DESIGN.md §10.
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 #include <hip/hip_fp16.h>
@@ -59,9 +61,9 @@ int launch_walk(const float* x, const adfl_slq_chunk* chunks, int64_t nchunks, f
 namespace adfl_tnx {
 
 #ifdef ADFL_TN_STATS  // tools/ref_norm_prof.py --stats builds: phase D counters per wave, printed per launch
-__device__ unsigned long long g_tn_stats[8][10];  // window descents, tiles in detail, segment rounds, cycles, cycles in
+__device__ unsigned long long g_tn_stats[8][12];  // window descents, tiles in detail, segment rounds, cycles, cycles in
 // detail, cycles waiting for segment loads, cycles in window descents, window scans, exact-path segment rounds,
-// cycles in segments
+// cycles in segments, cycles waiting for a window's records, cycles in window scans up to a tile in detail
 #define TN_STAT(i, v) do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_tn_stats[blockIdx.y & 7][i], (unsigned long long)(v)); } while (0)
 // k_tn_short's counters, summed over its waves: segments, rounds, exact-map rounds, lanes run with fma, G + 1
 // continuations that finished the segment, cycles in short_segment, cycles per wave, (unused), waves, cycles in
@@ -892,7 +894,7 @@ __global__ __launch_bounds__(256) void k_tn_maps_f32(const float* __restrict__ x
   for (int p = 0; p < EPV; ++p) {
     const int g = s_g[((tid * EPV + p - v.delta) % 8 + 8) % 8];
     B[p] = f2v{pow2f(g), pow2f(g - 1 < -126 ? -126 : g - 1)};  // (g - 1 < -126: not a grid; e1 is +inf below)
-    h[p] = f2v{pow2fs(g - 24), pow2fs(g - 25 < -149 ? -149 : g - 25)};
+    h[p] = f2v{pow2fs(g - 24 < -149 ? -149 : g - 24), pow2fs(g - 25 < -149 ? -149 : g - 25)};
   }
   // per element: k = fma(x, x, B) - B and the residual fma(-x, x, k) on both grids (two packed fmas, a packed
   // add, a packed accumulate); a half-ulp residual is a wave mask accumulated in scalar registers (one compare
@@ -1167,318 +1169,6 @@ __global__ __launch_bounds__(256) void k_tn_windows(const adfl_slq_chunk* __rest
   }
 }
 
-// ---- phase D
-// A segment (<= 1024 steps, lane l holding steps 16 l .. 16 l + 15) run from the exact accumulator acc.
-// fp32 accumulators, no tie possible in the wave: each lane's steps add a constant on the binade G and one
-// on G + 1 — both summed in one pass and scanned together, so the usual segment (one crossing) costs one
-// round: the first lane that leaves G runs its steps with fma, and the lanes after it are checked on G + 1
-// from the sums' differences. Otherwise (ties, two crossings, non-finite values) maps, lane by lane.
-template <int DT>
-__device__ __forceinline__ typename Acc<Dt<DT>::kWide>::T resolve_segment(const typename Dt<DT>::E (&v)[kLane],
-                                                                           typename Acc<Dt<DT>::kWide>::T acc, int lane) {
-  constexpr bool W = Dt<DT>::kWide;
-  using A_t = typename Acc<W>::T;
-  int start = 0;
-  for (;;) {
-    if (!__builtin_isfinite(acc)) {  // inf stays inf unless a NaN follows; NaN stays NaN
-      bool nan = false;
-#pragma unroll
-      for (int i = 0; i < kLane; ++i) nan |= __builtin_isnan(v[i]);
-      if (__ballot(nan && lane >= start)) acc = (A_t)__builtin_nan("");
-      return acc;
-    }
-    TN_STAT(2, 1);
-    const int G = grid_of(acc);
-    const double A = a_of(acc);
-    if constexpr (!W && Dt<DT>::kSq) {  // exact-square inputs: the lane maps on G and G + 1 in one pass
-      Map m0, m1;
-      lane_maps_pair<W, true>(v, G, +1, m0, m1);
-      if (lane < start) m0 = Map{0.0, 0.0};
-      const double Al = apply(wave_excl(m0, lane), A);
-      const double out = apply(m0, Al);
-      const unsigned long long ball = __ballot(lane >= start && !(out < Acc<W>::kTop));
-      if (ball == 0ull) return rebuild<W>(__shfl(out, 63, 64), G);
-      const int ls = __builtin_ctzll(ball);
-      A_t a = rebuild<W>(__shfl(Al, ls, 64), G);
-      if (lane == ls) {
-#pragma unroll
-        for (int i = 0; i < kLane; ++i) a = fma_t(v[i], v[i], a);
-      }
-      acc = __shfl(a, ls, 64);
-      start = ls + 1;
-      if (start == 64) return acc;
-      if (__builtin_isfinite(acc) && grid_of(acc) == G + 1) {  // on from lane ls + 1 with the maps on G + 1
-        const Map n1 = lane > ls ? m1 : Map{0.0, 0.0};
-        const double Al1 = apply(wave_excl(n1, lane), a_of(acc));
-        const double out1 = apply(n1, Al1);
-        if (__ballot(lane > ls && !(out1 < Acc<W>::kTop)) == 0ull) return rebuild<W>(__shfl(out1, 63, 64), G + 1);
-      }
-      continue;
-    }
-    if constexpr (!W) {
-      const double sc = pow2(23 - G);
-      double K0 = 0.0, K1 = 0.0;
-      bool maybe = false;
-#pragma unroll
-      for (int i = 0; i < kLane; ++i) {
-        const double d = (double)v[i];
-        const double x2 = d * (d * sc), h = x2 * 0.5, w = x2 * 2.0;
-        K0 += (x2 + kMagic) - kMagic;
-        K1 += (h + kMagic) - kMagic;
-        maybe |= ((w + kMagic) - kMagic) == w && w != 0.0;  // 2v an integer: a tie is possible (on G or G + 1)
-      }
-      if (__ballot(maybe) == 0ull) {
-        if (lane < start) K0 = K1 = 0.0;
-        double I0 = K0, I1 = K1;  // inclusive scans
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const double p0 = __shfl_up(I0, o, 64), p1 = __shfl_up(I1, o, 64);
-          if (lane >= o) {
-            I0 += p0;
-            I1 += p1;
-          }
-        }
-        const double out = A + I0, Al = out - K0;
-        const unsigned long long ball = __ballot(lane >= start && !(out < Acc<W>::kTop));
-        if (ball == 0ull) return rebuild<W>(__shfl(out, 63, 64), G);
-        const int ls = __builtin_ctzll(ball);
-        A_t a = rebuild<W>(__shfl(Al, ls, 64), G);
-        if (lane == ls) {
-#pragma unroll
-          for (int i = 0; i < kLane; ++i) a = fma_t(v[i], v[i], a);
-        }
-        acc = __shfl(a, ls, 64);
-        start = ls + 1;
-        if (start == 64) return acc;
-        // on from lane ls + 1 on G + 1: the K1 sums of lanes ls + 1 .. (exact while the total is below 2^53)
-        if (__builtin_isfinite(acc) && grid_of(acc) == G + 1 && G + 1 <= Acc<W>::kGmax &&
-            __shfl(I1, 63, 64) < 0x1p52) {
-          const double out1 = a_of(acc) + (I1 - __shfl(I1, ls, 64));
-          if (__ballot(lane > ls && !(out1 < Acc<W>::kTop)) == 0ull) return rebuild<W>(__shfl(out1, 63, 64), G + 1);
-        }
-        continue;
-      }
-    }
-    TN_STAT(8, 1);
-    Map m = lane_map_exact<W>(v, G);
-    if (lane < start) m = Map{0.0, 0.0};
-    const Map ex = wave_excl(m, lane);
-    const double Al = apply(ex, A);
-    const double out = apply(m, Al);
-    const bool bad = lane >= start && !(out < Acc<W>::kTop);
-    const unsigned long long ball = __ballot(bad);
-    if (ball == 0ull) return rebuild<W>(__shfl(out, 63, 64), G);
-    const int ls = __builtin_ctzll(ball);
-    const double As = __shfl(Al, ls, 64);
-    A_t a = rebuild<W>(As, G);
-    if (lane == ls) {
-#pragma unroll
-      for (int i = 0; i < kLane; ++i) a = fma_t(v[i], v[i], a);
-    }
-    acc = __shfl(a, ls, 64);
-    start = ls + 1;
-    if (start == 64) return acc;
-  }
-}
-
-template <int DT>
-__device__ __forceinline__ void load_seg(const void* x, const Tensor& T, int c, Split sp, int64_t s0, int64_t s1,
-                                         int lane, typename Dt<DT>::E (&v)[kLane]) {
-#pragma unroll
-  for (int i = 0; i < kLane; ++i) {
-    const int64_t s = s0 + lane * kLane + i;
-    const typename Dt<DT>::E e = Dt<DT>::ld(x, elem_of<DT>(T, c, sp, s < s1 ? s : s1 - 1));  // clamped
-    v[i] = s < s1 ? e : (typename Dt<DT>::E)0;
-  }
-}
-
-template <int DT>
-__device__ typename Acc<Dt<DT>::kWide>::T resolve_tile(const void* x, const Tensor& T, int c, Split sp, const Tile& tl,
-                                                       typename Acc<Dt<DT>::kWide>::T acc, int lane) {
-  typename Dt<DT>::E v[kLane];
-  TN_STAT(1, 1);
-#ifdef ADFL_TN_STATS
-  const long long c0 = clock64();
-#endif
-  for (int64_t s0 = tl.s0; s0 < tl.s1; s0 += kSeg) {
-    load_seg<DT>(x, T, c, sp, s0, s0 + kSeg < tl.s1 ? s0 + kSeg : tl.s1, lane, v);
-#ifdef ADFL_TN_STATS
-    {
-      const long long l0 = clock64();
-      float z = 0.0f;
-#pragma unroll
-      for (int i = 0; i < kLane; ++i) z += (float)v[i];
-      __asm__ volatile("" ::"v"(z));
-      TN_STAT(5, clock64() - l0);
-    }
-#endif
-#ifdef ADFL_TN_STATS
-    const long long r0 = clock64();
-#endif
-    acc = resolve_segment<DT>(v, acc, lane);
-#ifdef ADFL_TN_STATS
-    TN_STAT(9, clock64() - r0);
-#endif
-  }
-#ifdef ADFL_TN_STATS
-  TN_STAT(4, clock64() - c0);
-#endif
-  return acc;
-}
-
-// One window (kWinTiles tiles of chain c from tile w0; lane l holds tiles l * kTPL ..) from the exact acc:
-// scan the tiles' maps on acc's binade; the first tile not covered (a crossing, a miss of the predictor, a
-// large step) is resolved in detail; and on from the tile after it.
-template <int DT>
-__device__ typename Acc<Dt<DT>::kWide>::T resolve_window(const void* x, const Tensor& T, int c, Split sp,
-                                                         const double* S, const Rec* recs, const double4* maps,
-                                                         int64_t w0, int64_t nt, typename Acc<Dt<DT>::kWide>::T acc,
-                                                         int lane) {
-  constexpr bool W = Dt<DT>::kWide;
-  using A_t = typename Acc<W>::T;
-  Rec r[kTPL];
-  double4 mp[kTPL];  // the side maps (read for every tile, so the loads are all in flight; used where kSide)
-#pragma unroll
-  for (int k = 0; k < kTPL; ++k) {
-    const int64_t t = w0 + lane * kTPL + k;
-    const int64_t slot = tile_of<DT>(T, c, sp, t < nt ? t : nt - 1).slot;  // clamped: loads in flight
-    const Rec q = recs[slot];
-    mp[k] = maps[slot];
-    r[k] = t < nt ? q : Rec{kPad << 24, 0u};
-  }
-  int start = 0;  // window tiles before it are done
-  const int wlen = nt - w0 < kWinTiles ? (int)(nt - w0) : kWinTiles;
-  while (start < wlen) {
-    TN_STAT(7, 1);
-    if (!__builtin_isfinite(acc)) {  // inf stays inf unless a NaN follows: the remaining tiles' sums say
-      bool nan = false;
-      for (int64_t u = w0 + start + lane; u < nt; u += 64) {
-        const int64_t sl = tile_of<DT>(T, c, sp, u).slot;
-        nan |= __builtin_isnan(S[sl]) || (rec_flags(recs[sl]) & kNaN);
-      }
-      if (__ballot(nan)) acc = (A_t)__builtin_nan("");
-      return acc;
-    }
-    const int G = grid_of(acc);
-    const double A = a_of(acc);
-    bool side = false;
-#pragma unroll
-    for (int k = 0; k < kTPL; ++k) side |= (rec_flags(r[k]) & kSide) && lane * kTPL + k >= start;
-    const bool any_side = __ballot(side) != 0ull;
-    const auto tile_map = [&](int k) -> Map {
-      const Rec q = r[k];
-      const uint32_t fl = rec_flags(q);
-      if ((fl & kPad) || lane * kTPL + k < start) return Map{0.0, 0.0};
-      const int j = rec_g<W>(q) - G;
-      if (j != 0 && j != 1) return Map{__builtin_inf(), __builtin_inf()};
-      if (fl & kSide) return j == 0 ? Map{mp[k].x, mp[k].y} : Map{mp[k].z, mp[k].w};
-      const double K = rec_k(q, j);
-      return Map{K, K};
-    };
-    double Al, out;
-    if (!any_side) {
-      double K = 0.0;
-#pragma unroll
-      for (int k = 0; k < kTPL; ++k) K += tile_map(k).e;
-      Al = A + wave_excl_sum(K, lane);
-      out = Al + K;
-    } else {
-      Map m{0.0, 0.0};
-#pragma unroll
-      for (int k = 0; k < kTPL; ++k) m = compose(m, tile_map(k));
-      Al = apply(wave_excl(m, lane), A);
-      out = apply(m, Al);
-    }
-    const unsigned long long ball = __ballot(!(out < Acc<W>::kTop));
-    if (ball == 0ull) return rebuild<W>(__shfl(out, 63, 64), G);
-    // the first tile not covered: each lane's first tile whose map leaves the binade from its Al
-    int kb = kTPL;
-    double Ab = Al;
-#pragma unroll
-    for (int k = 0; k < kTPL; ++k) {
-      if (kb == kTPL) {
-        const double nxt = apply(tile_map(k), Ab);
-        if (!(nxt < Acc<W>::kTop)) kb = k;
-        else Ab = nxt;
-      }
-    }
-    const int ls = __builtin_ctzll(ball);
-    const int tb = ls * kTPL + __shfl(kb, ls, 64);
-    acc = rebuild<W>(__shfl(Ab, ls, 64), G);
-    acc = resolve_tile<DT>(x, T, c, sp, tile_of<DT>(T, c, sp, w0 + tb), acc, lane);
-    start = tb + 1;
-  }
-  return acc;
-}
-
-template <int DT>
-__device__ typename Acc<Dt<DT>::kWide>::T resolve_chain(const void* x, const Tensor& T, int c, Split sp,
-                                                        const double* S, const Rec* recs, const double4* maps,
-                                                        const int* wing, const double4* winmaps, bool use_recs,
-                                                        int lane) {
-  constexpr bool W = Dt<DT>::kWide;
-  using A_t = typename Acc<W>::T;
-  const int64_t nt = chain_tiles<DT>(T, c, sp);
-  A_t acc = (A_t)0;
-  if (!use_recs) {
-    for (int64_t t = 0; t < nt; ++t) acc = resolve_tile<DT>(x, T, c, sp, tile_of<DT>(T, c, sp, t), acc, lane);
-    return acc;
-  }
-  // Windows 64 at a time (lane l: window wb + l), each as its summary map on acc's binade (phase C2); the
-  // first window not covered is resolved tile by tile (resolve_window), then on from the window after it.
-  const int64_t nw = (nt + kWinTiles - 1) / kWinTiles;
-  for (int64_t wb = 0; wb < nw; wb += 64) {
-    const int64_t w = wb + lane;
-    const bool valid = w < nw;
-    const int64_t wslot = tile_of<DT>(T, c, sp, (valid ? w : nw - 1) * kWinTiles).slot;  // clamped
-    const int gw = wing[wslot];
-    const double4 wm = winmaps[wslot];
-    int wstart = 0;
-    const int wlen = nw - wb < 64 ? (int)(nw - wb) : 64;
-    while (wstart < wlen) {
-      if (!__builtin_isfinite(acc)) {  // inf stays inf unless a NaN follows: the remaining tiles' sums say
-        bool nan = false;
-        for (int64_t u = (wb + wstart) * kWinTiles + lane; u < nt; u += 64)
-          nan |= __builtin_isnan(S[tile_of<DT>(T, c, sp, u).slot]) || (rec_flags(recs[tile_of<DT>(T, c, sp, u).slot]) & kNaN);
-        if (__ballot(nan)) acc = (A_t)__builtin_nan("");
-        return acc;
-      }
-      const int G = grid_of(acc);
-      const double A = a_of(acc);
-      Map m{0.0, 0.0};
-      if (valid && lane >= wstart) {
-        const int j = gw - G;
-        m = j == 0 ? Map{wm.x, wm.y} : (j == 1 ? Map{wm.z, wm.w} : Map{__builtin_inf(), __builtin_inf()});
-      }
-      double Al, out;
-      if (__ballot(m.e != m.o) == 0ull) {
-        Al = A + wave_excl_sum(m.e, lane);
-        out = Al + m.e;
-      } else {
-        Al = apply(wave_excl(m, lane), A);
-        out = apply(m, Al);
-      }
-      const unsigned long long ball = __ballot(!(out < Acc<W>::kTop));
-      if (ball == 0ull) {
-        acc = rebuild<W>(__shfl(out, 63, 64), G);
-        break;
-      }
-      const int ls = __builtin_ctzll(ball);
-      acc = rebuild<W>(__shfl(Al, ls, 64), G);
-      TN_STAT(0, 1);
-#ifdef ADFL_TN_STATS
-      const long long w0c = clock64();
-#endif
-      acc = resolve_window<DT>(x, T, c, sp, S, recs, maps, (wb + ls) * kWinTiles, nt, acc, lane);
-#ifdef ADFL_TN_STATS
-      TN_STAT(6, clock64() - w0c);
-#endif
-      wstart = ls + 1;
-    }
-  }
-  return acc;
-}
-
 // ---- short fp32 tensors: k_tn_short, one block per tensor, one wave per chain, one launch
 // The fp32 form of the binade model, with no fp64 and no integer conversion. On binade G (ulp u = 2^(G-23),
 // A = acc / u in [2^23, 2^24); G = -126 also holds the subnormals) a step adds R(x^2 / u) * u, which is exactly
@@ -1673,6 +1363,385 @@ __device__ __forceinline__ float short_segment(const float (&v)[kSL], float acc,
     SH_STAT(3, 1);
     acc = lane_fma(v, acc + lane_f(I1, l1 - 1), lane, l1);
     start = l1 + 1;
+  }
+  return acc;
+}
+
+// ---- phase D
+// A segment (<= 1024 steps, lane l holding steps 16 l .. 16 l + 15) run from the exact accumulator acc.
+// fp32 accumulators, no tie possible in the wave: each lane's steps add a constant on the binade G and one
+// on G + 1 — both summed in one pass and scanned together, so the usual segment (one crossing) costs one
+// round: the first lane that leaves G runs its steps with fma, and the lanes after it are checked on G + 1
+// from the sums' differences. Otherwise (ties, two crossings, non-finite values) maps, lane by lane.
+template <int DT>
+__device__ __forceinline__ typename Acc<Dt<DT>::kWide>::T resolve_segment(const typename Dt<DT>::E (&v)[kLane],
+                                                                           typename Acc<Dt<DT>::kWide>::T acc, int lane) {
+  constexpr bool W = Dt<DT>::kWide;
+  using A_t = typename Acc<W>::T;
+  int start = 0;
+  for (;;) {
+    if (!__builtin_isfinite(acc)) {  // inf stays inf unless a NaN follows; NaN stays NaN
+      bool nan = false;
+#pragma unroll
+      for (int i = 0; i < kLane; ++i) nan |= __builtin_isnan(v[i]);
+      if (__ballot(nan && lane >= start)) acc = (A_t)__builtin_nan("");
+      return acc;
+    }
+    TN_STAT(2, 1);
+    const int G = grid_of(acc);
+    const double A = a_of(acc);
+    if constexpr (!W && Dt<DT>::kSq) {  // exact-square inputs: the lane maps on G and G + 1 in one pass
+      Map m0, m1;
+      lane_maps_pair<W, true>(v, G, +1, m0, m1);
+      if (lane < start) m0 = Map{0.0, 0.0};
+      const double Al = apply(wave_excl(m0, lane), A);
+      const double out = apply(m0, Al);
+      const unsigned long long ball = __ballot(lane >= start && !(out < Acc<W>::kTop));
+      if (ball == 0ull) return rebuild<W>(__shfl(out, 63, 64), G);
+      const int ls = __builtin_ctzll(ball);
+      A_t a = rebuild<W>(__shfl(Al, ls, 64), G);
+      if (lane == ls) {
+#pragma unroll
+        for (int i = 0; i < kLane; ++i) a = fma_t(v[i], v[i], a);
+      }
+      acc = __shfl(a, ls, 64);
+      start = ls + 1;
+      if (start == 64) return acc;
+      if (__builtin_isfinite(acc) && grid_of(acc) == G + 1) {  // on from lane ls + 1 with the maps on G + 1
+        const Map n1 = lane > ls ? m1 : Map{0.0, 0.0};
+        const double Al1 = apply(wave_excl(n1, lane), a_of(acc));
+        const double out1 = apply(n1, Al1);
+        if (__ballot(lane > ls && !(out1 < Acc<W>::kTop)) == 0ull) return rebuild<W>(__shfl(out1, 63, 64), G + 1);
+      }
+      continue;
+    }
+    if constexpr (!W) {
+      const double sc = pow2(23 - G);
+      double K0 = 0.0, K1 = 0.0;
+      bool maybe = false;
+#pragma unroll
+      for (int i = 0; i < kLane; ++i) {
+        const double d = (double)v[i];
+        const double x2 = d * (d * sc), h = x2 * 0.5, w = x2 * 2.0;
+        K0 += (x2 + kMagic) - kMagic;
+        K1 += (h + kMagic) - kMagic;
+        maybe |= ((w + kMagic) - kMagic) == w && w != 0.0;  // 2v an integer: a tie is possible (on G or G + 1)
+      }
+      if (__ballot(maybe) == 0ull) {
+        if (lane < start) K0 = K1 = 0.0;
+        double I0 = K0, I1 = K1;  // inclusive scans
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const double p0 = __shfl_up(I0, o, 64), p1 = __shfl_up(I1, o, 64);
+          if (lane >= o) {
+            I0 += p0;
+            I1 += p1;
+          }
+        }
+        const double out = A + I0, Al = out - K0;
+        const unsigned long long ball = __ballot(lane >= start && !(out < Acc<W>::kTop));
+        if (ball == 0ull) return rebuild<W>(__shfl(out, 63, 64), G);
+        const int ls = __builtin_ctzll(ball);
+        A_t a = rebuild<W>(__shfl(Al, ls, 64), G);
+        if (lane == ls) {
+#pragma unroll
+          for (int i = 0; i < kLane; ++i) a = fma_t(v[i], v[i], a);
+        }
+        acc = __shfl(a, ls, 64);
+        start = ls + 1;
+        if (start == 64) return acc;
+        // on from lane ls + 1 on G + 1: the K1 sums of lanes ls + 1 .. (exact while the total is below 2^53)
+        if (__builtin_isfinite(acc) && grid_of(acc) == G + 1 && G + 1 <= Acc<W>::kGmax &&
+            __shfl(I1, 63, 64) < 0x1p52) {
+          const double out1 = a_of(acc) + (I1 - __shfl(I1, ls, 64));
+          if (__ballot(lane > ls && !(out1 < Acc<W>::kTop)) == 0ull) return rebuild<W>(__shfl(out1, 63, 64), G + 1);
+        }
+        continue;
+      }
+    }
+    TN_STAT(8, 1);
+    Map m = lane_map_exact<W>(v, G);
+    if (lane < start) m = Map{0.0, 0.0};
+    const Map ex = wave_excl(m, lane);
+    const double Al = apply(ex, A);
+    const double out = apply(m, Al);
+    const bool bad = lane >= start && !(out < Acc<W>::kTop);
+    const unsigned long long ball = __ballot(bad);
+    if (ball == 0ull) return rebuild<W>(__shfl(out, 63, 64), G);
+    const int ls = __builtin_ctzll(ball);
+    const double As = __shfl(Al, ls, 64);
+    A_t a = rebuild<W>(As, G);
+    if (lane == ls) {
+#pragma unroll
+      for (int i = 0; i < kLane; ++i) a = fma_t(v[i], v[i], a);
+    }
+    acc = __shfl(a, ls, 64);
+    start = ls + 1;
+    if (start == 64) return acc;
+  }
+}
+
+template <int DT>
+__device__ __forceinline__ void load_seg(const void* x, const Tensor& T, int c, Split sp, int64_t s0, int64_t s1,
+                                         int lane, typename Dt<DT>::E (&v)[kLane]) {
+#pragma unroll
+  for (int i = 0; i < kLane; ++i) {
+    const int64_t s = s0 + lane * kLane + i;
+    const typename Dt<DT>::E e = Dt<DT>::ld(x, elem_of<DT>(T, c, sp, s < s1 ? s : s1 - 1));  // clamped
+    v[i] = s < s1 ? e : (typename Dt<DT>::E)0;
+  }
+}
+
+template <int DT>
+__device__ typename Acc<Dt<DT>::kWide>::T resolve_tile(const void* x, const Tensor& T, int c, Split sp, const Tile& tl,
+                                                       typename Acc<Dt<DT>::kWide>::T acc, int lane) {
+  typename Dt<DT>::E v[kLane];
+  TN_STAT(1, 1);
+#ifdef ADFL_TN_STATS
+  const long long c0 = clock64();
+#endif
+  for (int64_t s0 = tl.s0; s0 < tl.s1; s0 += kSeg) {
+    load_seg<DT>(x, T, c, sp, s0, s0 + kSeg < tl.s1 ? s0 + kSeg : tl.s1, lane, v);
+#ifdef ADFL_TN_STATS
+    {
+      const long long l0 = clock64();
+      float z = 0.0f;
+#pragma unroll
+      for (int i = 0; i < kLane; ++i) z += (float)v[i];
+      __asm__ volatile("" ::"v"(z));
+      TN_STAT(5, clock64() - l0);
+    }
+#endif
+#ifdef ADFL_TN_STATS
+    const long long r0 = clock64();
+#endif
+    if constexpr (DT == ADFL_DTYPE_F32 && kSL == kLane) {  // k_tn_short's fp32 rounds (no fp64, DPP scans), same answer
+#ifdef ADFL_TN_STATS
+      unsigned long long shs[11] = {};
+#endif
+      acc = short_segment(v, acc, lane SH_PASS);
+    } else {
+      acc = resolve_segment<DT>(v, acc, lane);
+    }
+#ifdef ADFL_TN_STATS
+    TN_STAT(9, clock64() - r0);
+#endif
+  }
+#ifdef ADFL_TN_STATS
+  TN_STAT(4, clock64() - c0);
+#endif
+  return acc;
+}
+
+// One window (kWinTiles tiles of chain c from tile w0; lane l holds tiles l * kTPL ..) from the exact acc:
+// scan the tiles' maps on acc's binade; the first tile not covered (a crossing, a miss of the predictor, a
+// large step) is resolved in detail; and on from the tile after it.
+template <int DT>
+__device__ typename Acc<Dt<DT>::kWide>::T resolve_window(const void* x, const Tensor& T, int c, Split sp,
+                                                         const double* S, const Rec* recs, const double4* maps,
+                                                         int64_t w0, int64_t nt, typename Acc<Dt<DT>::kWide>::T acc,
+                                                         int lane) {
+  constexpr bool W = Dt<DT>::kWide;
+  using A_t = typename Acc<W>::T;
+  Rec r[kTPL];
+  double4 mp[kTPL];  // the side maps (read for every tile, so the loads are all in flight; used where kSide)
+#pragma unroll
+  for (int k = 0; k < kTPL; ++k) {
+    const int64_t t = w0 + lane * kTPL + k;
+    const int64_t slot = tile_of<DT>(T, c, sp, t < nt ? t : nt - 1).slot;  // clamped: loads in flight
+    const Rec q = recs[slot];
+    mp[k] = maps[slot];
+    r[k] = t < nt ? q : Rec{kPad << 24, 0u};
+  }
+#ifdef ADFL_TN_STATS
+  {
+    const long long l0 = clock64();
+    uint32_t z = 0;
+#pragma unroll
+    for (int k = 0; k < kTPL; ++k) z ^= r[k].w0 ^ r[k].w1 ^ (uint32_t)__double_as_longlong(mp[k].x);
+    __asm__ volatile("" ::"v"(z));
+    TN_STAT(10, clock64() - l0);
+  }
+#endif
+  int start = 0;  // window tiles before it are done
+  const int wlen = nt - w0 < kWinTiles ? (int)(nt - w0) : kWinTiles;
+  while (start < wlen) {
+    TN_STAT(7, 1);
+#ifdef ADFL_TN_STATS
+    const long long sc0 = clock64();
+#endif
+    if (!__builtin_isfinite(acc)) {  // inf stays inf unless a NaN follows: the remaining tiles' sums say
+      bool nan = false;
+      for (int64_t u = w0 + start + lane; u < nt; u += 64) {
+        const int64_t sl = tile_of<DT>(T, c, sp, u).slot;
+        nan |= __builtin_isnan(S[sl]) || (rec_flags(recs[sl]) & kNaN);
+      }
+      if (__ballot(nan)) acc = (A_t)__builtin_nan("");
+      return acc;
+    }
+    const int G = grid_of(acc);
+    const double A = a_of(acc);
+    bool side = false;
+#pragma unroll
+    for (int k = 0; k < kTPL; ++k) side |= (rec_flags(r[k]) & kSide) && lane * kTPL + k >= start;
+    const bool any_side = __ballot(side) != 0ull;
+    const auto tile_map = [&](int k) -> Map {
+      const Rec q = r[k];
+      const uint32_t fl = rec_flags(q);
+      if ((fl & kPad) || lane * kTPL + k < start) return Map{0.0, 0.0};
+      const int j = rec_g<W>(q) - G;
+      if (j != 0 && j != 1) return Map{__builtin_inf(), __builtin_inf()};
+      if (fl & kSide) return j == 0 ? Map{mp[k].x, mp[k].y} : Map{mp[k].z, mp[k].w};
+      const double K = rec_k(q, j);
+      return Map{K, K};
+    };
+    if constexpr (!W) {
+      if (!any_side) {  // fp32 accumulators: the DPP scan in fp32, as in resolve_chain
+        float Kk[kTPL], K = 0.0f;
+#pragma unroll
+        for (int k = 0; k < kTPL; ++k) {
+          Kk[k] = (float)tile_map(k).e;
+          K += Kk[k];
+        }
+        const float Af = (float)A, I = wave_incl_f(K), o = Af + I;
+        const unsigned long long ball = __ballot(!(o < 0x1p24f));
+        if (ball == 0ull) return rebuild<W>((double)lane_f(o, 63), G);
+        const int ls = __builtin_ctzll(ball);
+        float Ab = ls > 0 ? Af + lane_f(I, ls - 1) : Af;  // lane ls's start, exact (wave-uniform)
+        int kb = kTPL;
+#pragma unroll
+        for (int k = 0; k < kTPL; ++k) {
+          if (kb == kTPL) {
+            const float nxt = Ab + Kk[k];
+            if (!(nxt < 0x1p24f)) kb = k;
+            else Ab = nxt;
+          }
+        }
+        const int tb = ls * kTPL + __builtin_amdgcn_readlane(kb, ls);
+        acc = rebuild<W>((double)lane_f(Ab, ls), G);
+        TN_STAT(11, clock64() - sc0);
+        acc = resolve_tile<DT>(x, T, c, sp, tile_of<DT>(T, c, sp, w0 + tb), acc, lane);
+        start = tb + 1;
+        continue;
+      }
+    }
+    double Al, out;
+    if (!any_side) {
+      double K = 0.0;
+#pragma unroll
+      for (int k = 0; k < kTPL; ++k) K += tile_map(k).e;
+      Al = A + wave_excl_sum(K, lane);
+      out = Al + K;
+    } else {
+      Map m{0.0, 0.0};
+#pragma unroll
+      for (int k = 0; k < kTPL; ++k) m = compose(m, tile_map(k));
+      Al = apply(wave_excl(m, lane), A);
+      out = apply(m, Al);
+    }
+    const unsigned long long ball = __ballot(!(out < Acc<W>::kTop));
+    if (ball == 0ull) return rebuild<W>(__shfl(out, 63, 64), G);
+    // the first tile not covered: each lane's first tile whose map leaves the binade from its Al
+    int kb = kTPL;
+    double Ab = Al;
+#pragma unroll
+    for (int k = 0; k < kTPL; ++k) {
+      if (kb == kTPL) {
+        const double nxt = apply(tile_map(k), Ab);
+        if (!(nxt < Acc<W>::kTop)) kb = k;
+        else Ab = nxt;
+      }
+    }
+    const int ls = __builtin_ctzll(ball);
+    const int tb = ls * kTPL + __shfl(kb, ls, 64);
+    acc = rebuild<W>(__shfl(Ab, ls, 64), G);
+    TN_STAT(11, clock64() - sc0);
+    acc = resolve_tile<DT>(x, T, c, sp, tile_of<DT>(T, c, sp, w0 + tb), acc, lane);
+    start = tb + 1;
+  }
+  return acc;
+}
+
+template <int DT>
+__device__ typename Acc<Dt<DT>::kWide>::T resolve_chain(const void* x, const Tensor& T, int c, Split sp,
+                                                        const double* S, const Rec* recs, const double4* maps,
+                                                        const int* wing, const double4* winmaps, bool use_recs,
+                                                        int lane) {
+  constexpr bool W = Dt<DT>::kWide;
+  using A_t = typename Acc<W>::T;
+  const int64_t nt = chain_tiles<DT>(T, c, sp);
+  A_t acc = (A_t)0;
+  if (!use_recs) {
+    for (int64_t t = 0; t < nt; ++t) acc = resolve_tile<DT>(x, T, c, sp, tile_of<DT>(T, c, sp, t), acc, lane);
+    return acc;
+  }
+  // Windows 64 at a time (lane l: window wb + l), each as its summary map on acc's binade (phase C2); the
+  // first window not covered is resolved tile by tile (resolve_window), then on from the window after it.
+  const int64_t nw = (nt + kWinTiles - 1) / kWinTiles;
+  for (int64_t wb = 0; wb < nw; wb += 64) {
+    const int64_t w = wb + lane;
+    const bool valid = w < nw;
+    const int64_t wslot = tile_of<DT>(T, c, sp, (valid ? w : nw - 1) * kWinTiles).slot;  // clamped
+    const int gw = wing[wslot];
+    const double4 wm = winmaps[wslot];
+    int wstart = 0;
+    const int wlen = nw - wb < 64 ? (int)(nw - wb) : 64;
+    while (wstart < wlen) {
+      if (!__builtin_isfinite(acc)) {  // inf stays inf unless a NaN follows: the remaining tiles' sums say
+        bool nan = false;
+        for (int64_t u = (wb + wstart) * kWinTiles + lane; u < nt; u += 64)
+          nan |= __builtin_isnan(S[tile_of<DT>(T, c, sp, u).slot]) || (rec_flags(recs[tile_of<DT>(T, c, sp, u).slot]) & kNaN);
+        if (__ballot(nan)) acc = (A_t)__builtin_nan("");
+        return acc;
+      }
+      const int G = grid_of(acc);
+      const double A = a_of(acc);
+      Map m{0.0, 0.0};
+      if (valid && lane >= wstart) {
+        const int j = gw - G;
+        m = j == 0 ? Map{wm.x, wm.y} : (j == 1 ? Map{wm.z, wm.w} : Map{__builtin_inf(), __builtin_inf()});
+      }
+      const bool sums = __ballot(m.e != m.o) == 0ull;
+      unsigned long long ball;
+      int ls;
+      if (!W && sums) {
+        // fp32 accumulators: integer totals, exact in fp32 below 2^24 and at least 2^24 above (terms >= 0, RN
+        // monotone — k_tn_short's argument), so the scan is k_tn_short's DPP one: no fp64, no shuffles
+        const float Af = (float)A, I = wave_incl_f((float)m.e), o = Af + I;
+        ball = __ballot(!(o < 0x1p24f));
+        if (ball == 0ull) {
+          acc = rebuild<W>((double)lane_f(o, 63), G);
+          break;
+        }
+        ls = __builtin_ctzll(ball);
+        acc = rebuild<W>((double)(ls > 0 ? Af + lane_f(I, ls - 1) : Af), G);
+      } else {
+        double Al, out;
+        if (sums) {
+          Al = A + wave_excl_sum(m.e, lane);
+          out = Al + m.e;
+        } else {
+          Al = apply(wave_excl(m, lane), A);
+          out = apply(m, Al);
+        }
+        ball = __ballot(!(out < Acc<W>::kTop));
+        if (ball == 0ull) {
+          acc = rebuild<W>(__shfl(out, 63, 64), G);
+          break;
+        }
+        ls = __builtin_ctzll(ball);
+        acc = rebuild<W>(__shfl(Al, ls, 64), G);
+      }
+      TN_STAT(0, 1);
+#ifdef ADFL_TN_STATS
+      const long long w0c = clock64();
+#endif
+      acc = resolve_window<DT>(x, T, c, sp, S, recs, maps, (wb + ls) * kWinTiles, nt, acc, lane);
+#ifdef ADFL_TN_STATS
+      TN_STAT(6, clock64() - w0c);
+#endif
+      wstart = ls + 1;
+    }
   }
   return acc;
 }
@@ -1970,10 +2039,10 @@ __global__ __launch_bounds__(64) void k_tn_finish(const void* __restrict__ x, co
   if (blockIdx.x == 0) {
     for (int w = 0; w < 8; ++w) {
       printf("tn_stats chain %d: windows %llu tiles %llu rounds %llu cycles %llu detail %llu segload %llu windesc %llu"
-             " winscans %llu exactrounds %llu segcycles %llu\n", w, g_tn_stats[w][0], g_tn_stats[w][1], g_tn_stats[w][2],
-             g_tn_stats[w][3], g_tn_stats[w][4], g_tn_stats[w][5], g_tn_stats[w][6], g_tn_stats[w][7], g_tn_stats[w][8],
-             g_tn_stats[w][9]);
-      for (int i = 0; i < 10; ++i) g_tn_stats[w][i] = 0;
+             " winscans %llu exactrounds %llu segcycles %llu recwait %llu scancycles %llu\n", w, g_tn_stats[w][0],
+             g_tn_stats[w][1], g_tn_stats[w][2], g_tn_stats[w][3], g_tn_stats[w][4], g_tn_stats[w][5], g_tn_stats[w][6],
+             g_tn_stats[w][7], g_tn_stats[w][8], g_tn_stats[w][9], g_tn_stats[w][10], g_tn_stats[w][11]);
+      for (int i = 0; i < 12; ++i) g_tn_stats[w][i] = 0;
     }
   }
 #endif
