@@ -210,6 +210,41 @@ def _codec_encode(codec: str, x_dev, lay, bits: int, uniforms, seed: int, levels
     return lv, sg
 
 
+def _range_encode_args(sub, dev) -> Tuple[int, int, int, int, int, int]:
+    """A sub-layout's fixed arguments for _range_encode (cached on it): (chunk table, nchunks, tfirst list,
+    ntensors, norm kinds, norm scratch bytes)."""
+    cache = sub.__dict__.setdefault("_range_encode_args", {})
+    a = cache.get(dev.index)
+    if a is None:
+        L = _lib.load()
+        short_max = L.adfl_torch_norm_short_max_dt(sops.DTYPE_F32)
+        kinds = (1 if int(sub.sizes.min()) <= short_max else 0) | (2 if int(sub.sizes.max()) > short_max else 0)
+        a = cache[dev.index] = (sub.device_chunks(dev).data_ptr(), sub.nchunks, sub.device_tfirst(dev).data_ptr(),
+                                sub.ntensors, kinds, int(L.adfl_torch_norm_scratch_bytes(sub.nchunks, sub.ntensors)))
+    return a
+
+
+def _range_encode(codec: str, x_dev, sub, bits: int, seed: int, levels, signs, norms, made: int, ws, st) -> None:
+    """_codec_encode of QSGD / CNAT with the reference's norm and Philox uniforms for one staging range, as
+    direct native calls on the sub-layout's cached arguments: the same launches (adfl_torch_norms_work, then
+    adfl_qsgd_quantize_batched / adfl_cnat_encode_batched_work) and bytes as the sops wrappers, without their
+    per-call checks and allocations (~60 -> ~15 us of host time per range)."""
+    L = _lib.load()
+    dev = x_dev.device
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    cp, nc, tp, nt, kinds, need = _range_encode_args(sub, dev)
+    nd = norms.data_ptr() + 4 * made
+    xd = x_dev.data_ptr()
+    if codec == "cnat":   # the exponents do not depend on the norm: encode, then the reference's norms over it
+        wp, nw = sops._work(sub, dev)
+        check(L.adfl_cnat_encode_batched_work(xd, cp, nc, wp, nw, bits, 0, seed, 0, ws.data_ptr(), ws.numel(),
+                                              levels.data_ptr(), signs.data_ptr(), nd, sh))
+    scratch = st.buf("tn_scratch", need, torch.uint8)   # stream-ordered reuse: every range runs on this stream
+    check(L.adfl_torch_norms_work(sops.DTYPE_F32, xd, cp, nc, tp, nt, kinds, 1, scratch.data_ptr(), need, None, nd, sh))
+    if codec == "qsgd":
+        check(L.adfl_qsgd_quantize_batched(xd, cp, nc, bits, nd, 0, seed, 0, levels.data_ptr(), signs.data_ptr(), sh))
+
+
 def _sub_layout(lay, t0: int, t1: int):
     """Tensors [t0, t1) of `lay` at their bucket offsets, as a layout of their own (cached on `lay`: the staging
     ranges of a layout complete the same tensor runs every call)."""
@@ -257,6 +292,7 @@ def _encode_stoch_host(tensors, names, hptrs: np.ndarray, lay, st, codec: str, b
                 for lo, hi in ranges]
     ends = lay.offsets + lay.sizes
     code = 1 if codec == "cnat" else 0
+    fast = torch_norm and codec in ("qsgd", "cnat") and uniforms is None   # _range_encode's case
     lv_parts: List[torch.Tensor] = []
     sg_parts: List[torch.Tensor] = []
     lv_ptrs = np.zeros(lay.ntensors, dtype=np.uint64)
@@ -287,8 +323,12 @@ def _encode_stoch_host(tensors, names, hptrs: np.ndarray, lay, st, codec: str, b
                 continue
             with _ph("enc.kernel_launch"):
                 stream.wait_event(landed[r])
-                _codec_encode(codec, x_dev, _sub_layout(lay, made, done), bits, uniforms, seed, levels, signs,
-                              norms[made:], mins[made:] if mins is not None else None, ws, torch_norm)
+                if fast:
+                    _range_encode(codec, x_dev, _sub_layout(lay, made, done), bits, seed, levels, signs, norms, made,
+                                  ws, st)
+                else:
+                    _codec_encode(codec, x_dev, _sub_layout(lay, made, done), bits, uniforms, seed, levels, signs,
+                                  norms[made:], mins[made:] if mins is not None else None, ws, torch_norm)
                 e0, e1 = int(lay.offsets[made]), int(ends[done - 1])
                 src, dst, nb = copies
                 src[0], src[1], dst[0], dst[1] = ld + e0, gd + e0, lh + e0, gh + e0
