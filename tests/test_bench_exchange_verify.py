@@ -1,8 +1,9 @@
 """CPU, world_size 2 and 4 (gloo): bench.py's self-check of the N > 1 exchange leg (exchange_verify) — the
 fingerprints of every gathered row against its sender's, the own row byte for byte, and the
 exact_self=False mean bit-identical on every rank (Examples/ray_ad.py:188) — driven with the oracle codec
-in place of the HIP codec, plus a rank whose received row is corrupted: every rank must then report
-parity false."""
+in place of the HIP codec on the argument sets of bench.py's N > 1 legs (exchange_leg's flat C4 exchange,
+exchange_bucket_leg's C3-shaped bucket with per-tensor scales), plus a rank whose received row is corrupted:
+every rank must then report parity false."""
 
 import os
 import socket
@@ -22,10 +23,18 @@ def _worker(rank, world, port, corrupt, q):
         from adfl_amd.exchange import PeerExchange
         from test_exchange_gloo import OracleCodec
 
+        from adfl_amd import ops
+
         results = []
-        for numel, bits, packed, chunks in [(4099, 8, False, 1), (12345, 4, True, 3)]:
-            ex = PeerExchange(numel, bits=bits, packed=packed, chunks=chunks, device=torch.device("cpu"),
-                              codec=OracleCodec())
+        # bench.py's two N > 1 legs: exchange_leg's PeerExchange(n, bits=8) (chunks 1, unpacked) and
+        # exchange_bucket_leg's PeerExchange(total, bits=8, layout=BucketLayout(256 near-equal tensors)), at
+        # small sizes; plus an int4 chunked flat exchange
+        base, rem = divmod(70_001, 256)
+        lay = ops.BucketLayout([base + (1 if i < rem else 0) for i in range(256)])
+        cases = [(4099, 8, False, 1, None), (12345, 4, True, 3, None), (lay.total, 8, False, 1, lay)]
+        for numel, bits, packed, chunks, layout in cases:
+            kw = dict(packed=packed, chunks=chunks) if layout is None else dict(layout=layout)
+            ex = PeerExchange(numel, bits=bits, device=torch.device("cpu"), codec=OracleCodec(), **kw)
             rng = np.random.default_rng(50 + rank)
             x = torch.from_numpy(rng.standard_normal(numel, dtype=np.float32) * np.float32(1e-3))
             if corrupt:
