@@ -1914,6 +1914,10 @@ __global__ __launch_bounds__(kShThreads) void k_tn_short(const float* __restrict
   Blk ra, rb;
   SH_TL(0);
   load(ra, 0);
+  // every wave's segment-0 loads queue before any segment-1 load (a bare s_barrier: no wait for the loads),
+  // so the last wave's first data is not behind the other waves' second segment in the CU's load queue
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
   load(rb, 1);
   stage(ra, 0);
@@ -1982,7 +1986,7 @@ __device__ __forceinline__ float rn_bf16(float f) {
 // Phase D, one wave per chain: grid (tensors, 8) — by_chunk: (chunks, 8), only tensors' first chunks work
 // (layouts of short tensors only, where phase A, which fills tfirst, did not run); blockIdx.y strides the
 // chains (one chain per CU, so eight chains of one tensor do not share a SIMD). skip_short: fp32 tensors up
-// to kShortMax are the in-order walker's (adfl_tn::launch_walk). Each chain's exact accumulator goes to
+// to kShortMaxF32 are k_tn_short's (ADFL_TN_WALKER builds: the in-order walker's). Each chain's exact accumulator goes to
 // chain_acc[tensor][chain] for k_tn_finish.
 template <int DT>
 __global__ __launch_bounds__(64) void k_tn_chains(const void* __restrict__ x, const adfl_slq_chunk* __restrict__ chunks, int64_t nall,
