@@ -1304,9 +1304,62 @@ __device__ float short_exact_round(const float (&v)[kSL], float acc, int G, int 
   return lane_fma(w, rebuild<false>(lane_d(Al, ls), G), lane, ls);
 }
 
+// The same round for exact-square inputs (fp16 / bf16 values: x^2 has at most 22 significant bits), with no fp64:
+// on grid G, h = x^2 / u is exact in fp32, so k = rint(h) and a tie (h - k = +-1/2) are exact, and a lane's map
+// (what its steps add to an even / an odd A, sq_step) is an integer pair. The maps are scanned as fp32 pairs by
+// DPP, composed in lane order: exact below 2^24, and at least 2^24 above (every term >= 0), which is all a
+// covered run needs; a lane with a step of h >= 2^21 is not covered (+inf).
+__device__ __forceinline__ bool odd_f(float v) { return __builtin_amdgcn_fractf(v * 0.5f) != 0.0f; }  // v an integer
+template <int CTRL, int RM>
+__device__ __forceinline__ void dpp_compose(float& e, float& o) {  // (e, o) <- (the moved lane's map) then (e, o)
+  const float pe = dpp0<CTRL, RM>(e), po = dpp0<CTRL, RM>(o);   // identity (0, 0) where no lane moves in
+  const float ne = pe + (odd_f(pe) ? o : e), no = po + (odd_f(po) ? e : o);
+  e = ne;
+  o = no;
+}
+__device__ float short_sq_round(const float (&v)[kSL], float acc, int G, int lane, int& start) {
+  float w[kSL];
+#pragma unroll
+  for (int i = 0; i < kSL; ++i) {  // through an empty asm: the rare path's work is not hoisted into every round
+    w[i] = v[i];
+    __asm__ volatile("" : "+v"(w[i]));
+  }
+  const int s = 23 - G;
+  const float sa = pow2f(s >> 1), sb = (s & 1) ? 2.0f : 1.0f;
+  int ie = 0, io = 1;
+  bool big = false;
+#pragma unroll
+  for (int i = 0; i < kSL; ++i) {
+    const float xs = w[i] * sa;
+    const float h = xs * xs * sb;
+    big |= !(h < 0x1p21f);  // NaN / inf too
+    sq_step(big ? 0.0f : h, ie, io);
+  }
+  float e = big ? __builtin_inff() : (float)ie, o = big ? __builtin_inff() : (float)(io - 1);
+  if (lane < start) e = o = 0.0f;
+  dpp_compose<0x111, 0xf>(e, o);  // row_shr:1
+  dpp_compose<0x112, 0xf>(e, o);  // row_shr:2
+  dpp_compose<0x114, 0xf>(e, o);  // row_shr:4
+  dpp_compose<0x118, 0xf>(e, o);  // row_shr:8
+  dpp_compose<0x142, 0xa>(e, o);  // row_bcast:15
+  dpp_compose<0x143, 0xc>(e, o);  // row_bcast:31
+  const float A = (float)a_of(acc);
+  const float out = A + (odd_f(A) ? o : e);  // A through lanes 0 .. lane
+  const unsigned long long ball = __ballot(lane >= start && !(out < 0x1p24f));
+  if (ball == 0ull) {
+    start = 64;
+    return rebuild<false>((double)lane_f(out, 63), G);
+  }
+  const int ls = __builtin_ctzll(ball);
+  start = ls + 1;
+  return lane_fma(w, rebuild<false>((double)(ls > 0 ? lane_f(out, ls - 1) : A), G), lane, ls);
+}
+
 constexpr int kSerial = 256 / ADFL_TN_SHORT_SL;  // lanes (256 steps) run in order at a chain's start (short_segment)
 
 // One segment of a chain (lane l: steps 16 l .. 16 l + 15, in order) from the exact accumulator acc (wave-uniform).
+// SQ: exact-square inputs (fp16 / bf16), whose tie rounds take short_sq_round instead of the fp64 maps.
+template <bool SQ = false>
 __device__ __forceinline__ float short_segment(const float (&v)[kSL], float acc, int lane SH_ARG) {
   int start = 0;
   SH_STAT(0, 1);
@@ -1336,7 +1389,8 @@ __device__ __forceinline__ float short_segment(const float (&v)[kSL], float acc,
     float K0 = lane_incs(v, G, ties);
     if (ties >> start) {  // a possible tie in a lane still to run
       SH_STAT(2, 1);
-      acc = short_exact_round(v, acc, G, lane, start);
+      if constexpr (SQ) acc = short_sq_round(v, acc, G, lane, start);
+      else acc = short_exact_round(v, acc, G, lane, start);
       continue;
     }
     if (lane < start) K0 = 0.0f;
@@ -1959,6 +2013,129 @@ __global__ __launch_bounds__(kShThreads) void k_tn_short(const float* __restrict
   }
 }
 
+// ---- short fp16 tensors (up to kShortMax elements): one block per tensor, one wave per piece, one launch.
+// torch's fp16 order is at::parallel_for's split (split_of): nt = 1 or 2 pieces here (n <= 2^16), each one fp32
+// chain over its contiguous elements from 0, the piece sums added in order to 0. x^2 of an fp16 value is exact
+// in fp32, so a piece is k_tn_short's chain with contiguous steps: wave c walks piece c in 1024-step segments
+// (lane l: steps 16 l .. 16 l + 15) by short_segment. A piece's elements are contiguous, so each wave stages its
+// own segment — 16-byte loads of the aligned block under it, converted to fp32 into the wave's own LDS rows —
+// and needs no block barrier; the next three segments' loads are in flight while one is walked.
+constexpr int kH16Waves = 2;                    // pieces per tensor at n <= kShortMax = 2^16 (GRAIN 32768)
+constexpr int kH16Row = 64 * kShLS;             // floats per wave's staged segment (lane rows of 16 + 4)
+static_assert(kShortMax <= 2 * kGrain, "k_tn_short_f16 holds two pieces per tensor");
+
+__global__ __launch_bounds__(64 * kH16Waves) void k_tn_short_f16(const uint16_t* __restrict__ x,
+                                                                  const adfl_slq_chunk* __restrict__ chunks,
+                                                                  const int* __restrict__ tfirst, int64_t max_n, int threads,
+                                                                  double* __restrict__ norms64, float* __restrict__ norms32) {
+  __shared__ __attribute__((aligned(16))) float buf[kH16Waves][kH16Row];
+  __shared__ float s_acc[kH16Waves];
+  const int ci = tfirst[blockIdx.x];
+  const adfl_slq_chunk ch = chunks[ci];
+  const int64_t n = (int64_t)(ch.nchunks - 1) * ADFL_SLQ_CHUNK_ELEMS + chunks[ci + ch.nchunks - 1].len;
+  if (n > max_n) return;
+  const uint16_t* const xt = x + ch.start;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const Split sp = split_of(n, threads);
+  float acc = 0.0f;
+  if (wave < (int)sp.nt) {
+    const int64_t a = (int64_t)wave * sp.cs, L = (a + sp.cs < n ? a + sp.cs : n) - a;  // the piece's steps
+    // one buffer resource over the tensor's 16-byte blocks (reads past them return 0)
+    const int dt = (int)(((uintptr_t)xt & 15) >> 1);                // the tensor's start in its block, in halves
+    const uint16_t* const xa = xt - dt;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(xa), 0, (int)(((n + dt) * 2 + 15) & ~15LL),
+                                                      0x00020000);
+    const int nseg = (int)((L + kSeg - 1) / kSeg);
+    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+    struct Blk {
+      u4 r0, r1, r2;  // vectors lane and lane + 64 of the segment's block, and vector 128 (lane 0's)
+      int delta;
+    };
+    const auto load = [&](Blk& k, int j) {
+      const int64_t e = dt + a + (int64_t)j * kSeg;                 // the segment's first element, from xa
+      const int64_t vb = e >> 3;                                    // its 16-byte block
+      k.delta = (int)(e & 7);
+      const int o = (int)(vb * 16);
+      k.r0 = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rs, o + lane * 16, 0, 0));
+      k.r1 = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rs, o + (lane + 64) * 16, 0, 0));
+      k.r2 = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rs, o + 128 * 16, 0, 0));
+    };
+    float* const row = buf[wave];
+#ifdef ADFL_TN_STATS
+    unsigned long long shs[11] = {};
+#endif
+    const auto stage_run = [&](const Blk& k, int j) {
+      const int left = (int)(L - (int64_t)j * kSeg < kSeg ? L - (int64_t)j * kSeg : kSeg);  // steps in this segment
+      const auto put = [&](const u4& r, int v) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int st = 8 * v + q - k.delta;
+          if (st >= 0 && st < kSeg) {
+            const uint32_t w = r[q >> 1];
+            const float f = __half2float(__ushort_as_half((unsigned short)((q & 1) ? (w >> 16) : (w & 0xffffu))));
+            row[(st >> 4) * kShLS + (st & 15)] = st < left ? f : 0.0f;
+          }
+        }
+      };
+      put(k.r0, lane);
+      put(k.r1, lane + 64);
+      if (lane == 0) put(k.r2, 128);
+      const float4* const rd = reinterpret_cast<const float4*>(row + lane * kShLS);
+      float v[kSL];
+#pragma unroll
+      for (int q = 0; q < kSL / 4; ++q) {
+        const float4 f = rd[q];
+        v[4 * q] = f.x;
+        v[4 * q + 1] = f.y;
+        v[4 * q + 2] = f.z;
+        v[4 * q + 3] = f.w;
+      }
+      acc = short_segment<true>(v, acc, lane SH_PASS);
+    };
+#ifdef ADFL_TN_STATS
+    const long long k0c = clock64();
+#endif
+    // wave-uniform: four register sets, the next three segments' loads in flight while one is walked (one
+    // segment ahead left the HBM latency exposed: two waves per CU have nothing else to hide it behind)
+    // (loads past the tensor read zeros from the buffer resource, so they are issued unconditionally: a guarded
+    // load made the compiler wait for every load at the merge)
+    Blk k0, k1, k2, k3;
+    load(k0, 0);
+    load(k1, 1);
+    load(k2, 2);
+    for (int j = 0;; j += 4) {
+      load(k3, j + 3);
+      stage_run(k0, j);
+      if (j + 1 >= nseg) break;
+      load(k0, j + 4);
+      stage_run(k1, j + 1);
+      if (j + 2 >= nseg) break;
+      load(k1, j + 5);
+      stage_run(k2, j + 2);
+      if (j + 3 >= nseg) break;
+      load(k2, j + 6);
+      stage_run(k3, j + 3);
+      if (j + 4 >= nseg) break;
+    }
+#ifdef ADFL_TN_STATS
+    shs[6] += clock64() - k0c;
+    shs[8] += 1;
+    if (lane == 0)
+      for (int i = 0; i < 11; ++i) atomicAdd(&g_sh_stats[i], shs[i]);
+#endif
+  }
+  if (lane == 0) s_acc[wave] = acc;
+  __syncthreads();
+  if (tid == 0) {
+    float tot = 0.0f;
+    for (int c = 0; c < (int)sp.nt; ++c) tot = tot + s_acc[c];
+    float r = __half2float(__float2half_rn((float)__builtin_sqrt((double)tot)));
+    if (n == 1) r = __builtin_fabsf(__half2float(__ushort_as_half(xt[0])));  // a one-element tensor's norm is |x|
+    if (norms32) norms32[ch.tensor] = r;
+    if (norms64) norms64[ch.tensor] = r;
+  }
+}
+
 #ifdef ADFL_TN_STATS
 __global__ void k_sh_stats_print() {
   const unsigned long long* g = g_sh_stats;
@@ -2132,6 +2309,19 @@ int launch(const void* x, const adfl_slq_chunk* chunks, int64_t nchunks, const i
   const Scratch s = carve(scratch, nchunks, ntensors);
   const bool any_long = (kinds & ADFL_TORCH_NORM_LONG) != 0, any_short = (kinds & ADFL_TORCH_NORM_SHORT) != 0;
   const bool walk = DT == ADFL_DTYPE_F32;  // fp32 short tensors: k_tn_short (ADFL_TN_WALKER builds: the in-order walker)
+  // fp16 short tensors: k_tn_short_f16; bf16 / fp64 ones go straight to phase D (with the long ones, or alone)
+  const bool own_short = walk || DT == ADFL_DTYPE_F16;
+  if (DT == ADFL_DTYPE_F16 && any_short) {
+    if (!tfirst) {
+      k_tn_tfirst<<<(unsigned)((nchunks + 255) / 256), 256, 0, st>>>(chunks, nchunks, s.tfirst);
+      tfirst = s.tfirst;
+    }
+    k_tn_short_f16<<<(unsigned)ntensors, 64 * kH16Waves, 0, st>>>((const uint16_t*)x, chunks, tfirst, kShortMax, threads,
+                                                                  n64, n32);
+#ifdef ADFL_TN_STATS
+    k_sh_stats_print<<<1, 1, 0, st>>>();
+#endif
+  }
   if (walk && any_short) {
 #ifdef ADFL_TN_WALKER
     if (int e = adfl_tn::launch_walk((const float*)x, chunks, nchunks, n32, n64, st)) return e;
@@ -2163,10 +2353,11 @@ int launch(const void* x, const adfl_slq_chunk* chunks, int64_t nchunks, const i
                                                                                    s.exact + 1);
     k_tn_windows<DT><<<dim3((unsigned)ntensors, 8, 8), 256, 0, st>>>(chunks, nchunks, s.tfirst, threads, s.recs, s.maps, s.wing,
                                                                      s.winmaps);
-    k_tn_chains<DT><<<dim3((unsigned)ntensors, 8), 64, 0, st>>>(x, chunks, nchunks, s.tfirst, 0, walk, threads, s.S, s.recs,
+    k_tn_chains<DT><<<dim3((unsigned)ntensors, 8), 64, 0, st>>>(x, chunks, nchunks, s.tfirst, 0, own_short, threads, s.S, s.recs,
                                                                  s.maps, s.wing, s.winmaps, s.chain_acc);
-    k_tn_finish<DT><<<(unsigned)ntensors, 64, 0, st>>>(x, chunks, nchunks, s.tfirst, 0, walk, threads, s.chain_acc, n64, n32);
-  } else if (!walk) {
+    k_tn_finish<DT><<<(unsigned)ntensors, 64, 0, st>>>(x, chunks, nchunks, s.tfirst, 0, own_short, threads, s.chain_acc, n64,
+                                                       n32);
+  } else if (!own_short) {
     k_tn_chains<DT><<<dim3((unsigned)nchunks, 8), 64, 0, st>>>(x, chunks, nchunks, s.tfirst, 1, 0, threads, s.S, s.recs,
                                                                 s.maps, s.wing, s.winmaps, s.chain_acc);
     k_tn_finish<DT><<<(unsigned)nchunks, 64, 0, st>>>(x, chunks, nchunks, s.tfirst, 1, 0, threads, s.chain_acc, n64, n32);
