@@ -95,7 +95,9 @@ constexpr int64_t kShortMax = 1 << 16;            // tensors up to this size ski
 #define ADFL_TN_SHORT_MAX_F32 (1 << 19)
 #endif
 constexpr int64_t kShortMaxF32 = ADFL_TN_SHORT_MAX_F32;  // fp32: k_tn_short (one block per tensor) up to this size
-template <int DT> constexpr int64_t short_max() { return DT == ADFL_DTYPE_F32 ? kShortMaxF32 : kShortMax; }
+template <int DT> constexpr int64_t short_max() {  // fp32 / bf16: k_tn_short(_bf16); fp16: k_tn_short_f16; fp64: D
+  return DT == ADFL_DTYPE_F32 || DT == ADFL_DTYPE_BF16 ? kShortMaxF32 : kShortMax;
+}
 constexpr int64_t kGrain = 32768;                 // at::internal::GRAIN_SIZE
 constexpr int kMaxChains = 512;                   // fp16: chains (torch threads) per tensor the combine holds
 constexpr double kMagic = 6755399441055744.0;     // 1.5 * 2^52: (v + kMagic) - kMagic = rint(v), 0 <= v < 2^51
@@ -2136,6 +2138,126 @@ __global__ __launch_bounds__(64 * kH16Waves) void k_tn_short_f16(const uint16_t*
   }
 }
 
+__device__ __forceinline__ float rn_bf16(float f) {
+  const uint32_t b = __float_as_uint(f);
+  if (__builtin_isnan(f)) return __uint_as_float((b | 0x00400000u) & 0xffff0000u);
+  return __uint_as_float((b + 0x7fffu + ((b >> 16) & 1u)) & 0xffff0000u);
+}
+
+// ---- short bf16 tensors (up to kShortMaxF32 elements): k_tn_short's layout for 2-byte elements. torch's bf16
+// order is 8 fp32 chains over the leading n - n % 16 elements (element e into chain e % 8), the lane sum left to
+// right, then the n % 16 tail with fma; x^2 of a bf16 value is exact in fp32 (tie rounds: short_sq_round). The
+// 8 waves stream the tensor in 8192-element segments (16 KB): each thread loads 2 16-byte vectors of the aligned
+// block (thread 0's third covers the start's offset), converts them to fp32 into the chains' LDS rows, and wave c
+// walks chain c's 1024 steps by short_segment; two LDS buffers, one barrier per segment, the next segment's
+// loads in flight while one is walked.
+__global__ __launch_bounds__(kShThreads) void k_tn_short_bf16(const uint16_t* __restrict__ x,
+                                                               const adfl_slq_chunk* __restrict__ chunks,
+                                                               const int* __restrict__ tfirst, int64_t max_n,
+                                                               double* __restrict__ norms64, float* __restrict__ norms32) {
+  __shared__ __attribute__((aligned(16))) float buf[2][8 * kShRow];
+  __shared__ float s_acc[8];
+  const int ci = tfirst[blockIdx.x];
+  const adfl_slq_chunk ch = chunks[ci];
+  const int64_t n = (int64_t)(ch.nchunks - 1) * ADFL_SLQ_CHUNK_ELEMS + chunks[ci + ch.nchunks - 1].len;
+  if (n > max_n) return;
+  const uint16_t* const xt = x + ch.start;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const auto bf = [](uint32_t h) { return __uint_as_float(h << 16); };
+  const int64_t nv = n - n % 16;
+  float acc = 0.0f;
+  if (nv > 0) {
+    const int nseg = (int)((nv + kShSeg - 1) / kShSeg);
+    const int dt = (int)(((uintptr_t)xt & 15) >> 1);  // the start's offset in its 16-byte block, in elements
+    const uint16_t* const xa = xt - dt;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(xa), 0, (int)(((nv + dt) * 2 + 15) & ~15LL),
+                                                      0x00020000);
+    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+    struct Blk {
+      u4 r0, r1, r2;  // vectors tid and tid + 512 of the segment's block, and vector 1024 (thread 0's)
+    };
+    const auto load = [&](Blk& k, int j) {
+      const int o = j * (kShSeg * 2);
+      k.r0 = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rs, o + tid * 16, 0, 0));
+      k.r1 = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rs, o + (tid + kShThreads) * 16, 0, 0));
+      k.r2 = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rs, o + 2 * kShThreads * 16, 0, 0));
+    };
+    const auto stage = [&](const Blk& k, int j) {
+      float* const bj = buf[j & 1];
+      const int64_t left = nv - (int64_t)j * kShSeg;  // chain steps' elements from this segment's start
+      const auto put = [&](const u4& r, int v) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int e = 8 * v + q - dt;  // element of the segment: chain e % 8, step e / 8
+          if (e >= 0 && e < kShSeg) {
+            const uint32_t w = r[q >> 1];
+            const float f = e < left ? bf((q & 1) ? (w >> 16) : (w & 0xffffu)) : 0.0f;
+            const int st = e >> 3;
+            bj[(e & 7) * kShRow + (st >> 4) * kShLS + (st & 15)] = f;
+          }
+        }
+      };
+      put(k.r0, tid);
+      put(k.r1, tid + kShThreads);
+      if (tid == 0) put(k.r2, 2 * kShThreads);
+    };
+    const int rdo = wave * kShRow + lane * kShLS;
+#ifdef ADFL_TN_STATS
+    unsigned long long shs[11] = {};
+#endif
+    const auto run = [&](int j) {
+      const float4* const rd = reinterpret_cast<const float4*>(buf[j & 1] + rdo);
+      float v[kSL];
+#pragma unroll
+      for (int q = 0; q < kSL / 4; ++q) {
+        const float4 f = rd[q];
+        v[4 * q] = f.x;
+        v[4 * q + 1] = f.y;
+        v[4 * q + 2] = f.z;
+        v[4 * q + 3] = f.w;
+      }
+      acc = short_segment<true>(v, acc, lane SH_PASS);
+    };
+    Blk ra, rb;
+    load(ra, 0);
+    load(rb, 1);  // past the end: zeros from the buffer resource (unconditional, so the waits count exactly)
+    stage(ra, 0);
+    __syncthreads();
+    for (int j = 0;; j += 2) {  // block-uniform control flow throughout
+      load(ra, j + 2);
+      run(j);
+      stage(rb, j + 1);
+      __syncthreads();
+      if (j + 1 >= nseg) break;
+      load(rb, j + 3);
+      run(j + 1);
+      stage(ra, j + 2);
+      __syncthreads();
+      if (j + 2 >= nseg) break;
+    }
+#ifdef ADFL_TN_STATS
+    shs[8] += 1;
+    if (lane == 0)
+      for (int i = 0; i < 11; ++i) atomicAdd(&g_sh_stats[i], shs[i]);
+#endif
+  }
+  if (lane == 0) s_acc[wave] = acc;
+  __syncthreads();
+  if (tid == 0) {  // lane sum left to right, the n % 16 tail with fma, sqrt, to bf16
+    float b = s_acc[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) b = b + s_acc[j];
+    for (int64_t i = nv; i < n; ++i) {
+      const float e = bf(xt[i]);
+      b = __builtin_fmaf(e, e, b);
+    }
+    float r = rn_bf16((float)__builtin_sqrt((double)b));
+    if (n == 1) r = __builtin_fabsf(bf(xt[0]));  // a one-element tensor's norm is |x|
+    if (norms32) norms32[ch.tensor] = r;
+    if (norms64) norms64[ch.tensor] = r;
+  }
+}
+
 #ifdef ADFL_TN_STATS
 __global__ void k_sh_stats_print() {
   const unsigned long long* g = g_sh_stats;
@@ -2154,11 +2276,6 @@ __global__ void k_sh_stats_print() {
 }
 #endif
 
-__device__ __forceinline__ float rn_bf16(float f) {
-  const uint32_t b = __float_as_uint(f);
-  if (__builtin_isnan(f)) return __uint_as_float((b | 0x00400000u) & 0xffff0000u);
-  return __uint_as_float((b + 0x7fffu + ((b >> 16) & 1u)) & 0xffff0000u);
-}
 
 // Phase D, one wave per chain: grid (tensors, 8) — by_chunk: (chunks, 8), only tensors' first chunks work
 // (layouts of short tensors only, where phase A, which fills tfirst, did not run); blockIdx.y strides the
@@ -2310,7 +2427,17 @@ int launch(const void* x, const adfl_slq_chunk* chunks, int64_t nchunks, const i
   const bool any_long = (kinds & ADFL_TORCH_NORM_LONG) != 0, any_short = (kinds & ADFL_TORCH_NORM_SHORT) != 0;
   const bool walk = DT == ADFL_DTYPE_F32;  // fp32 short tensors: k_tn_short (ADFL_TN_WALKER builds: the in-order walker)
   // fp16 short tensors: k_tn_short_f16; bf16 / fp64 ones go straight to phase D (with the long ones, or alone)
-  const bool own_short = walk || DT == ADFL_DTYPE_F16;
+  const bool own_short = walk || DT == ADFL_DTYPE_F16 || DT == ADFL_DTYPE_BF16;
+  if (DT == ADFL_DTYPE_BF16 && any_short) {
+    if (!tfirst) {
+      k_tn_tfirst<<<(unsigned)((nchunks + 255) / 256), 256, 0, st>>>(chunks, nchunks, s.tfirst);
+      tfirst = s.tfirst;
+    }
+    k_tn_short_bf16<<<(unsigned)ntensors, kShThreads, 0, st>>>((const uint16_t*)x, chunks, tfirst, short_max<DT>(), n64, n32);
+#ifdef ADFL_TN_STATS
+    k_sh_stats_print<<<1, 1, 0, st>>>();
+#endif
+  }
   if (DT == ADFL_DTYPE_F16 && any_short) {
     if (!tfirst) {
       k_tn_tfirst<<<(unsigned)((nchunks + 255) / 256), 256, 0, st>>>(chunks, nchunks, s.tfirst);
@@ -2379,7 +2506,12 @@ int64_t adfl_torch_norm_short_max(void) { return adfl_tnx::kShortMax; }
 
 int64_t adfl_torch_norm_short_max_dt(int32_t dtype) {
   if (dtype < ADFL_DTYPE_F32 || dtype > ADFL_DTYPE_F64) return ADFL_E_ARG;
-  return dtype == ADFL_DTYPE_F32 ? adfl_tnx::kShortMaxF32 : adfl_tnx::kShortMax;
+  switch (dtype) {
+    case ADFL_DTYPE_F32: return adfl_tnx::short_max<ADFL_DTYPE_F32>();
+    case ADFL_DTYPE_BF16: return adfl_tnx::short_max<ADFL_DTYPE_BF16>();
+    case ADFL_DTYPE_F16: return adfl_tnx::short_max<ADFL_DTYPE_F16>();
+    default: return adfl_tnx::short_max<ADFL_DTYPE_F64>();
+  }
 }
 
 int adfl_torch_norms_work(int32_t dtype, const void* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks,

@@ -68,15 +68,17 @@ enum { ADFL_TORCH_NORM_SHORT = 1, ADFL_TORCH_NORM_LONG = 2 };
  *            elements are summed in min(threads, ceil(n / 32768)) contiguous pieces: 1..512 for fp16 buckets;
  *            any value >= 1 for the other dtypes, which do not use it).
  *   kinds:   which tensors the bucket holds, so launches with nothing to do are skipped:
- *            ADFL_TORCH_NORM_SHORT (some of at most adfl_torch_norm_short_max_dt(dtype) elements: fp32 ones in
- *            one launch, one block per tensor) | ADFL_TORCH_NORM_LONG (some longer: the phased path); 0 = both.
+ *            ADFL_TORCH_NORM_SHORT (some of at most adfl_torch_norm_short_max_dt(dtype) elements: fp32, bf16
+ *            and fp16 ones in one launch, one block per tensor) | ADFL_TORCH_NORM_LONG (some longer: the phased
+ *            path); 0 = both.
  *   outputs: d_norms64[t] = the norm as a double (the dtype's value: exact for every dtype) and / or
  *            d_norms32[t] = (float) of it; either may be NULL, not both.
  * d_scratch: adfl_torch_norm_scratch_bytes(nchunks, ntensors) bytes, 256-byte aligned, no initialisation.
  * Four launches (one for layouts of short tensors only). */
 int64_t adfl_torch_norm_scratch_bytes(int64_t nchunks, int64_t ntensors);
-int64_t adfl_torch_norm_short_max(void);          /* fp16 / bf16 / fp64: 65,536 */
-int64_t adfl_torch_norm_short_max_dt(int32_t dtype); /* the short-tensor bound of a dtype (fp32: 2^19), or ADFL_E_ARG */
+int64_t adfl_torch_norm_short_max(void);          /* fp16 / fp64: 65,536 */
+int64_t adfl_torch_norm_short_max_dt(int32_t dtype); /* the short-tensor bound of a dtype (fp32, bf16: 2^19; fp16,
+                                                        fp64: 2^16), or ADFL_E_ARG */
 int adfl_torch_norms(int32_t dtype, const void* d_x, const adfl_slq_chunk* d_chunks, int64_t nchunks,
                      int64_t ntensors, int32_t kinds, int32_t threads, void* d_scratch, int64_t scratch_bytes,
                      double* d_norms64, float* d_norms32, void* stream);

@@ -196,4 +196,8 @@ def test_reference_norms_abi_rejects_bad_arguments():
     assert call(args(n64=None)) == -1
     assert call(args(nt=2)) == -1
     assert L.adfl_torch_norm_short_max() == 1 << 16
+    # one block per tensor up to these sizes (k_tn_short / k_tn_short_bf16 / k_tn_short_f16; fp64: phase D)
+    assert [L.adfl_torch_norm_short_max_dt(d) for d in (_lib.DTYPE_F32, _lib.DTYPE_BF16, _lib.DTYPE_F16,
+                                                         _lib.DTYPE_F64)] == [1 << 19, 1 << 19, 1 << 16, 1 << 16]
+    assert L.adfl_torch_norm_short_max_dt(7) < 0
     torch.cuda.synchronize()
