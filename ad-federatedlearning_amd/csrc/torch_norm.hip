@@ -41,9 +41,9 @@
 //      G and G + 1, scanned; the lane that crosses runs its steps with fma); then k_tn_finish: the lane sum
 //      (fp16: piece sums in order), the tail, sqrt and the rounding to the dtype. fp32 runs its segments with
 //      k_tn_short's short_segment and its window / tile scans in fp32 by DPP (integer totals below 2^24).
-// fp32 tensors up to kShortMaxF32 elements take k_tn_short (one block per tensor; ADFL_TN_WALKER builds: the
-// in-order walker, torch_norm_walk.h); other short tensors go straight to D with every tile resolved in detail.
-// DESIGN.md §10.
+// Short tensors, one block per tensor in one launch: fp32 up to kShortMaxF32 elements k_tn_short (ADFL_TN_WALKER
+// builds: the in-order walker, torch_norm_walk.h), bf16 up to the same k_tn_short_bf16, fp16 up to kShortMax
+// k_tn_short_f16; short fp64 tensors go straight to D with every tile resolved in detail. DESIGN.md §10.
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 #include <hip/hip_fp16.h>
