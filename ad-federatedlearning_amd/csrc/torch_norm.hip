@@ -1619,6 +1619,20 @@ __device__ typename Acc<Dt<DT>::kWide>::T resolve_window(const void* x, const Te
     TN_STAT(10, clock64() - l0);
   }
 #endif
+  // the records decoded once per window (every scan re-selects from them by the accumulator's binade): flags,
+  // predicted binade, and (fp32) the totals on g and g - 1 as fp32 integers (+inf where not covered)
+  uint32_t flk[kTPL];
+  int gk[kTPL];
+  float K0f[kTPL], K1f[kTPL];
+#pragma unroll
+  for (int k = 0; k < kTPL; ++k) {
+    flk[k] = rec_flags(r[k]);
+    gk[k] = rec_g<W>(r[k]);
+    if constexpr (!W) {
+      K0f[k] = (float)rec_k(r[k], 0);
+      K1f[k] = (float)rec_k(r[k], 1);
+    }
+  }
   int start = 0;  // window tiles before it are done
   const int wlen = nt - w0 < kWinTiles ? (int)(nt - w0) : kWinTiles;
   while (start < wlen) {
@@ -1639,7 +1653,7 @@ __device__ typename Acc<Dt<DT>::kWide>::T resolve_window(const void* x, const Te
     const double A = a_of(acc);
     bool side = false;
 #pragma unroll
-    for (int k = 0; k < kTPL; ++k) side |= (rec_flags(r[k]) & kSide) && lane * kTPL + k >= start;
+    for (int k = 0; k < kTPL; ++k) side |= (flk[k] & kSide) && lane * kTPL + k >= start;
     const bool any_side = __ballot(side) != 0ull;
     const auto tile_map = [&](int k) -> Map {
       const Rec q = r[k];
@@ -1655,8 +1669,10 @@ __device__ typename Acc<Dt<DT>::kWide>::T resolve_window(const void* x, const Te
       if (!any_side) {  // fp32 accumulators: the DPP scan in fp32, as in resolve_chain
         float Kk[kTPL], K = 0.0f;
 #pragma unroll
-        for (int k = 0; k < kTPL; ++k) {
-          Kk[k] = (float)tile_map(k).e;
+        for (int k = 0; k < kTPL; ++k) {  // tile_map(k).e from the window's decoded records
+          const int j = gk[k] - G;
+          Kk[k] = ((flk[k] & kPad) || lane * kTPL + k < start) ? 0.0f
+                                                                : (j == 0 ? K0f[k] : (j == 1 ? K1f[k] : __builtin_inff()));
           K += Kk[k];
         }
         const float Af = (float)A, I = wave_incl_f(K), o = Af + I;
