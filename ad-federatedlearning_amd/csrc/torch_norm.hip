@@ -192,6 +192,33 @@ __device__ __forceinline__ double wave_excl_sum(double v, int lane) {
   return lane == 0 ? 0.0 : x;
 }
 
+template <int CTRL, int RM>
+__device__ __forceinline__ float dpp0(float v) {  // the DPP-moved value, +0 where the lane has no source
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, RM, 0xf, false));
+}
+__device__ __forceinline__ bool odd_f(float v) { return __builtin_amdgcn_fractf(v * 0.5f) != 0.0f; }  // v an integer
+template <int CTRL, int RM>
+__device__ __forceinline__ void dpp_compose(float& e, float& o) {  // (e, o) <- (the moved lane's map) then (e, o)
+  const float pe = dpp0<CTRL, RM>(e), po = dpp0<CTRL, RM>(o);   // identity (0, 0) where no lane moves in
+  const float ne = pe + (odd_f(pe) ? o : e), no = po + (odd_f(po) ? e : o);
+  e = ne;
+  o = no;
+}
+// every lane: the composition of all 64 lanes' maps in lane order, as fp32 pairs by DPP — for maps of integers
+// (exact-square inputs): exact below 2^24, at least 2^24 above (every term >= 0), which is all a consumer of a
+// fp32-accumulator map tests (Acc<false>::kTop); +inf stays +inf
+__device__ __forceinline__ float lane63_f(float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63)); }
+__device__ __forceinline__ Map wave_compose_f(Map m) {
+  float e = (float)m.e, o = (float)m.o;
+  dpp_compose<0x111, 0xf>(e, o);  // row_shr:1
+  dpp_compose<0x112, 0xf>(e, o);  // row_shr:2
+  dpp_compose<0x114, 0xf>(e, o);  // row_shr:4
+  dpp_compose<0x118, 0xf>(e, o);  // row_shr:8
+  dpp_compose<0x142, 0xa>(e, o);  // row_bcast:15
+  dpp_compose<0x143, 0xc>(e, o);  // row_bcast:31
+  return Map{(double)lane63_f(e), (double)lane63_f(o)};
+}
+
 // ---- one step's increment on grid with ulp 2^-s (s = kM - g): k and whether it is a tie (then k = floor)
 __device__ __forceinline__ void inc_exact(float x, double sc, double& k, bool& tie) {
   const double d = (double)x;
@@ -990,12 +1017,15 @@ __global__ __launch_bounds__(256) void k_tn_maps_exact(const void* __restrict__ 
   __shared__ int s_g[8];
   __shared__ uint32_t s_nf[8];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int count = exact_list[-1];
+  // exact_list NULL: every chunk of a long tensor (exact-square dtypes, whose ties are real and frequent: phase
+  // C's order-free pass listed nearly every chunk anyway, so it is skipped)
+  const int count = exact_list ? exact_list[-1] : (int)nall;
   for (int li = blockIdx.x; li < count; li += gridDim.x) {
-    const int ci = exact_list[li];
+    const int ci = exact_list ? exact_list[li] : li;
     const Tensor T = tensor_of(chunks, ci, nall);
     const Split sp = split_of(T.n, threads);
     const ChunkGeo G = geo_of<DT>(T, ci, sp);
+    if (!exact_list && (T.n <= short_max<DT>() || G.lim <= 0)) continue;  // (block-uniform)
     const int npieces = D::kContig ? (G.bnd < G.len ? 2 : 1) : D::NC;
     if (tid < npieces) {
       const Rec q = recs[slot_of(ci, tid, T.nall)];
@@ -1048,8 +1078,13 @@ __global__ __launch_bounds__(256) void k_tn_maps_exact(const void* __restrict__ 
           const int g = s_g[pc < npieces ? pc : 0];
           Map l0, l1;
           lane_maps_pair<W, D::kSq>(z, g, -1, l0, l1);
-          acc0[pc] = compose(acc0[pc], wave_compose(l0, lane));
-          acc1[pc] = compose(acc1[pc], wave_compose(l1, lane));
+          if constexpr (D::kSq) {  // integer maps: fp32 DPP composition (round 6)
+            acc0[pc] = compose(acc0[pc], wave_compose_f(l0));
+            acc1[pc] = compose(acc1[pc], wave_compose_f(l1));
+          } else {
+            acc0[pc] = compose(acc0[pc], wave_compose(l0, lane));
+            acc1[pc] = compose(acc1[pc], wave_compose(l1, lane));
+          }
         }
       } else {
         const int g = s_g[D::NC == 8 ? row : row / 2];
@@ -1062,8 +1097,14 @@ __global__ __launch_bounds__(256) void k_tn_maps_exact(const void* __restrict__ 
         }
         Map l0, l1;
         lane_maps_pair<W, D::kSq>(w, g, -1, l0, l1);
-        const Map m0 = wave_compose(l0, lane);
-        const Map m1 = wave_compose(l1, lane);
+        Map m0, m1;
+        if constexpr (D::kSq) {  // integer maps: fp32 DPP composition (round 6)
+          m0 = wave_compose_f(l0);
+          m1 = wave_compose_f(l1);
+        } else {
+          m0 = wave_compose(l0, lane);
+          m1 = wave_compose(l1, lane);
+        }
         if (lane == 0) {
           s_m[wave][h][0] = m0.e;
           s_m[wave][h][1] = m0.o;
@@ -1209,10 +1250,6 @@ __device__ __forceinline__ float tail32(const float* x, int64_t d, int64_t n, fl
   return b;
 }
 
-template <int CTRL, int RM>
-__device__ __forceinline__ float dpp0(float v) {  // the DPP-moved value, +0 where the lane has no source
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, RM, 0xf, false));
-}
 // inclusive wave scan in fp32 by DPP (row shifts, then the row broadcasts 15 and 31): exact on multiples of u
 // whose sums stay below 2^24 u, a lower bound of 2^24 u otherwise (any summation tree of terms >= 0)
 __device__ __forceinline__ float wave_incl_f(float v) {
@@ -1311,14 +1348,6 @@ __device__ float short_exact_round(const float (&v)[kSL], float acc, int G, int 
 // (what its steps add to an even / an odd A, sq_step) is an integer pair. The maps are scanned as fp32 pairs by
 // DPP, composed in lane order: exact below 2^24, and at least 2^24 above (every term >= 0), which is all a
 // covered run needs; a lane with a step of h >= 2^21 is not covered (+inf).
-__device__ __forceinline__ bool odd_f(float v) { return __builtin_amdgcn_fractf(v * 0.5f) != 0.0f; }  // v an integer
-template <int CTRL, int RM>
-__device__ __forceinline__ void dpp_compose(float& e, float& o) {  // (e, o) <- (the moved lane's map) then (e, o)
-  const float pe = dpp0<CTRL, RM>(e), po = dpp0<CTRL, RM>(o);   // identity (0, 0) where no lane moves in
-  const float ne = pe + (odd_f(pe) ? o : e), no = po + (odd_f(po) ? e : o);
-  e = ne;
-  o = no;
-}
 __device__ float short_sq_round(const float (&v)[kSL], float acc, int G, int lane, int& start) {
   float w[kSL];
 #pragma unroll
@@ -2488,12 +2517,18 @@ int launch(const void* x, const adfl_slq_chunk* chunks, int64_t nchunks, const i
     k_tn_winsums<DT><<<dim3((unsigned)ntensors, 8, 8), 256, 0, st>>>(chunks, nchunks, s.tfirst, threads, s.S, s.wsum);
     k_tn_grids<DT><<<dim3((unsigned)ntensors, 8, 8), 256, 0, st>>>(chunks, nchunks, s.tfirst, threads, s.S, s.wsum, s.recs);
     if (hipError_t e = hipMemsetAsync(s.exact, 0, 4, st)) return (int)e;
-    if constexpr (DT == ADFL_DTYPE_F32)
+    if constexpr (DT == ADFL_DTYPE_F32) {
       k_tn_maps_f32<<<(unsigned)nchunks, 256, 0, st>>>((const float*)x, chunks, nchunks, s.recs, s.exact + 1);
-    else
+      k_tn_maps_exact<DT><<<(unsigned)(nchunks < 1024 ? nchunks : 1024), 256, 0, st>>>(x, chunks, nchunks, threads, s.recs,
+                                                                                     s.maps, s.exact + 1);
+    } else if constexpr (Dt<DT>::kSq) {  // bf16 / fp16: every long tensor's chunk by exact maps, one pass
+      k_tn_maps_exact<DT><<<(unsigned)(nchunks < 2048 ? nchunks : 2048), 256, 0, st>>>(x, chunks, nchunks, threads, s.recs,
+                                                                                     s.maps, nullptr);
+    } else {
       k_tn_maps<DT><<<(unsigned)nchunks, 256, 0, st>>>(x, chunks, nchunks, threads, s.recs, s.maps, s.exact + 1);
-    k_tn_maps_exact<DT><<<(unsigned)(nchunks < 1024 ? nchunks : 1024), 256, 0, st>>>(x, chunks, nchunks, threads, s.recs, s.maps,
-                                                                                   s.exact + 1);
+      k_tn_maps_exact<DT><<<(unsigned)(nchunks < 1024 ? nchunks : 1024), 256, 0, st>>>(x, chunks, nchunks, threads, s.recs,
+                                                                                     s.maps, s.exact + 1);
+    }
     k_tn_windows<DT><<<dim3((unsigned)ntensors, 8, 8), 256, 0, st>>>(chunks, nchunks, s.tfirst, threads, s.recs, s.maps, s.wing,
                                                                      s.winmaps);
     k_tn_chains<DT><<<dim3((unsigned)ntensors, 8), 64, 0, st>>>(x, chunks, nchunks, s.tfirst, 0, own_short, threads, s.S, s.recs,
