@@ -1600,11 +1600,12 @@ __device__ typename Acc<Dt<DT>::kWide>::T resolve_tile(const void* x, const Tens
 #ifdef ADFL_TN_STATS
     const long long r0 = clock64();
 #endif
-    if constexpr (DT == ADFL_DTYPE_F32 && kSL == kLane) {  // k_tn_short's fp32 rounds (no fp64, DPP scans), same answer
+    if constexpr (!Dt<DT>::kWide && kSL == kLane) {  // k_tn_short's fp32 rounds (no fp64, DPP scans), same answer;
+                                                      // bf16 / fp16 (exact squares) with their fp32 tie rounds
 #ifdef ADFL_TN_STATS
       unsigned long long shs[11] = {};
 #endif
-      acc = short_segment(v, acc, lane SH_PASS);
+      acc = short_segment<Dt<DT>::kSq>(v, acc, lane SH_PASS);
     } else {
       acc = resolve_segment<DT>(v, acc, lane);
     }
