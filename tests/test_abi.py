@@ -55,6 +55,18 @@ def test_abi_version_and_constants():
     assert ctypes.sizeof(_lib.Chunk) == 24
 
 
+def test_reference_norm_short_bounds_per_dtype():
+    """Host-only queries of the reference-order norm: the short-tensor bound per dtype (one block per tensor:
+    fp32 / bf16 up to 2^19, fp16 up to 2^16, fp64 likewise, csrc/torch_norm.hip) — what a caller needs for
+    `kinds` — and the scratch size."""
+    lib = _lib.load()
+    got = [lib.adfl_torch_norm_short_max_dt(d) for d in (_lib.DTYPE_F32, _lib.DTYPE_BF16, _lib.DTYPE_F16, _lib.DTYPE_F64)]
+    assert got == [1 << 19, 1 << 19, 1 << 16, 1 << 16]
+    assert lib.adfl_torch_norm_short_max_dt(-1) < 0 and lib.adfl_torch_norm_short_max_dt(9) < 0
+    assert lib.adfl_torch_norm_short_max() == 1 << 16
+    assert lib.adfl_torch_norm_scratch_bytes(100, 10) > 0 > lib.adfl_torch_norm_scratch_bytes(-1, 1)
+
+
 @pytest.mark.parametrize("code,frag", [(0, "ok"), (-1, "invalid argument"), (-2, "bits"), (-3, "aligned"),
                                        (-4, "workspace")])
 def test_strerror(code, frag):
