@@ -74,7 +74,8 @@ enum { ADFL_TORCH_NORM_SHORT = 1, ADFL_TORCH_NORM_LONG = 2 };
  *   outputs: d_norms64[t] = the norm as a double (the dtype's value: exact for every dtype) and / or
  *            d_norms32[t] = (float) of it; either may be NULL, not both.
  * d_scratch: adfl_torch_norm_scratch_bytes(nchunks, ntensors) bytes, 256-byte aligned, no initialisation.
- * Four launches (one for layouts of short tensors only). */
+ * Up to nine launches, stream-ordered with no host waits (one for layouts of short fp32 / bf16 / fp16 tensors
+ * only). */
 int64_t adfl_torch_norm_scratch_bytes(int64_t nchunks, int64_t ntensors);
 int64_t adfl_torch_norm_short_max(void);          /* fp16 / fp64: 65,536 */
 int64_t adfl_torch_norm_short_max_dt(int32_t dtype); /* the short-tensor bound of a dtype (fp32, bf16: 2^19; fp16,
