@@ -27,7 +27,7 @@
 //
 // Phases (long tensors: more than kShortMax elements), one launch each, every block independent:
 //   A  k_tn_sums: per 8192-element chunk and chain (fp16: piece), the fp64 sum S of x^2 (one read of x;
-//      fp32, k_tn_sums_f32: of a 1/16 sample, weighted 16 — phase C's increments are exact there, so S only
+//      fp32 / bf16, k_tn_sums_sampled: of a 1/16 sample, weighted 16 — their phase C totals are exact, so S only
 //      predicts binades and flags nothing);
 //   B  k_tn_winsums + k_tn_grids: per window of 512 tiles the sum of S, then per tile the exclusive prefix P
 //      (earlier windows + a wave scan) predicts the binade of the accumulator at the tile's start:
@@ -592,17 +592,24 @@ __global__ __launch_bounds__(256) void k_tn_sums(const void* __restrict__ x, con
   }
 }
 
-// fp32 phase A: the same sample (16 of a chunk's 256 lines, weighted 16) and tfirst, one wave per chunk and
+// fp32 / bf16 phase A: the same sample (16 of a chunk's 256 lines, weighted 16) and tfirst, one wave per chunk and
 // kSumsCPW chunks per wave with every load issued first — a block per chunk issued 2 KB and waited (66 us on C2,
 // latency-bound); lane l loads vectors f0 = 8 (16 (l / 8) + rot) + l % 8 and f0 + 1024 (lines l / 8 and
 // l / 8 + 8 of the sample), so the lanes of one parity hold the same chains and no LDS or barrier is needed.
 constexpr int kSumsCPW = 4;
-__global__ __launch_bounds__(256) void k_tn_sums_f32(const float* __restrict__ x, const adfl_slq_chunk* __restrict__ chunks,
-                                                     int64_t nall, int* __restrict__ tfirst, double* __restrict__ S) {
+// (bf16 — 2-byte elements, 8 to a vector, each vector one element of every chain — takes the same sample: 8 of
+// its chunk's 128 lines, lane l loading vector f0 only, and every lane holding all 8 chains)
+template <int DT>
+__global__ __launch_bounds__(256) void k_tn_sums_sampled(const void* __restrict__ x, const adfl_slq_chunk* __restrict__ chunks,
+                                                         int64_t nall, int* __restrict__ tfirst, double* __restrict__ S) {
+  using V = View<DT>;
+  constexpr int EPV = V::EPV;            // 4 (fp32) / 8 (bf16)
+  constexpr int NH = EPV == 4 ? 2 : 1;   // vectors per lane: 16 sampled lines of 256 (fp32) / 8 of 128 (bf16)
+  constexpr int kCls = 8 / EPV;          // lanes of one class hold the same chains
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t c0 = ((int64_t)blockIdx.x * 4 + wave) * kSumsCPW;
   const u32x4* const x0 = (const u32x4*)((uintptr_t)x & ~(uintptr_t)15);  // a valid address for idle lanes
-  u32x4 r[kSumsCPW][2];
+  u32x4 r[kSumsCPW][NH];
   bool live[kSumsCPW];
   int delta[kSumsCPW], lim[kSumsCPW], f0[kSumsCPW];
 #pragma unroll
@@ -610,44 +617,47 @@ __global__ __launch_bounds__(256) void k_tn_sums_f32(const float* __restrict__ x
     const int64_t ci = c0 + j;
     live[j] = false;
     delta[j] = lim[j] = f0[j] = 0;
-    const u32x4* p0 = x0;
-    const u32x4* p1 = x0;
+    const u32x4* p[NH];
+#pragma unroll
+    for (int h = 0; h < NH; ++h) p[h] = x0;
     if (ci < nall) {
       const Tensor T = tensor_of(chunks, (int)ci, nall);
       if (lane == 0 && ci == T.first) tfirst[T.tensor] = (int)ci;
-      const ChunkGeo G = geo_of<ADFL_DTYPE_F32>(T, (int)ci, Split{1, T.n});
-      if (T.n > kShortMaxF32 && G.lim > 0) {
-        const View<ADFL_DTYPE_F32> v(x, T.base + G.c0e, G.lim);
+      const ChunkGeo G = geo_of<DT>(T, (int)ci, Split{1, T.n});
+      if (T.n > short_max<DT>() && G.lim > 0) {
+        const V v(x, T.base + G.c0e, G.lim);
         live[j] = true;
         delta[j] = v.delta;
         lim[j] = G.lim;
         f0[j] = 8 * (16 * (lane >> 3) + (int)((ci * 7) & 15)) + (lane & 7);
-        p0 = v.vb + (f0[j] < v.nvec ? f0[j] : v.nvec - 1);
-        p1 = v.vb + (f0[j] + 1024 < v.nvec ? f0[j] + 1024 : v.nvec - 1);
+#pragma unroll
+        for (int h = 0; h < NH; ++h) p[h] = v.vb + (f0[j] + 1024 * h < v.nvec ? f0[j] + 1024 * h : v.nvec - 1);
       }
     }
-    r[j][0] = ld_x(p0);
-    r[j][1] = ld_x(p1);
+#pragma unroll
+    for (int h = 0; h < NH; ++h) r[j][h] = ld_x(p[h]);
   }
 #pragma unroll
   for (int j = 0; j < kSumsCPW; ++j) {
     if (!live[j]) continue;  // uniform over the wave
-    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    double acc[EPV];
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int q = 0; q < EPV; ++q) acc[q] = 0.0;
 #pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        const int e = (f0[j] + 1024 * h) * 4 + p - delta[j];
-        const double d = (e >= 0 && e < lim[j]) ? (double)View<ADFL_DTYPE_F32>::elem(r[j][h], p) : 0.0;
-        acc[p] = __fma_rn(d, d, acc[p]);
+    for (int h = 0; h < NH; ++h)
+#pragma unroll
+      for (int q = 0; q < EPV; ++q) {
+        const int e = (f0[j] + 1024 * h) * EPV + q - delta[j];
+        const double d = (e >= 0 && e < lim[j]) ? (double)V::elem(r[j][h], q) : 0.0;
+        acc[q] = __fma_rn(d, d, acc[q]);
       }
 #pragma unroll
-    for (int p = 0; p < 4; ++p)
+    for (int q = 0; q < EPV; ++q)
 #pragma unroll
-      for (int o = 2; o < 64; o <<= 1) acc[p] += __shfl_xor(acc[p], o, 64);
-    if (lane < 2) {
+      for (int o = kCls; o < 64; o <<= 1) acc[q] += __shfl_xor(acc[q], o, 64);
+    if (lane < kCls) {
 #pragma unroll
-      for (int p = 0; p < 4; ++p) S[slot_of(c0 + j, ((lane * 4 + p - delta[j]) % 8 + 8) % 8, nall)] = acc[p] * 16.0;
+      for (int q = 0; q < EPV; ++q) S[slot_of(c0 + j, ((lane * EPV + q - delta[j]) % 8 + 8) % 8, nall)] = acc[q] * 16.0;
     }
   }
 }
@@ -719,10 +729,11 @@ __global__ __launch_bounds__(256) void k_tn_grids(const adfl_slq_chunk* __restri
 #pragma unroll
       for (int k = 0; k < kTPL; ++k) {
         const int64_t t = w0 + lane * kTPL + k;
-        // fp32's S is sampled: P is raised by a margin that covers the sample's error (a Gaussian tile's sampled
+        // fp32's and bf16's S is sampled: P is raised by a margin that covers the sample's error (a Gaussian tile's sampled
         // sum is within about 18% of its own, a prefix of t tiles within 18% / sqrt(t)); P may overshoot the
         // accumulator by up to 2x and still predict it (the maps are on g and g - 1), not undershoot it
-        const double Pm = DT == ADFL_DTYPE_F32 ? P * (1.0 + fmin(0.9, 1.0 / __builtin_sqrt((double)t + 1.0))) : P;
+        const double Pm = (DT == ADFL_DTYPE_F32 || DT == ADFL_DTYPE_BF16) ? P * (1.0 + fmin(0.9, 1.0 / __builtin_sqrt((double)t + 1.0)))
+                                                                          : P;
         if (t < nt) recs[tile_of<DT>(T, c, sp, t).slot] = make_rec<D::kWide>(0.0, 0.0, grid_pred<D::kWide>(Pm), 0u);
         P += y[k];
       }
@@ -1016,10 +1027,17 @@ __global__ __launch_bounds__(256) void k_tn_maps_exact(const void* __restrict__ 
   __shared__ double s_m[4][2][4];
   __shared__ int s_g[8];
   __shared__ uint32_t s_nf[8];
+  // bf16 (whose S is a sample that may miss a NaN): whether the chunk holds a NaN, double-buffered by iteration
+  // (set while staging, read after the barrier, the other buffer cleared for the next iteration)
+  __shared__ int s_anynan[2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr bool kNanScan = DT == ADFL_DTYPE_BF16;
+  if (kNanScan && tid == 0) s_anynan[0] = s_anynan[1] = 0;
+  if (kNanScan) __syncthreads();
   // exact_list NULL: every chunk of a long tensor (exact-square dtypes, whose ties are real and frequent: phase
   // C's order-free pass listed nearly every chunk anyway, so it is skipped)
   const int count = exact_list ? exact_list[-1] : (int)nall;
+  int it = 0;
   for (int li = blockIdx.x; li < count; li += gridDim.x) {
     const int ci = exact_list ? exact_list[li] : li;
     const Tensor T = tensor_of(chunks, ci, nall);
@@ -1051,7 +1069,11 @@ __global__ __launch_bounds__(256) void k_tn_maps_exact(const void* __restrict__ 
             row = D::NC == 8 ? c : c * 2 + s / kSeg;
             sl = s % kSeg;
           }
-          st[row * 64 * kLS + (sl / kLane) * kLS + sl % kLane] = V::elem(r[i], p);
+          const E el = V::elem(r[i], p);
+          if constexpr (kNanScan) {
+            if (el != el) s_anynan[it & 1] = 1;
+          }
+          st[row * 64 * kLS + (sl / kLane) * kLS + sl % kLane] = el;
         }
       }
     }
@@ -1142,8 +1164,11 @@ __global__ __launch_bounds__(256) void k_tn_maps_exact(const void* __restrict__ 
       if (g - 1 < Acc<W>::kGmin) a1 = Map{__builtin_inf(), __builtin_inf()};
       const int64_t slot = slot_of(ci, tid, T.nall);
       maps[slot] = make_double4(a0.e, a0.o, a1.e, a1.o);
-      recs[slot] = make_rec<W>(0.0, 0.0, g, kSide | s_nf[tid]);
+      const uint32_t nf = s_nf[tid] | ((kNanScan && s_anynan[it & 1]) ? kNaN : 0u);
+      recs[slot] = make_rec<W>(0.0, 0.0, g, kSide | nf);
     }
+    if (kNanScan && tid == 0) s_anynan[(it + 1) & 1] = 0;
+    ++it;
     __syncthreads();
   }
 }
@@ -2510,9 +2535,9 @@ int launch(const void* x, const adfl_slq_chunk* chunks, int64_t nchunks, const i
 #endif
   }
   if (any_long) {
-    if constexpr (DT == ADFL_DTYPE_F32)
-      k_tn_sums_f32<<<(unsigned)((nchunks + 4 * kSumsCPW - 1) / (4 * kSumsCPW)), 256, 0, st>>>((const float*)x, chunks, nchunks,
-                                                                                             s.tfirst, s.S);
+    if constexpr (DT == ADFL_DTYPE_F32 || DT == ADFL_DTYPE_BF16)  // a 1/16 sample (S only predicts binades)
+      k_tn_sums_sampled<DT><<<(unsigned)((nchunks + 4 * kSumsCPW - 1) / (4 * kSumsCPW)), 256, 0, st>>>(x, chunks, nchunks,
+                                                                                                     s.tfirst, s.S);
     else
       k_tn_sums<DT><<<(unsigned)nchunks, 256, 0, st>>>(x, chunks, nchunks, threads, s.tfirst, s.S);
     k_tn_winsums<DT><<<dim3((unsigned)ntensors, 8, 8), 256, 0, st>>>(chunks, nchunks, s.tfirst, threads, s.S, s.wsum);
