@@ -1090,7 +1090,7 @@ __global__ __launch_bounds__(256) void k_tn_maps_exact(const void* __restrict__ 
         w[i] = (!D::kContig || e < G.lim) ? st[row * 64 * kLS + lane * kLS + i] : (E)0;
       }
       if constexpr (D::kContig) {
-        for (int pc = 0; pc < 2; ++pc) {  // steps outside a piece are zeros (identity)
+        for (int pc = 0; pc < npieces; ++pc) {  // steps outside a piece are zeros (identity); one piece: one pass
           E z[kLane];
 #pragma unroll
           for (int i = 0; i < kLane; ++i) {
