@@ -2557,7 +2557,9 @@ int launch(const void* x, const adfl_slq_chunk* chunks, int64_t nchunks, const i
     }
     k_tn_windows<DT><<<dim3((unsigned)ntensors, 8, 8), 256, 0, st>>>(chunks, nchunks, s.tfirst, threads, s.recs, s.maps, s.wing,
                                                                      s.winmaps);
-    k_tn_chains<DT><<<dim3((unsigned)ntensors, 8), 64, 0, st>>>(x, chunks, nchunks, s.tfirst, 0, own_short, threads, s.S, s.recs,
+    // one wave per chain: 8 strided chains, or fp16's pieces (up to min(threads, 512) of them)
+    const unsigned cy = DT == ADFL_DTYPE_F16 ? (unsigned)(threads < 8 ? 8 : (threads > kMaxChains ? kMaxChains : threads)) : 8u;
+    k_tn_chains<DT><<<dim3((unsigned)ntensors, cy), 64, 0, st>>>(x, chunks, nchunks, s.tfirst, 0, own_short, threads, s.S, s.recs,
                                                                  s.maps, s.wing, s.winmaps, s.chain_acc);
     k_tn_finish<DT><<<(unsigned)ntensors, 64, 0, st>>>(x, chunks, nchunks, s.tfirst, 0, own_short, threads, s.chain_acc, n64,
                                                        n32);
