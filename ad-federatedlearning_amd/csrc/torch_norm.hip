@@ -27,7 +27,7 @@
 //
 // Phases (long tensors: more than kShortMax elements), one launch each, every block independent:
 //   A  k_tn_sums: per 8192-element chunk and chain (fp16: piece), the fp64 sum S of x^2 (one read of x;
-//      fp32 / bf16, k_tn_sums_sampled: of a 1/16 sample, weighted 16 — their phase C totals are exact, so S only
+//      fp32 / bf16 / fp16, k_tn_sums_sampled: of a 1/16 sample, weighted 16 — their phase C totals are exact, so S only
 //      predicts binades and flags nothing);
 //   B  k_tn_winsums + k_tn_grids: per window of 512 tiles the sum of S, then per tile the exclusive prefix P
 //      (earlier windows + a wave scan) predicts the binade of the accumulator at the tile's start:
@@ -599,10 +599,13 @@ __global__ __launch_bounds__(256) void k_tn_sums(const void* __restrict__ x, con
 constexpr int kSumsCPW = 4;
 // (bf16 — 2-byte elements, 8 to a vector, each vector one element of every chain — takes the same sample: 8 of
 // its chunk's 128 lines, lane l loading vector f0 only, and every lane holding all 8 chains)
+// (fp16: the same 8 lines; a lane's 8 elements are summed into the chunk's two pieces, split at the piece edge)
 template <int DT>
 __global__ __launch_bounds__(256) void k_tn_sums_sampled(const void* __restrict__ x, const adfl_slq_chunk* __restrict__ chunks,
-                                                         int64_t nall, int* __restrict__ tfirst, double* __restrict__ S) {
+                                                         int64_t nall, int threads, int* __restrict__ tfirst,
+                                                         double* __restrict__ S) {
   using V = View<DT>;
+  constexpr bool kC = Dt<DT>::kContig;
   constexpr int EPV = V::EPV;            // 4 (fp32) / 8 (bf16)
   constexpr int NH = EPV == 4 ? 2 : 1;   // vectors per lane: 16 sampled lines of 256 (fp32) / 8 of 128 (bf16)
   constexpr int kCls = 8 / EPV;          // lanes of one class hold the same chains
@@ -611,24 +614,26 @@ __global__ __launch_bounds__(256) void k_tn_sums_sampled(const void* __restrict_
   const u32x4* const x0 = (const u32x4*)((uintptr_t)x & ~(uintptr_t)15);  // a valid address for idle lanes
   u32x4 r[kSumsCPW][NH];
   bool live[kSumsCPW];
-  int delta[kSumsCPW], lim[kSumsCPW], f0[kSumsCPW];
+  int delta[kSumsCPW], lim[kSumsCPW], f0[kSumsCPW], bnd[kSumsCPW], len[kSumsCPW];
 #pragma unroll
   for (int j = 0; j < kSumsCPW; ++j) {
     const int64_t ci = c0 + j;
     live[j] = false;
-    delta[j] = lim[j] = f0[j] = 0;
+    delta[j] = lim[j] = f0[j] = bnd[j] = len[j] = 0;
     const u32x4* p[NH];
 #pragma unroll
     for (int h = 0; h < NH; ++h) p[h] = x0;
     if (ci < nall) {
       const Tensor T = tensor_of(chunks, (int)ci, nall);
       if (lane == 0 && ci == T.first) tfirst[T.tensor] = (int)ci;
-      const ChunkGeo G = geo_of<DT>(T, (int)ci, Split{1, T.n});
+      const ChunkGeo G = geo_of<DT>(T, (int)ci, kC ? split_of(T.n, threads) : Split{1, T.n});
       if (T.n > short_max<DT>() && G.lim > 0) {
         const V v(x, T.base + G.c0e, G.lim);
         live[j] = true;
         delta[j] = v.delta;
         lim[j] = G.lim;
+        bnd[j] = G.bnd;
+        len[j] = G.len;
         f0[j] = 8 * (16 * (lane >> 3) + (int)((ci * 7) & 15)) + (lane & 7);
 #pragma unroll
         for (int h = 0; h < NH; ++h) p[h] = v.vb + (f0[j] + 1024 * h < v.nvec ? f0[j] + 1024 * h : v.nvec - 1);
@@ -640,6 +645,26 @@ __global__ __launch_bounds__(256) void k_tn_sums_sampled(const void* __restrict_
 #pragma unroll
   for (int j = 0; j < kSumsCPW; ++j) {
     if (!live[j]) continue;  // uniform over the wave
+    if constexpr (kC) {  // fp16: two pieces at most, every lane holding both
+      double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+      for (int q = 0; q < EPV; ++q) {
+        const int e = f0[j] * EPV + q - delta[j];
+        const double d = (e >= 0 && e < lim[j]) ? (double)V::elem(r[j][0], q) : 0.0;
+        if (e < bnd[j]) a0 = __fma_rn(d, d, a0);
+        else a1 = __fma_rn(d, d, a1);
+      }
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        a0 += __shfl_xor(a0, o, 64);
+        a1 += __shfl_xor(a1, o, 64);
+      }
+      if (lane == 0) {
+        S[slot_of(c0 + j, 0, nall)] = a0 * 16.0;
+        if (bnd[j] < len[j]) S[slot_of(c0 + j, 1, nall)] = a1 * 16.0;
+      }
+      continue;
+    }
     double acc[EPV];
 #pragma unroll
     for (int q = 0; q < EPV; ++q) acc[q] = 0.0;
@@ -729,11 +754,10 @@ __global__ __launch_bounds__(256) void k_tn_grids(const adfl_slq_chunk* __restri
 #pragma unroll
       for (int k = 0; k < kTPL; ++k) {
         const int64_t t = w0 + lane * kTPL + k;
-        // fp32's and bf16's S is sampled: P is raised by a margin that covers the sample's error (a Gaussian tile's sampled
+        // fp32's, bf16's and fp16's S is sampled: P is raised by a margin that covers the sample's error (a Gaussian tile's sampled
         // sum is within about 18% of its own, a prefix of t tiles within 18% / sqrt(t)); P may overshoot the
         // accumulator by up to 2x and still predict it (the maps are on g and g - 1), not undershoot it
-        const double Pm = (DT == ADFL_DTYPE_F32 || DT == ADFL_DTYPE_BF16) ? P * (1.0 + fmin(0.9, 1.0 / __builtin_sqrt((double)t + 1.0)))
-                                                                          : P;
+        const double Pm = !D::kWide ? P * (1.0 + fmin(0.9, 1.0 / __builtin_sqrt((double)t + 1.0))) : P;
         if (t < nt) recs[tile_of<DT>(T, c, sp, t).slot] = make_rec<D::kWide>(0.0, 0.0, grid_pred<D::kWide>(Pm), 0u);
         P += y[k];
       }
@@ -1027,11 +1051,11 @@ __global__ __launch_bounds__(256) void k_tn_maps_exact(const void* __restrict__ 
   __shared__ double s_m[4][2][4];
   __shared__ int s_g[8];
   __shared__ uint32_t s_nf[8];
-  // bf16 (whose S is a sample that may miss a NaN): whether the chunk holds a NaN, double-buffered by iteration
+  // bf16 / fp16 (whose S is a sample that may miss a NaN): whether the chunk holds a NaN, double-buffered by iteration
   // (set while staging, read after the barrier, the other buffer cleared for the next iteration)
   __shared__ int s_anynan[2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  constexpr bool kNanScan = DT == ADFL_DTYPE_BF16;
+  constexpr bool kNanScan = DT == ADFL_DTYPE_BF16 || DT == ADFL_DTYPE_F16;
   if (kNanScan && tid == 0) s_anynan[0] = s_anynan[1] = 0;
   if (kNanScan) __syncthreads();
   // exact_list NULL: every chunk of a long tensor (exact-square dtypes, whose ties are real and frequent: phase
@@ -2535,9 +2559,9 @@ int launch(const void* x, const adfl_slq_chunk* chunks, int64_t nchunks, const i
 #endif
   }
   if (any_long) {
-    if constexpr (DT == ADFL_DTYPE_F32 || DT == ADFL_DTYPE_BF16)  // a 1/16 sample (S only predicts binades)
+    if constexpr (!Dt<DT>::kWide)  // fp32 / bf16 / fp16: a 1/16 sample (S only predicts binades)
       k_tn_sums_sampled<DT><<<(unsigned)((nchunks + 4 * kSumsCPW - 1) / (4 * kSumsCPW)), 256, 0, st>>>(x, chunks, nchunks,
-                                                                                                     s.tfirst, s.S);
+                                                                                                     threads, s.tfirst, s.S);
     else
       k_tn_sums<DT><<<(unsigned)nchunks, 256, 0, st>>>(x, chunks, nchunks, threads, s.tfirst, s.S);
     k_tn_winsums<DT><<<dim3((unsigned)ntensors, 8, 8), 256, 0, st>>>(chunks, nchunks, s.tfirst, threads, s.S, s.wsum);
