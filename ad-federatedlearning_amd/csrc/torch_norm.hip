@@ -1435,7 +1435,10 @@ __device__ float short_sq_round(const float (&v)[kSL], float acc, int G, int lan
   return lane_fma(w, rebuild<false>((double)(ls > 0 ? lane_f(out, ls - 1) : A), G), lane, ls);
 }
 
-constexpr int kSerial = 256 / ADFL_TN_SHORT_SL;  // lanes (256 steps) run in order at a chain's start (short_segment)
+#ifndef ADFL_TN_SERIAL_STEPS
+#define ADFL_TN_SERIAL_STEPS 256
+#endif
+constexpr int kSerial = ADFL_TN_SERIAL_STEPS / ADFL_TN_SHORT_SL;  // lanes (256 steps) run in order at a chain's start (short_segment)
 
 // One segment of a chain (lane l: steps 16 l .. 16 l + 15, in order) from the exact accumulator acc (wave-uniform).
 // SQ: exact-square inputs (fp16 / bf16), whose tie rounds take short_sq_round instead of the fp64 maps.
