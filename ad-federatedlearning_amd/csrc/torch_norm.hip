@@ -596,7 +596,10 @@ __global__ __launch_bounds__(256) void k_tn_sums(const void* __restrict__ x, con
 // kSumsCPW chunks per wave with every load issued first — a block per chunk issued 2 KB and waited (66 us on C2,
 // latency-bound); lane l loads vectors f0 = 8 (16 (l / 8) + rot) + l % 8 and f0 + 1024 (lines l / 8 and
 // l / 8 + 8 of the sample), so the lanes of one parity hold the same chains and no LDS or barrier is needed.
-constexpr int kSumsCPW = 4;
+#ifndef ADFL_TN_SUMS_CPW
+#define ADFL_TN_SUMS_CPW 2
+#endif
+constexpr int kSumsCPW = ADFL_TN_SUMS_CPW;  // chunks per wave in the sampled phase A
 // (bf16 — 2-byte elements, 8 to a vector, each vector one element of every chain — takes the same sample: 8 of
 // its chunk's 128 lines, lane l loading vector f0 only, and every lane holding all 8 chains)
 // (fp16: the same 8 lines; a lane's 8 elements are summed into the chunk's two pieces, split at the piece edge)
@@ -676,13 +679,26 @@ __global__ __launch_bounds__(256) void k_tn_sums_sampled(const void* __restrict_
         const double d = (e >= 0 && e < lim[j]) ? (double)V::elem(r[j][h], q) : 0.0;
         acc[q] = __fma_rn(d, d, acc[q]);
       }
+    // reduce-scatter over the lanes of a class: halve the values a lane holds at lane bits 5, 4 (, 3), then
+    // sum the one left over the remaining bits down to kCls — 10 (bf16) / 6 (fp32) shuffles instead of 48 / 20
+    int qb = 0;  // the first value index this lane still holds
 #pragma unroll
-    for (int q = 0; q < EPV; ++q)
+    for (int o = 32, n = EPV; n > 1; o >>= 1) {
+      n >>= 1;
+      const bool hi = (lane & o) != 0;
 #pragma unroll
-      for (int o = kCls; o < 64; o <<= 1) acc[q] += __shfl_xor(acc[q], o, 64);
-    if (lane < kCls) {
+      for (int i = 0; i < n; ++i) {
+        const double give = hi ? acc[i] : acc[i + n], keep = hi ? acc[i + n] : acc[i];
+        acc[i] = keep + __shfl_xor(give, o, 64);
+      }
+      if (hi) qb += n;
+    }
+    constexpr int kLow = 64 / EPV;  // lane bits below this: still to be summed (down to kCls)
 #pragma unroll
-      for (int q = 0; q < EPV; ++q) S[slot_of(c0 + j, ((lane * EPV + q - delta[j]) % 8 + 8) % 8, nall)] = acc[q] * 16.0;
+    for (int o = kLow / 2; o >= kCls; o >>= 1) acc[0] += __shfl_xor(acc[0], o, 64);
+    if ((lane & (kLow - 1)) < kCls) {  // one lane per (class, value)
+      const int cls = lane & (kCls - 1);
+      S[slot_of(c0 + j, ((cls * EPV + qb - delta[j]) % 8 + 8) % 8, nall)] = acc[0] * 16.0;
     }
   }
 }
