@@ -34,7 +34,8 @@
 //      g = binade(P (1 + 2^-8)) — a prediction only (a miss leaves the tile uncovered, resolved in D);
 //   C  k_tn_maps: per tile, its integer totals on g and g - 1, order-free (k = rint(hi), rint(2 hi)); a
 //      chunk whose squares may hide a tie is listed for k_tn_maps_exact, which stages it chain-major through
-//      LDS and composes each lane's 16 steps as (Ke, Ko) maps in order (second read of x);
+//      LDS and composes each lane's 16 steps as (Ke, Ko) maps in order (second read of x); fp32: k_tn_maps_f32
+//      (exact fp32 increments); bf16 / fp16, whose ties are real: every chunk straight to k_tn_maps_exact;
 //   C2 k_tn_windows: per window, the composition of its tiles' maps for the two binades it can start in;
 //   D  k_tn_chains: one wave per chain: windows 64 at a time on the exact accumulator's binade, the first one
 //      not covered tile by tile, the first tile not covered in segments of 1024 steps (lane sums or maps on
@@ -1052,7 +1053,8 @@ __global__ __launch_bounds__(256) void k_tn_maps_f32(const float* __restrict__ x
   if (tid == 0 && s_slow) exact_list[atomicAdd(exact_list - 1, 1)] = ci;  // the count sits just before the list
 }
 
-// The listed chunks, exactly: chain-major staging (16 steps per lane block, +1 pad), maps composed in order.
+// The listed chunks (bf16 / fp16: every long tensor's chunk), exactly: chain-major staging (16 steps per lane
+// block, +1 pad), maps composed in order.
 template <int DT>
 __global__ __launch_bounds__(256) void k_tn_maps_exact(const void* __restrict__ x, const adfl_slq_chunk* __restrict__ chunks, int64_t nall,
                                                        int threads, Rec* __restrict__ recs, double4* __restrict__ maps,
@@ -1521,7 +1523,8 @@ __device__ __forceinline__ float short_segment(const float (&v)[kSL], float acc,
 }
 
 // ---- phase D
-// A segment (<= 1024 steps, lane l holding steps 16 l .. 16 l + 15) run from the exact accumulator acc.
+// A segment (<= 1024 steps, lane l holding steps 16 l .. 16 l + 15) run from the exact accumulator acc
+// (fp64 accumulators; fp32 / bf16 / fp16 ones take short_segment, resolve_tile).
 // fp32 accumulators, no tie possible in the wave: each lane's steps add a constant on the binade G and one
 // on G + 1 — both summed in one pass and scanned together, so the usual segment (one crossing) costs one
 // round: the first lane that leaves G runs its steps with fma, and the lanes after it are checked on G + 1
