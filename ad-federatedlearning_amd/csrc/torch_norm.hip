@@ -1978,16 +1978,19 @@ __global__ __launch_bounds__(kShThreads) void k_tn_short(const float* __restrict
     f4v r[kShVec];
     f3v t;  // 3 dwords: a dead 4th component's register was reused at once, which waited for the load (WAW)
   };
-  const auto load = [&](Blk& k, int j) {
+  // part 0: every vector and the extra one; part 1 / 2: the first half / the rest
+  const auto load_part = [&](Blk& k, int j, int part) {
     const int64_t base = (int64_t)j * (kShSeg * 4), left = vbytes - base;
     const int bytes = left <= 0 ? 0 : (int)min(left, (int64_t)kShSeg * 4 + 16);
     const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xa) + (left <= 0 ? 0 : (int64_t)j * kShSeg), 0,
                                                       bytes, 0x00020000);
 #pragma unroll
     for (int i = 0; i < kShVec; ++i)
-      k.r[i] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, (i * kShThreads + tid) * 16, 0, 0));
-    k.t = __builtin_bit_cast(f3v, __builtin_amdgcn_raw_buffer_load_b96(rs, kShSeg * 4, 0, 0));
+      if (part == 0 || (part == 1) == (i < kShVec / 2))
+        k.r[i] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, (i * kShThreads + tid) * 16, 0, 0));
+    if (part != 1) k.t = __builtin_bit_cast(f3v, __builtin_amdgcn_raw_buffer_load_b96(rs, kShSeg * 4, 0, 0));
   };
+  const auto load = [&](Blk& k, int j) { load_part(k, j, 0); };
   // Thread tid's element p of vector i is e = kShSeg j + 2048 i + 4 tid + p - delta: chain e % 8, step e / 8 of
   // the segment (lane step / kSL, slot step % kSL); i adds 256 steps (256 / kSL lanes). Thread 0's first delta elements of
   // vector 0 belong to segment j - 1 (staged from its own extra vector): they go to a spare slot past the rows.
@@ -2095,15 +2098,21 @@ __global__ __launch_bounds__(kShThreads) void k_tn_short(const float* __restrict
   load(rb, 1);
   stage(ra, 0);
   sync();
+  // Each segment's loads in two halves: the first before the walk, the rest after the stage, so the CU's load
+  // queue holds at most half a segment more while a wave issues (a whole segment before the walk stalled the
+  // issue 0.5-1.4k cycles: queue full; all of it after the stage exposed the latency on long walks). Measured:
+  // kernel 17.3 -> 16.6 us on C3 equal, C3 log-uniform call 50.2 -> 49.2 us (profiles/r06/norm/split_load_ab/).
   for (int j = 0;; j += 2) {  // block-uniform control flow throughout
-    load(ra, j + 2);
+    load_part(ra, j + 2, 1);
     run(j);
     stage(rb, j + 1);  // after the walk: its loads have had the walk's time to land (past the end: zeros)
+    load_part(ra, j + 2, 2);
     sync();
     if (j + 1 >= nseg) break;
-    load(rb, j + 3);
+    load_part(rb, j + 3, 1);
     run(j + 1);
     stage(ra, j + 2);
+    load_part(rb, j + 3, 2);
     sync();
     if (j + 2 >= nseg) break;
   }
